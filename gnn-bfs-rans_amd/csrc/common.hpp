@@ -1,0 +1,86 @@
+// Shared helpers for the libmignn HIP sources (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/mignn.h"
+
+namespace mignn {
+
+// Thread-local description of the last failure (mignn_last_error()).
+void set_error(const char* fmt, ...);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Check the launch that was just enqueued.
+inline int launch_status(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: %s", what, hipGetErrorString(e));
+        return MIGNN_ERR_HIP;
+    }
+    return MIGNN_OK;
+}
+
+#define MIGNN_REQUIRE(cond, ...)                  \
+    do {                                          \
+        if (!(cond)) {                            \
+            ::mignn::set_error(__VA_ARGS__);      \
+            return MIGNN_ERR_ARG;                 \
+        }                                         \
+    } while (0)
+
+#define MIGNN_HIP(call)                                                        \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) {                                                \
+            ::mignn::set_error("%s: %s", #call, hipGetErrorString(e_));        \
+            return MIGNN_ERR_HIP;                                              \
+        }                                                                      \
+    } while (0)
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline unsigned grid_for(int64_t work, int block, int64_t cap = 1 << 20) {
+    int64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<unsigned>(g);
+}
+
+// f32 MFMA 16x16x4: lane l supplies A[i=l&15][k=l>>4], B[k=l>>4][j=l&15];
+// acc[r] = D[row=(l>>4)*4+r][col=l&15].  Exact fp32 (k-ordered fmaf chain).
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float4 fma4(float s, float4 x, float4 acc) {
+    acc.x = fmaf(s, x.x, acc.x);
+    acc.y = fmaf(s, x.y, acc.y);
+    acc.z = fmaf(s, x.z, acc.z);
+    acc.w = fmaf(s, x.w, acc.w);
+    return acc;
+}
+
+// Reference epilogue order (gnn_model.py:184-191 with the conv bias first):
+//   v = acc + bias; v = residual + v; v = v*scale + shift; relu.
+__device__ __forceinline__ float epilogue(float acc, int flags, float bias, float res, float sc,
+                                          float sh) {
+    float v = acc;
+    if (flags & MIGNN_EPI_BIAS) v = v + bias;
+    if (flags & MIGNN_EPI_RESIDUAL) v = res + v;
+    if (flags & MIGNN_EPI_AFFINE) v = v * sc + sh;
+    if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;  // NaN-propagating, like torch.relu
+    return v;
+}
+
+}  // namespace mignn

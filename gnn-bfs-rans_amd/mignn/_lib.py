@@ -1,0 +1,94 @@
+"""ctypes binding of libmignn.so (the C ABI declared in include/mignn.h).
+
+The library is loaded lazily on first use and the product path fails loudly
+when it is missing: there is no CPU or eager-PyTorch fallback.  `torch` is
+imported first on purpose -- it brings in its HIP runtime
+(libamdhip64.so.7), which the dynamic loader then shares with libmignn.so, so
+torch's streams and device pointers are valid inside the library.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_int64, c_size_t, c_void_p
+
+import torch  # noqa: F401  (must precede loading libmignn.so)
+
+LIB_NAME = "libmignn.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+EPI_BIAS, EPI_RESIDUAL, EPI_AFFINE, EPI_RELU = 1, 2, 4, 8
+CSR_VERBATIM, CSR_ONE_SELF_LOOP = 0, 1
+
+_P = c_void_p
+# name -> (restype, argtypes); mirrors include/mignn.h
+SIGNATURES = {
+    "mignn_abi_version": (c_int, []),
+    "mignn_last_error": (ctypes.c_char_p, []),
+    "mignn_csr_scratch_bytes": (c_size_t, [c_int64, c_int64]),
+    "mignn_csr_build": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_size_t, _P]),
+    "mignn_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P, _P,
+                             c_int64, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_input_proj": (c_int, [_P, c_int64, c_int, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_bn_fold": (c_int, [_P, _P, _P, _P, c_float, c_int, _P, _P, _P]),
+    "mignn_gcn_aggregate": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
+                                    c_int64, _P]),
+    "mignn_sum_aggregate": (c_int, [_P, _P, _P, c_int64, c_float, c_int64, c_int64, c_int, _P,
+                                    c_int64, _P]),
+    "mignn_gat_aggregate": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, c_int,
+                                    c_float, _P, c_int64, _P]),
+    "mignn_transformer_aggregate": (c_int, [_P, _P, _P, c_int64, _P, c_int64, c_int64, c_int64,
+                                            c_int, c_int, c_float, _P, c_int64, _P]),
+    "mignn_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P, _P,
+                                c_int, _P, c_int64, _P]),
+    "mignn_rows_gather": (c_int, [_P, c_int64, _P, c_int64, c_int, _P, c_int64, _P]),
+    "mignn_grid_graph": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, _P, _P]),
+}
+
+_lib = None
+
+
+class MignnError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise if the .so is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MignnError(
+                f"{LIB_NAME} not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+                "There is no CPU fallback.")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        if h.mignn_abi_version() != 1:
+            raise MignnError("libmignn ABI mismatch")
+        _lib = h
+    return _lib
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def last_error() -> str:
+    msg = lib().mignn_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise MignnError(f"{what} failed (status {rc}): {last_error()}")

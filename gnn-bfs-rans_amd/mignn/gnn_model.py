@@ -1,0 +1,505 @@
+"""FlowGNN on MI355X: the reference's model API, executed by libmignn.so.
+
+Drop-in for `gnn_model.FlowGNN` (reference gnn_model.py:14-220) and
+`FlowGNNSurrogate` (:223-291):
+
+* same constructor arguments, `forward(x, edge_index, edge_attr=None,
+  batch=None) -> [N, output_dim]`, `predict_fields`, and the same
+  `state_dict` keys as the PyG-built reference model, so a
+  reference checkpoint's `model_state_dict` loads with `load_state_dict`
+  (PyG 2.3/2.4 `lin_src/lin_dst` and 2.5+ `lin` GAT layouts both accepted);
+* same errors: `ValueError("Unknown layer type ...")`, `ValueError` on a bad
+  edge_index shape / edge_attr count, and any failure inside a layer becomes
+  `RuntimeError("Message passing failed in layer i (type): ...")` with the
+  reference's diagnostic lines (gnn_model.py:173-181); invalid indices are
+  dropped silently (:133-141), on the device, without host syncs.
+
+Every arithmetic step of `forward` runs in the HIP library (CSR build,
+aggregation, MFMA transforms, fused epilogues); PyTorch only allocates device
+memory and provides the stream.  There is no CPU path: tensors must be on a
+ROCm device and the library must be built.  Eval mode only (training /
+backward is SURVEY.md §8f-3, not built yet).
+
+Weight re-association (one-time per weight version, float64 on the device):
+* GAT: logits a_src = x . (W_h^T att_src_h) -> an [N, 2*heads] GEMV-GEMM;
+  out = mean_h (sum_j alpha x_j) W_h^T -> one [N, heads*H] x [heads*H, H] GEMM.
+* TransformerConv: q~_h = Wk_h^T q_h, so q_h . k_j = q~_h . x_j + q_h . bk_h;
+  value / skip projections are applied after aggregation by one GEMM.
+  The [N, heads*C] Q/K/V tensors of the reference are never materialised.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import CSR_ONE_SELF_LOOP, CSR_VERBATIM, EPI_AFFINE, EPI_BIAS, EPI_RELU, EPI_RESIDUAL
+
+HEADS = 4  # gnn_model.py:67, :79
+
+
+# ---------------------------------------------------------------------------
+# PyG-named parameter containers (state_dict layout of the reference model)
+# ---------------------------------------------------------------------------
+
+class GCNConv(nn.Module):
+    """Parameters of PyG GCNConv(H, H): `lin.weight` [H,H] (no bias), `bias` [H]."""
+
+    def __init__(self, in_channels: int, out_channels: int):
+        super().__init__()
+        self.lin = nn.Linear(in_channels, out_channels, bias=False)
+        self.bias = nn.Parameter(torch.zeros(out_channels))
+
+
+class GATConv(nn.Module):
+    """Parameters of PyG GATConv(H, H, heads=4, concat=False)."""
+
+    def __init__(self, in_channels: int, out_channels: int, heads: int = HEADS,
+                 concat: bool = False, dropout: float = 0.0, negative_slope: float = 0.2):
+        super().__init__()
+        self.heads, self.out_channels = heads, out_channels
+        self.dropout, self.negative_slope = dropout, negative_slope
+        self.lin = nn.Linear(in_channels, heads * out_channels, bias=False)
+        self.att_src = nn.Parameter(torch.zeros(1, heads, out_channels))
+        self.att_dst = nn.Parameter(torch.zeros(1, heads, out_channels))
+        self.bias = nn.Parameter(torch.zeros(out_channels))
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        # PyG 2.3/2.4 registered the shared projection as lin_src (== lin_dst).
+        src, dst, new = prefix + "lin_src.weight", prefix + "lin_dst.weight", prefix + "lin.weight"
+        if src in state_dict and new not in state_dict:
+            state_dict[new] = state_dict.pop(src)
+            state_dict.pop(dst, None)
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+
+class GINConv(nn.Module):
+    """Parameters of PyG GINConv(nn=Seq(Lin, ReLU, Lin), eps=0, train_eps=False)."""
+
+    def __init__(self, nn_module: nn.Module, eps: float = 0.0):
+        super().__init__()
+        self.nn = nn_module
+        self.register_buffer("eps", torch.tensor([float(eps)]))
+
+
+class TransformerConv(nn.Module):
+    """Parameters of PyG TransformerConv(H, H, heads=4, concat=False)."""
+
+    def __init__(self, in_channels: int, out_channels: int, heads: int = HEADS,
+                 concat: bool = False, dropout: float = 0.0):
+        super().__init__()
+        self.heads, self.out_channels, self.dropout = heads, out_channels, dropout
+        self.lin_key = nn.Linear(in_channels, heads * out_channels)
+        self.lin_query = nn.Linear(in_channels, heads * out_channels)
+        self.lin_value = nn.Linear(in_channels, heads * out_channels)
+        self.lin_skip = nn.Linear(in_channels, out_channels)
+
+
+class BatchNorm(nn.Module):
+    """PyG BatchNorm: `module` = BatchNorm1d(H, eps=1e-5, momentum=0.1)."""
+
+    def __init__(self, in_channels: int, eps: float = 1e-5, momentum: float = 0.1):
+        super().__init__()
+        self.module = nn.BatchNorm1d(in_channels, eps=eps, momentum=momentum)
+
+
+# ---------------------------------------------------------------------------
+# Graph structure cache
+# ---------------------------------------------------------------------------
+
+class Csr:
+    __slots__ = ("row_ptr", "col", "dinv", "info", "num_nodes", "num_edges", "edge_index")
+
+    def __init__(self, row_ptr, col, dinv, info, num_nodes, num_edges, edge_index):
+        self.row_ptr, self.col, self.dinv, self.info = row_ptr, col, dinv, info
+        self.num_nodes, self.num_edges, self.edge_index = num_nodes, num_edges, edge_index
+
+
+def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
+    """Destination-major CSR on the device (mignn_csr_build); no host sync."""
+    dev = edge_index.device
+    ei = edge_index
+    if ei.dtype != torch.int64 or not ei.is_contiguous():
+        ei = ei.to(torch.int64).contiguous()
+    E = int(ei.shape[1])
+    N = int(num_nodes)
+    row_ptr = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(max(E + N, 1), dtype=torch.int32, device=dev)
+    dinv = torch.empty(max(N, 1), dtype=torch.float32, device=dev) if mode == CSR_ONE_SELF_LOOP else None
+    info = torch.zeros(4, dtype=torch.int64, device=dev)
+    L = _lib.lib()
+    nbytes = L.mignn_csr_scratch_bytes(E, N)
+    if nbytes == 0:
+        raise _lib.MignnError("csr scratch query failed: " + _lib.last_error())
+    scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    _lib.check(L.mignn_csr_build(_lib.ptr(ei), E, N, mode, _lib.ptr(row_ptr), _lib.ptr(col),
+                                 _lib.ptr(dinv), _lib.ptr(info), _lib.ptr(scratch), nbytes,
+                                 _lib.stream(dev)), "mignn_csr_build")
+    return Csr(row_ptr, col, dinv, info, N, E, ei)
+
+
+class _CsrCache:
+    """Keyed by (edge_index storage, version, shape, N, mode, device); holds a
+    reference to the edge_index so its storage cannot be recycled while cached."""
+
+    def __init__(self, capacity: int = 4):
+        self.capacity = capacity
+        self.entries: Dict[Tuple, Csr] = {}
+
+    def get(self, edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
+        key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
+               tuple(edge_index.stride()), edge_index.dtype, int(num_nodes), mode,
+               str(edge_index.device))
+        hit = self.entries.get(key)
+        if hit is not None:
+            return hit
+        csr = build_csr(edge_index, num_nodes, mode)
+        if len(self.entries) >= self.capacity:
+            self.entries.pop(next(iter(self.entries)))
+        self.entries[key] = csr
+        return csr
+
+
+# ---------------------------------------------------------------------------
+# Native op wrappers
+# ---------------------------------------------------------------------------
+
+def _stream(t: torch.Tensor) -> int:
+    return _lib.stream(t.device)
+
+
+def linear(a: torch.Tensor, w: torch.Tensor, bias=None, *, relu=False, residual=None,
+           scale=None, shift=None, a2: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = epi([a | a2] @ w.T) on MFMA (mignn_linear)."""
+    M, K1 = a.shape
+    K2 = 0 if a2 is None else a2.shape[1]
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    flags = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) \
+        | (EPI_AFFINE if scale is not None else 0) | (EPI_RELU if relu else 0)
+    _lib.check(_lib.lib().mignn_linear(
+        _lib.ptr(a), a.stride(0), M, K1, _lib.ptr(a2), 0 if a2 is None else a2.stride(0), K2,
+        _lib.ptr(w), N, _lib.ptr(bias), _lib.ptr(residual),
+        0 if residual is None else residual.stride(0), _lib.ptr(scale), _lib.ptr(shift), flags,
+        _lib.ptr(out), out.stride(0), _stream(a)), "mignn_linear")
+    return out
+
+
+def bn_fold(bn: nn.BatchNorm1d) -> Tuple[torch.Tensor, torch.Tensor]:
+    h = bn.num_features
+    dev = bn.running_mean.device
+    scale = torch.empty(h, dtype=torch.float32, device=dev)
+    shift = torch.empty(h, dtype=torch.float32, device=dev)
+    _lib.check(_lib.lib().mignn_bn_fold(
+        _lib.ptr(bn.weight), _lib.ptr(bn.bias), _lib.ptr(bn.running_mean),
+        _lib.ptr(bn.running_var), float(bn.eps), h, _lib.ptr(scale), _lib.ptr(shift),
+        _lib.stream(dev)), "mignn_bn_fold")
+    return scale, shift
+
+
+def _value_plus_edge_attr_check(a, b):
+    """Shape semantics of `value_j + edge_attr` in PyG TransformerConv.message
+    (ATen infer_size, same message text)."""
+    ndim = max(len(a), len(b))
+    for i in range(ndim - 1, -1, -1):
+        off = ndim - 1 - i
+        da = a[len(a) - 1 - off] if off < len(a) else 1
+        db = b[len(b) - 1 - off] if off < len(b) else 1
+        if da != db and da != 1 and db != 1:
+            raise RuntimeError(f"The size of tensor a ({da}) must match the size of tensor b "
+                               f"({db}) at non-singleton dimension {i}")
+    raise NotImplementedError("TransformerConv with a broadcastable edge_attr (edge_dim=None) "
+                              "is not supported")
+
+
+def _versions(*ts) -> Tuple:
+    return tuple((t.data_ptr(), t._version) for t in ts)
+
+
+# ---------------------------------------------------------------------------
+# FlowGNN
+# ---------------------------------------------------------------------------
+
+class FlowGNN(nn.Module):
+    """MI355X-native FlowGNN (reference gnn_model.py:14-220)."""
+
+    def __init__(self, input_dim: int = 3, hidden_dim: int = 128, output_dim: int = 8,
+                 num_layers: int = 4, layer_type: str = "GCN", use_edge_attr: bool = True,
+                 dropout: float = 0.1, use_batch_norm: bool = True):
+        super().__init__()
+        self.input_dim = input_dim
+        self.hidden_dim = hidden_dim
+        self.output_dim = output_dim
+        self.num_layers = num_layers
+        self.layer_type = layer_type
+        self.use_edge_attr = use_edge_attr
+        self.use_batch_norm = use_batch_norm
+        self.input_proj = nn.Linear(input_dim, hidden_dim)
+        self.gnn_layers = nn.ModuleList()
+        self.batch_norms = nn.ModuleList() if use_batch_norm else None
+        for _ in range(num_layers):
+            if layer_type == "GCN":
+                layer = GCNConv(hidden_dim, hidden_dim)
+            elif layer_type == "GAT":
+                layer = GATConv(hidden_dim, hidden_dim, heads=HEADS, concat=False, dropout=dropout)
+            elif layer_type == "GIN":
+                layer = GINConv(nn.Sequential(nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
+                                              nn.Linear(hidden_dim, hidden_dim)))
+            elif layer_type == "Transformer":
+                layer = TransformerConv(hidden_dim, hidden_dim, heads=HEADS, concat=False,
+                                        dropout=dropout)
+            else:
+                raise ValueError(f"Unknown layer type: {layer_type}")
+            self.gnn_layers.append(layer)
+            if use_batch_norm:
+                self.batch_norms.append(BatchNorm(hidden_dim))
+        self.output_proj = nn.Sequential(
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
+            nn.Linear(hidden_dim, hidden_dim // 2), nn.ReLU(),
+            nn.Linear(hidden_dim // 2, output_dim))
+        self.dropout = nn.Dropout(dropout)
+        self._csr = _CsrCache()
+        self._prep: Dict[Tuple, object] = {}
+
+    # ------------------------------------------------------------------ API
+    def predict_fields(self, output: torch.Tensor) -> dict:
+        """gnn_model.py:199-220."""
+        fields = {"U": output[:, :3], "p": output[:, 3:4], "k": output[:, 4:5],
+                  "epsilon": output[:, 5:6], "nut": output[:, 6:7]}
+        if output.shape[1] > 7:
+            fields["residual"] = output[:, 7:8]
+        return fields
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor,
+                edge_attr: Optional[torch.Tensor] = None,
+                batch: Optional[torch.Tensor] = None) -> torch.Tensor:
+        num_nodes = x.shape[0]
+        # gnn_model.py:126-127
+        if edge_index.dim() != 2 or edge_index.shape[0] != 2:
+            raise ValueError(f"edge_index must have shape [2, num_edges], got {edge_index.shape}")
+        self._check_runtime(x, edge_index)
+        E = edge_index.shape[1]
+        # gnn_model.py:152-156 (shape-only: invalid-edge filtering keeps counts aligned)
+        if edge_attr is not None and E > 0 and edge_attr.shape[0] != E:
+            raise ValueError(f"edge_attr must have {E} entries, got {edge_attr.shape[0]}")
+        H = self.hidden_dim
+        out = torch.empty((num_nodes, self.output_dim), dtype=torch.float32, device=x.device)
+        if num_nodes == 0:
+            return out
+        xin = x.contiguous().float() if (x.dtype != torch.float32 or not x.is_contiguous()) else x
+        buf_a = torch.empty((num_nodes, H), dtype=torch.float32, device=x.device)
+        buf_b = torch.empty_like(buf_a)
+        # input_proj (gnn_model.py:159)
+        self._input_proj(xin, buf_a)
+        mode = CSR_ONE_SELF_LOOP if self.layer_type in ("GCN", "GAT") else CSR_VERBATIM
+        csr = self._csr.get(edge_index, num_nodes, mode)
+        cur, nxt = buf_a, buf_b
+        for i, layer in enumerate(self.gnn_layers):
+            try:
+                if self.layer_type == "Transformer" and edge_attr is not None:
+                    # PyG TransformerConv.message adds a non-None edge_attr to value_j
+                    # ([E, heads, C] + [E, d]); reproduce the resulting torch error.
+                    _value_plus_edge_attr_check((E, HEADS, H), tuple(edge_attr.shape))
+                self._layer(i, layer, csr, cur, nxt, 0, num_nodes)
+            except RuntimeError as e:
+                raise self._layer_error(i, e, num_nodes, edge_index, cur, edge_attr) from e
+            cur, nxt = nxt, cur
+        self._output_mlp(cur, nxt, out)
+        return out
+
+    # ------------------------------------------------------------- internals
+    def _check_runtime(self, x, edge_index):
+        if self.training:
+            raise NotImplementedError(
+                "mignn FlowGNN implements the eval-mode forward (inference.py / visualize.py / "
+                "validate paths); call .eval().  Training-mode BN/dropout and backward are "
+                "SURVEY.md §8f-3 (next).")
+        if x.device.type != "cuda" or edge_index.device.type != "cuda":
+            raise RuntimeError(
+                "mignn FlowGNN runs on ROCm devices only (no CPU path): move the model and the "
+                "graph to 'cuda' (HIP).")
+        if self.input_proj.weight.device != x.device:
+            raise RuntimeError(f"model is on {self.input_proj.weight.device}, input on {x.device}")
+        for p in self.parameters():
+            if p.dtype != torch.float32:
+                raise RuntimeError("mignn FlowGNN computes in fp32; parameters must be float32")
+        if self.hidden_dim % 8 != 0:
+            raise RuntimeError("mignn FlowGNN requires hidden_dim % 8 == 0")
+
+    def _layer_error(self, i, e, num_nodes, edge_index, x, edge_attr):
+        E = edge_index.shape[1]
+        if E > 0:
+            rng = f"[{edge_index.min().item()}, {edge_index.max().item()}]"
+        else:
+            rng = "[N/A, N/A]"
+        return RuntimeError(
+            f"Message passing failed in layer {i} ({self.layer_type}): {str(e)}\n"
+            f"  num_nodes: {num_nodes}, num_edges: {E if E > 0 else 0}\n"
+            f"  edge_index range: {rng}\n"
+            f"  x shape: {x.shape}, edge_attr shape: "
+            f"{edge_attr.shape if edge_attr is not None else 'None'}")
+
+    def _input_proj(self, x, out):
+        w, b = self.input_proj.weight, self.input_proj.bias
+        if self.input_dim <= 8:
+            _lib.check(_lib.lib().mignn_input_proj(
+                _lib.ptr(x), x.shape[0], self.input_dim, _lib.ptr(w), _lib.ptr(b),
+                self.hidden_dim, _lib.ptr(out), out.stride(0), _stream(x)), "mignn_input_proj")
+        else:
+            linear(x, w, b, out=out)
+
+    def _bn(self, i):
+        if not self.use_batch_norm:
+            return None, None
+        bn = self.batch_norms[i].module
+        key = ("bn", i) + _versions(bn.weight, bn.bias, bn.running_mean, bn.running_var)
+        hit = self._prep.get(key)
+        if hit is None:
+            self._prep = {k: v for k, v in self._prep.items() if k[:2] != ("bn", i)}
+            hit = self._prep[key] = bn_fold(bn)
+        return hit
+
+    def _cached(self, tag, i, tensors, make):
+        key = (tag, i) + _versions(*tensors)
+        hit = self._prep.get(key)
+        if hit is None:
+            self._prep = {k: v for k, v in self._prep.items() if k[:2] != (tag, i)}
+            with torch.no_grad():
+                hit = self._prep[key] = make()
+        return hit
+
+    def _layer(self, i, layer, csr: Csr, x, out, rb: int, re: int, ldx_rows=None):
+        """One conv + residual + BN + ReLU (gnn_model.py:162-192) for rows [rb, re).
+        `x` holds every row the CSR references (own rows + halo rows)."""
+        H = self.hidden_dim
+        L = _lib.lib()
+        st = _stream(x)
+        scale, shift = self._bn(i)
+        epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
+        P = _lib.ptr
+        n = re - rb
+        if n <= 0:
+            return
+        if self.layer_type == "GCN":
+            w, b = layer.lin.weight, layer.bias
+            if H in (64, 128):
+                _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.dinv), P(x),
+                                             x.stride(0), rb, re, H, P(w), P(b), P(scale),
+                                             P(shift), epi, P(out), out.stride(0), st),
+                           "mignn_gcn_layer")
+            else:
+                agg = torch.empty((n, H), dtype=torch.float32, device=x.device)
+                _lib.check(L.mignn_gcn_aggregate(P(csr.row_ptr), P(csr.col), P(csr.dinv), P(x),
+                                                 x.stride(0), rb, re, H,
+                                                 P(agg) - rb * agg.stride(0) * 4, agg.stride(0),
+                                                 st), "mignn_gcn_aggregate")
+                linear(agg, w, b, relu=True, residual=x[rb:re], scale=scale, shift=shift,
+                       out=out[rb:re])
+        elif self.layer_type == "GIN":
+            nn0, nn2 = layer.nn[0], layer.nn[2]
+            eps = self._cached("eps", i, (layer.eps,), lambda: float(layer.eps.reshape(-1)[0]))
+            agg = torch.empty((n, H), dtype=torch.float32, device=x.device)
+            _lib.check(L.mignn_sum_aggregate(P(csr.row_ptr), P(csr.col), P(x), x.stride(0),
+                                             1.0 + eps, rb, re, H,
+                                             P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st),
+                       "mignn_sum_aggregate")
+            h1 = linear(agg, nn0.weight, nn0.bias, relu=True)
+            linear(h1, nn2.weight, nn2.bias, relu=True, residual=x[rb:re], scale=scale,
+                   shift=shift, out=out[rb:re])
+        elif self.layer_type == "GAT":
+            wlog, wcat = self._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
+                                      lambda: self._gat_weights(layer))
+            logits = linear(x, wlog)                                   # [rows, 2*heads]
+            agg = torch.empty((n, HEADS * H), dtype=torch.float32, device=x.device)
+            _lib.check(L.mignn_gat_aggregate(P(csr.row_ptr), P(csr.col), P(logits), P(x),
+                                             x.stride(0), rb, re, H, HEADS,
+                                             float(layer.negative_slope),
+                                             P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st),
+                       "mignn_gat_aggregate")
+            linear(agg, wcat, layer.bias, relu=True, residual=x[rb:re], scale=scale, shift=shift,
+                   out=out[rb:re])
+        elif self.layer_type == "Transformer":
+            ts = (layer.lin_query.weight, layer.lin_query.bias, layer.lin_key.weight,
+                  layer.lin_key.bias, layer.lin_value.weight, layer.lin_value.bias,
+                  layer.lin_skip.weight, layer.lin_skip.bias)
+            wqk, bqk, wout, bout = self._cached("tf", i, ts, lambda: self._tf_weights(layer))
+            K1 = HEADS * H + HEADS
+            qt = torch.empty((n, K1), dtype=torch.float32, device=x.device)
+            linear(x[rb:re], wqk, bqk, out=qt)
+            agg = torch.empty((n, K1), dtype=torch.float32, device=x.device)
+            _lib.check(L.mignn_transformer_aggregate(
+                P(csr.row_ptr), P(csr.col), P(qt) - rb * qt.stride(0) * 4, qt.stride(0), P(x),
+                x.stride(0), rb, re, H, HEADS, 1.0 / math.sqrt(H),
+                P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st), "mignn_transformer_aggregate")
+            linear(agg, wout, bout, a2=x[rb:re], relu=True, residual=x[rb:re], scale=scale,
+                   shift=shift, out=out[rb:re])
+        else:
+            raise ValueError(f"Unknown layer type: {self.layer_type}")
+
+    @staticmethod
+    def _gat_weights(layer: GATConv):
+        heads, C = layer.heads, layer.out_channels
+        W = layer.lin.weight.double().view(heads, C, -1)              # [h, c, k]
+        vs = torch.einsum("hck,hc->hk", W, layer.att_src.double().view(heads, C))
+        vd = torch.einsum("hck,hc->hk", W, layer.att_dst.double().view(heads, C))
+        wlog = torch.cat([vs, vd], 0).float().contiguous()            # [2*heads, H]
+        wcat = (W.permute(1, 0, 2).reshape(C, heads * W.shape[2]) / heads).float().contiguous()
+        return wlog, wcat
+
+    @staticmethod
+    def _tf_weights(layer: TransformerConv):
+        heads, C = layer.heads, layer.out_channels
+        d = lambda t: t.detach().double()  # noqa: E731
+        Wq = d(layer.lin_query.weight).view(heads, C, -1)   # [h, c, k]
+        Wk = d(layer.lin_key.weight).view(heads, C, -1)
+        Wv = d(layer.lin_value.weight).view(heads, C, -1)
+        bq = d(layer.lin_query.bias).view(heads, C)
+        bk = d(layer.lin_key.bias).view(heads, C)
+        bv = d(layer.lin_value.bias).view(heads, C)
+        Hin = Wq.shape[2]
+        M = torch.einsum("hck,hcq->hkq", Wk, Wq).reshape(heads * Hin, Hin)   # rows h*H+kk
+        mb = torch.einsum("hck,hc->hk", Wk, bq).reshape(heads * Hin)
+        wc = torch.einsum("hcq,hc->hq", Wq, bk)                               # [h, H]
+        cc = (bq * bk).sum(1)                                                 # [h]
+        wqk = torch.cat([M, wc], 0).float().contiguous()                      # [h*H + h, H]
+        bqk = torch.cat([mb, cc], 0).float().contiguous()
+        wv = Wv.permute(1, 0, 2).reshape(C, heads * Hin) / heads             # [C, h*H]
+        wbv = bv.t() / heads                                                  # [C, h]
+        wout = torch.cat([wv, wbv, d(layer.lin_skip.weight)], 1).float().contiguous()
+        bout = layer.lin_skip.bias.detach().float().contiguous()
+        return wqk, bqk, wout, bout
+
+    def _output_mlp(self, x, tmp, out):
+        """output_proj (gnn_model.py:90-100, :195): Lin-ReLU-Lin-ReLU-Lin-ReLU-Lin."""
+        l0, l3, l6, l8 = (self.output_proj[i] for i in (0, 3, 6, 8))
+        h1 = linear(x, l0.weight, l0.bias, relu=True, out=tmp)
+        h2 = linear(h1, l3.weight, l3.bias, relu=True, out=x)
+        h3 = linear(h2, l6.weight, l6.bias, relu=True)
+        linear(h3, l8.weight, l8.bias, out=out)
+
+
+class FlowGNNSurrogate(nn.Module):
+    """Encoder/decoder composition of FlowGNN (reference gnn_model.py:223-291)."""
+
+    def __init__(self, input_dim: int = 3, hidden_dim: int = 128, num_layers: int = 4,
+                 layer_type: str = "GCN", use_edge_attr: bool = True, dropout: float = 0.1):
+        super().__init__()
+        self.encoder = FlowGNN(input_dim=input_dim, hidden_dim=hidden_dim, output_dim=hidden_dim,
+                               num_layers=num_layers // 2, layer_type=layer_type,
+                               use_edge_attr=use_edge_attr, dropout=dropout)
+        self.decoder = FlowGNN(input_dim=hidden_dim, hidden_dim=hidden_dim, output_dim=8,
+                               num_layers=num_layers // 2, layer_type=layer_type,
+                               use_edge_attr=use_edge_attr, dropout=dropout)
+
+    def forward(self, x, edge_index, edge_attr=None, boundary_conditions=None):
+        encoded = self.encoder(x, edge_index, edge_attr)
+        if boundary_conditions is not None:
+            encoded = encoded + boundary_conditions
+        return self.decoder(encoded, edge_index, edge_attr)

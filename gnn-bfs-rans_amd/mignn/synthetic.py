@@ -1,0 +1,84 @@
+"""Synthetic inputs for parity tests and the benchmark.
+
+* `seeded_state_dict` re-draws every FlowGNN parameter from a seeded CPU
+  generator, so a given (architecture, seed) pair yields bit-identical weights
+  on any machine.
+* `grid_graph` builds the 3-D periodic hex grid (6-neighbour, E = 6N, no
+  self-loops) directly on the GPU with the native generator
+  (`mignn_grid_graph`, csrc/graph_build.hip).  Node order is natural
+  lexicographic (i fastest); an optional seeded permutation gives the
+  locality stress case.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+
+def seeded_state_dict(template: Dict[str, torch.Tensor], seed: int = 0) -> Dict[str, torch.Tensor]:
+    """Return a new state_dict with the same keys/shapes as `template`.
+
+    Linear weights/biases and attention vectors ~ U(-0.1, 0.1); BatchNorm
+    weight ~ U(0.5, 1.5), bias ~ U(-0.1, 0.1), running_mean ~ N(0, 0.1^2),
+    running_var ~ U(0.5, 1.5); GIN `eps` and `num_batches_tracked` are kept.
+    """
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    for k, t in template.items():
+        shape, dtype = t.shape, t.dtype
+        if k.endswith("num_batches_tracked") or k.endswith(".eps"):
+            out[k] = t.detach().cpu().clone()
+            continue
+        if k.endswith("running_mean"):
+            v = torch.randn(shape, generator=g) * 0.1
+        elif k.endswith("running_var"):
+            v = torch.rand(shape, generator=g) + 0.5
+        elif ".module.weight" in k and k.startswith("batch_norms"):
+            v = torch.rand(shape, generator=g) + 0.5
+        else:
+            v = (torch.rand(shape, generator=g) * 2 - 1) * 0.1
+        out[k] = v.to(dtype)
+    return out
+
+
+def grid_dims(num_nodes: int) -> Tuple[int, int, int]:
+    """Named synthetic sizes."""
+    named = {
+        1_000_000: (100, 100, 100),
+        10_000_000: (250, 200, 200),
+        100_000_000: (500, 400, 500),
+    }
+    if num_nodes in named:
+        return named[num_nodes]
+    n = round(num_nodes ** (1.0 / 3.0))
+    return (n, n, n)
+
+
+def grid_graph(nx: int, ny: int, nz: int, device="cuda", permute_seed: Optional[int] = None,
+               z_begin: int = 0, z_count: Optional[int] = None):
+    """Periodic nx*ny*nz hex grid on `device` (native generator).
+
+    Returns (x [N,3] f32 in [0,1]^3, edge_index [2, 6N] int64).  With
+    `z_begin/z_count` only the k-slab [z_begin, z_begin+z_count) is emitted
+    with global node ids (used by the sharded path).  `permute_seed`
+    relabels nodes with a seeded random permutation (locality stress case).
+    """
+    from . import _lib
+
+    nzc = nz if z_count is None else z_count
+    n = nx * ny * nzc
+    x = torch.empty((n, 3), dtype=torch.float32, device=device)
+    ei = torch.empty((2, 6 * n), dtype=torch.int64, device=device)
+    _lib.check(_lib.lib().mignn_grid_graph(nx, ny, nz, z_begin, nzc, _lib.ptr(ei), _lib.ptr(x),
+                                           _lib.stream()), "mignn_grid_graph")
+    if permute_seed is not None:
+        assert z_count is None, "permutation is defined on the full grid only"
+        g = torch.Generator().manual_seed(permute_seed)
+        perm = torch.randperm(n, generator=g).to(device)      # old id -> new id
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(n, device=device)
+        x = x[inv]
+        ei = perm[ei]
+    return x, ei

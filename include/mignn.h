@@ -1,0 +1,149 @@
+/*
+ * mignn.h -- C ABI of libmignn.so, the MI355X (gfx950) GNN message-passing
+ * engine behind FlowGNN.forward (reference: gnn_model.py:104-197).
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer owned by the caller (PyTorch's
+ *     caching allocator in the shipped host code).  The library never
+ *     allocates persistent device memory, never frees, never synchronises the
+ *     stream: scratch is passed in, `stream` is a hipStream_t passed as void*.
+ *   - Row-major fp32 activations; `ld*` arguments are row strides in elements
+ *     and must be multiples of 4 (16-byte rows) where a kernel loads float4.
+ *   - Return value: 0 = MIGNN_OK; nonzero codes below.  mignn_last_error()
+ *     returns a thread-local description of the last failure.  The host shim
+ *     maps failures inside a layer to the reference's
+ *     RuntimeError("Message passing failed in layer i (type): ...")
+ *     (gnn_model.py:173-181).
+ *   - Re-entrant per stream; no internal host threads.
+ */
+#ifndef MIGNN_H
+#define MIGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIGNN_ABI_VERSION 1
+
+enum mignn_status {
+    MIGNN_OK = 0,
+    MIGNN_ERR_ARG = 1,          /* bad shape / null pointer / alignment        */
+    MIGNN_ERR_UNSUPPORTED = 2,  /* configuration without a kernel              */
+    MIGNN_ERR_HIP = 3,          /* HIP launch / runtime error                  */
+    MIGNN_ERR_SCRATCH = 4       /* scratch buffer too small                    */
+};
+
+int mignn_abi_version(void);
+const char* mignn_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Graph structure.
+ * Replaces, on the device and without host syncs:
+ *   - the edge validation / silent filtering / all-invalid self-loop fallback
+ *     of gnn_model.py:125-149 (the reference does two .item() syncs here);
+ *   - PyG add_remaining_self_loops + gcn_norm's degree (GCNConv, gnn_model.py:63)
+ *     and remove_self_loops + add_self_loops (GATConv, gnn_model.py:65-68):
+ *     mode MIGNN_CSR_ONE_SELF_LOOP;
+ *   - the verbatim edge list GINConv / TransformerConv aggregate over
+ *     (gnn_model.py:70-80): mode MIGNN_CSR_VERBATIM.
+ * Output: destination-major CSR (row_ptr[N+1], col[<= E+N]) with the
+ * in-row order equal to the edge order of `edge_index` (stable), the
+ * appended self-loop last; dinv[i] = deg_i^-1/2 (ONE_SELF_LOOP mode, may be
+ * NULL).  info (device int64[4], may be NULL) = {kept edges, invalid edges,
+ * nnz, all-invalid fallback taken}.
+ * ------------------------------------------------------------------------ */
+enum { MIGNN_CSR_VERBATIM = 0, MIGNN_CSR_ONE_SELF_LOOP = 1 };
+
+size_t mignn_csr_scratch_bytes(int64_t num_edges, int64_t num_nodes);
+int mignn_csr_build(const int64_t* edge_index, /* [2, E] int64, contiguous */
+                    int64_t num_edges, int64_t num_nodes, int mode,
+                    int32_t* row_ptr, int32_t* col, float* dinv, int64_t* info,
+                    void* scratch, size_t scratch_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Dense node transforms (MFMA f32 16x16x4, exact fp32).
+ * C[m, :] = epi( [A | A2][m, :] . W^T ),  W is [n, k + k2] (torch Linear layout).
+ * epi (flags): +bias[n] -> relu_pre? -> +residual -> *scale+shift -> relu.
+ * Used for nn.Linear (input_proj gnn_model.py:55, output_proj :90-100, GIN nn
+ * :70-74) and the conv transforms.  k, k2 multiples of 4.
+ * ------------------------------------------------------------------------ */
+enum {
+    MIGNN_EPI_BIAS = 1,
+    MIGNN_EPI_RESIDUAL = 2,
+    MIGNN_EPI_AFFINE = 4, /* BatchNorm eval affine: v*scale + shift */
+    MIGNN_EPI_RELU = 8
+};
+int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
+                 const float* a2, int64_t lda2, int k2,
+                 const float* w, int n,
+                 const float* bias, const float* residual, int64_t ldr,
+                 const float* scale, const float* shift, int flags,
+                 float* c, int64_t ldc, void* stream);
+
+/* Linear(in_dim -> h) with in_dim <= 8 on the VALU (K too thin for MFMA):
+ * input_proj, gnn_model.py:55, :159. */
+int mignn_input_proj(const float* x, int64_t n, int in_dim, const float* w, const float* b,
+                     int h, float* out, int64_t ldo, void* stream);
+
+/* BatchNorm1d eval fold: scale = w / sqrt(var + eps), shift = b - mean*scale
+ * (the same fold ATen's CPU batch_norm applies).  BatchNorm, gnn_model.py:87. */
+int mignn_bn_fold(const float* weight, const float* bias, const float* mean, const float* var,
+                  float eps, int h, float* scale, float* shift, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Aggregations (rows [row_begin, row_end) of the CSR; out row r at out+r*ldo).
+ * ------------------------------------------------------------------------ */
+/* GCN: out_i = sum_{j in row i} dinv_j dinv_i x_j  (PyG gcn_norm weights) */
+int mignn_gcn_aggregate(const int32_t* row_ptr, const int32_t* col, const float* dinv,
+                        const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                        float* out, int64_t ldo, void* stream);
+/* GIN: out_i = sum_{j in row i} x_j + self_scale * x_i  (self_scale = 1 + eps) */
+int mignn_sum_aggregate(const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx,
+                        float self_scale, int64_t row_begin, int64_t row_end, int h,
+                        float* out, int64_t ldo, void* stream);
+/* GAT (heads <= 8): logits [N, 2*heads] = (a_src | a_dst).
+ * out_i[hd] = sum_j softmax_j(LeakyReLU(a_src[j,hd] + a_dst[i,hd])) x_j, out [*, heads*h] */
+int mignn_gat_aggregate(const int32_t* row_ptr, const int32_t* col, const float* logits,
+                        const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                        int heads, float negative_slope, float* out, int64_t ldo, void* stream);
+/* TransformerConv (heads <= 8): qt row = [q~_0 .. q~_{heads-1} | c_0 .. c_{heads-1}]
+ * (q~_hd = Wk_hd^T q_hd, c_hd = q_hd . bk_hd, ldq >= heads*h + heads).
+ * s_ji = (q~_i . x_j + c_i) * score_scale; alpha = softmax over row i;
+ * out row = [sum_j alpha x_j per head | sum_j alpha per head]. */
+int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t* col, const float* qt,
+                                int64_t ldq, const float* x, int64_t ldx, int64_t row_begin,
+                                int64_t row_end, int h, int heads, float score_scale,
+                                float* out, int64_t ldo, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused GCN layer (the north-star hot kernel):
+ *   out_i = relu( ((x_i + (sum_j w_ji x_j) W^T + bias) * scale + shift) )
+ * i.e. GCNConv + residual + BatchNorm(eval) + ReLU of gnn_model.py:166,184-191
+ * in one pass: CSR gather into an LDS tile, MFMA transform, fused epilogue.
+ * flags: MIGNN_EPI_* (BIAS|RESIDUAL|AFFINE|RELU as the model configures).
+ * h in {64, 128, 256}.
+ * ------------------------------------------------------------------------ */
+int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* dinv,
+                    const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                    const float* w, const float* bias, const float* scale, const float* shift,
+                    int flags, float* out, int64_t ldo, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Multi-GPU halo helpers and synthetic inputs.
+ * ------------------------------------------------------------------------ */
+/* dst[r, :] = src[idx[r], :] for r < n (halo pack / unpack by index list) */
+int mignn_rows_gather(const float* src, int64_t lds, const int32_t* idx, int64_t n, int h,
+                      float* dst, int64_t ldd, void* stream);
+/* Periodic nx*ny*nz hex grid, k-slab [z_begin, z_begin+z_count): writes
+ * edge_index [2, 6*n] (src = neighbour, dst = node; global ids) and
+ * x [n, 3] = cell centres in [0,1]^3.  n = nx*ny*z_count. */
+int mignn_grid_graph(int nx, int ny, int nz, int z_begin, int z_count, int64_t* edge_index,
+                     float* x, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIGNN_H */

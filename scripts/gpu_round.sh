@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU-box session: smoke -> GPU tests -> bench.  Stops at the first
+# abort / fault / timeout (exit >1); a plain test failure (exit 1) still lets
+# the bench run so the numbers are collected.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 900 python -m pytest tests -m gpu -x -q -s ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+exit $rc

@@ -1,0 +1,198 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+Runs ONLY in the build container, where /root/reference exists.  It imports the
+reference's own code -- openfoam_loader.py, graph_constructor.py, gnn_model.py,
+normalization.py -- and runs it:
+
+* `torch_geometric.data.Data` is absent (PyG not installed); a plain attribute
+  bag stands in for it (graph_constructor.py:8, :262-267 only sets attributes).
+* `torch_geometric.nn` is absent; the CPU oracle's PyG-named classes
+  (oracle/flowgnn_oracle.py) are injected in its place, so the reference's
+  `FlowGNN` wrapper (validation, residual, BN, ReLU, output MLP) runs as
+  written while the conv arithmetic is the restatement (parity unpinned for
+  the conv arithmetic itself -- SURVEY.md §8c).
+
+Outputs (all small, committed):
+  bfs_graphs.npz       reference-built train-path / inference-path graphs
+  models.npz           seeded state_dicts + forward outputs (fp32 wrapper run,
+                       fp64 oracle run) for every parity configuration
+  tiny_graphs.npz      hand-checkable edge cases, all four layer types
+  normalizer.json      FieldNormalizer.fit stats over time dirs 0/100/200/282
+
+Usage:  python tests/golden/make_golden.py
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "gnn-bfs-rans_amd"))
+
+from oracle import flowgnn_oracle as orc  # noqa: E402
+from mignn.synthetic import seeded_state_dict  # noqa: E402
+
+
+class _Data:  # stand-in for torch_geometric.data.Data (attribute bag)
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+def _inject_pyg():
+    pyg = types.ModuleType("torch_geometric")
+    data = types.ModuleType("torch_geometric.data")
+    data.Data = _Data
+    data.Batch = None
+    pyg.data = data
+    pyg.nn = orc
+    sys.modules["torch_geometric"] = pyg
+    sys.modules["torch_geometric.data"] = data
+    sys.modules["torch_geometric.nn"] = orc
+
+
+def main():
+    _inject_pyg()
+    sys.path.insert(0, REF)
+    from openfoam_loader import OpenFOAMLoader
+    from graph_constructor import GraphConstructor
+    from gnn_model import FlowGNN
+    from normalization import FieldNormalizer
+
+    case = os.path.join(REF, "OpenFOAM-data")
+    loader = OpenFOAMLoader(case)
+    mesh = loader.load_mesh()
+    gc = GraphConstructor(mesh)
+
+    # --- graphs (train.py:104-108 / visualize.py:341-350 and inference.py:256) ---
+    fields282 = loader.load_fields("282")
+    n_internal = len(fields282["p"])
+    g_train = gc.build_graph(node_features=mesh["cell_centers"], filter_internal=True,
+                             n_internal_cells=n_internal)
+    g_inf = gc.build_graph(node_features=mesh["cell_centers"])
+    graphs = {
+        "train_x": g_train.x.numpy(), "train_ei": g_train.edge_index.numpy().astype(np.int32),
+        "train_ea": g_train.edge_attr.numpy(),
+        "infer_x": g_inf.x.numpy(), "infer_ei": g_inf.edge_index.numpy().astype(np.int32),
+        "infer_ea": g_inf.edge_attr.numpy(),
+    }
+    np.savez_compressed(os.path.join(HERE, "bfs_graphs.npz"), **graphs)
+    print("train graph", g_train.x.shape, g_train.edge_index.shape,
+          "infer graph", g_inf.x.shape, g_inf.edge_index.shape)
+
+    # --- normalizer (train.py:50-77) ---
+    all_fields = {}
+    for t in ["0", "100", "200", "282"]:
+        try:
+            f = loader.load_fields(t)
+        except Exception:
+            continue
+        for k, v in f.items():
+            all_fields.setdefault(k, []).append(v)
+    norm = FieldNormalizer()
+    norm.fit({k: np.concatenate(v, axis=0) for k, v in all_fields.items()})
+    js = {k: {"mean": np.asarray(s["mean"]).tolist(), "std": np.asarray(s["std"]).tolist(),
+              "per_component": bool(s["per_component"])} for k, s in norm.scalers.items()}
+    with open(os.path.join(HERE, "normalizer.json"), "w") as fh:
+        json.dump(js, fh, indent=1)
+
+    # --- model configurations ---
+    configs = {
+        "c1_gcn_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GCN"),
+        "c2_gcn_h128_l4": dict(hidden_dim=128, num_layers=4, layer_type="GCN"),
+        "gat_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GAT"),
+        "gat_h128_l4": dict(hidden_dim=128, num_layers=4, layer_type="GAT"),
+        "gin_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GIN"),
+        "transformer_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="Transformer"),
+    }
+    out = {}
+    torch.manual_seed(0)
+    for seed, (name, cfg) in enumerate(configs.items()):
+        model = FlowGNN(input_dim=3, output_dim=7, use_edge_attr=True, dropout=0.0,
+                        use_batch_norm=True, **cfg)
+        sd = seeded_state_dict(model.state_dict(), seed=100 + seed)
+        model.load_state_dict(sd)
+        model.eval()
+        for gname, g in (("train", g_train), ("infer", g_inf)):
+            if gname == "infer" and cfg["layer_type"] not in ("GCN", "GIN") or \
+               gname == "infer" and cfg["hidden_dim"] != 64:
+                continue
+            ea = None if cfg["layer_type"] == "Transformer" else g.edge_attr
+            with torch.no_grad():
+                y32 = model(g.x, g.edge_index, ea)
+            y64 = orc.flowgnn_forward(sd, cfg, g.x, g.edge_index, ea, dtype=torch.float64)
+            y32o = orc.flowgnn_forward(sd, cfg, g.x, g.edge_index, ea, dtype=torch.float32)
+            d_wrap = (y32 - y32o).abs().max().item()
+            d_64 = (y32.double() - y64).abs().max().item()
+            print(f"{name:22s} {gname}: |ref-wrapper - oracle32| {d_wrap:.3e}  "
+                  f"|fp32 - fp64| {d_64:.3e}  absmax {y64.abs().max().item():.3f}")
+            assert d_wrap <= 1e-6, "wrapper restatement drifted from reference wrapper"
+            out[f"{name}/{gname}/y32"] = y32.numpy()
+            out[f"{name}/{gname}/y64"] = y64.numpy()
+        if cfg["layer_type"] == "Transformer":
+            try:
+                with torch.no_grad():
+                    model(g_train.x, g_train.edge_index, g_train.edge_attr)
+                raise AssertionError("expected the reference to raise")
+            except RuntimeError as e:
+                msg = str(e)
+                assert msg.startswith("Message passing failed in layer 0 (Transformer)"), msg
+                out[f"{name}/edge_attr_error"] = np.array(msg.split("\n")[0])
+        for k, v in sd.items():
+            out[f"{name}/sd/{k}"] = v.numpy()
+        out[f"{name}/cfg"] = np.array(json.dumps(cfg))
+    np.savez_compressed(os.path.join(HERE, "models.npz"), **out)
+
+    # --- tiny hand-checkable graphs, every layer type, H = 8 ---
+    tiny = {
+        # 6-node path 0-1-2-3-4-5, both directions
+        "path6": (6, [[0, 1, 1, 2, 2, 3, 3, 4, 4, 5], [1, 0, 2, 1, 3, 2, 4, 3, 5, 4]]),
+        # node 3 isolated (degree-0 row), node 0 has duplicate self-loops
+        "isolated_dupself": (5, [[0, 0, 0, 1, 2, 1, 4], [0, 0, 1, 0, 1, 2, 2]]),
+        # duplicate non-self edges count twice
+        "dup_edges": (4, [[0, 0, 1, 2, 3, 3], [1, 1, 2, 3, 0, 0]]),
+        # out-of-range indices are silently dropped (gnn_model.py:133-141)
+        "invalid_idx": (4, [[0, 1, 7, 2, -1, 3], [1, 2, 0, 3, 0, 0]]),
+        # every index invalid -> self-loops for all nodes (gnn_model.py:144-149)
+        "all_invalid": (3, [[5, 6], [7, 9]]),
+        # empty edge set: no validation branch, convs see E=0
+        "empty": (3, [[], []]),
+        # star: high in-degree hub (segmented softmax over many entries)
+        "star40": (41, [list(range(1, 41)) + [0] * 40, [0] * 40 + list(range(1, 41))]),
+    }
+    tg = {}
+    for ti, (tname, (n, ei)) in enumerate(tiny.items()):
+        g = torch.Generator().manual_seed(7 + ti)
+        x = torch.rand((n, 3), generator=g) * 2 - 1
+        ei_t = torch.tensor(ei, dtype=torch.long).reshape(2, -1)
+        tg[f"{tname}/x"] = x.numpy()
+        tg[f"{tname}/ei"] = ei_t.numpy()
+        for lt in ("GCN", "GAT", "GIN", "Transformer"):
+            cfg = dict(hidden_dim=8, num_layers=2, layer_type=lt)
+            model = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+            sd = seeded_state_dict(model.state_dict(), seed=1000 + ti)
+            model.load_state_dict(sd)
+            model.eval()
+            with torch.no_grad():
+                y32 = model(x, ei_t, None)
+            y64 = orc.flowgnn_forward(sd, cfg, x, ei_t, None, dtype=torch.float64)
+            assert (y32.double() - y64).abs().max().item() < 1e-5
+            tg[f"{tname}/{lt}/y64"] = y64.numpy()
+            tg[f"{tname}/{lt}/y32"] = y32.numpy()
+            for k, v in sd.items():
+                tg[f"{tname}/{lt}/sd/{k}"] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, "tiny_graphs.npz"), **tg)
+    print("wrote fixtures to", HERE)
+
+
+if __name__ == "__main__":
+    main()
