@@ -83,4 +83,11 @@ __device__ __forceinline__ float epilogue(float acc, int flags, float bias, floa
     return v;
 }
 
+// Register-resident-W persistent row-tile GEMM (tile_gemm.hip) for the
+// FlowGNN layer / head shapes; *handled=false when (k, n) has no instance.
+int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, int n,
+                const float* bias, const float* residual, int64_t ldr, const float* scale,
+                const float* shift, int flags, float* c, int64_t ldc, hipStream_t st,
+                bool* handled);
+
 }  // namespace mignn

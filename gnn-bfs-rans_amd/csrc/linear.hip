@@ -14,7 +14,8 @@
 // k = k0 + 4g + u.  A and W use the same k permutation, so the sum is exact
 // fp32 over all k (only the association order differs from a CPU GEMM).
 // Fragments are loaded straight from global memory (L1/L2-resident weights);
-// the GCN hot path has its own LDS-tiled persistent kernel (gcn_fused.hip).
+// FlowGNN's layer / head shapes (K, N <= 128) go to the register-resident-W
+// persistent kernel in tile_gemm.hip; this kernel covers everything else.
 #include "common.hpp"
 
 namespace mignn {
@@ -91,16 +92,25 @@ __global__ __launch_bounds__(256) void linear_kernel(
     }
 }
 
-// Linear(in_dim -> h) for in_dim <= 8: one thread per 4 output columns.
-__global__ void input_proj_kernel(const float* __restrict__ x, int64_t n, int in_dim,
-                                  const float* __restrict__ w, const float* __restrict__ b, int h,
-                                  float* __restrict__ out, int64_t ldo) {
+// Linear(in_dim -> h) for in_dim <= 8: thread (row slot, column quad) with
+// its 4 W rows and biases in registers; 32-bit index math only (a 64-bit
+// div/mod per element made this store-bound kernel 6x slower).
+__global__ __launch_bounds__(256) void input_proj_kernel(
+    const float* __restrict__ x, int64_t n, int in_dim, const float* __restrict__ w,
+    const float* __restrict__ b, int h, float* __restrict__ out, int64_t ldo) {
     const int h4 = h >> 2;
-    const int64_t total = n * h4;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t row = t / h4;
-        const int c = static_cast<int>(t % h4) * 4;
+    const int rpi = blockDim.x / h4;                 // rows per block iteration
+    const int slot = threadIdx.x / h4;
+    const int c = (threadIdx.x % h4) * 4;
+    if (slot >= rpi) return;
+    float wr[4][8], bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        bq[q] = b[c + q];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wr[q][k] = k < in_dim ? w[(c + q) * in_dim + k] : 0.f;
+    }
+    for (int64_t row = (int64_t)blockIdx.x * rpi + slot; row < n; row += (int64_t)gridDim.x * rpi) {
         float xv[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) xv[k] = k < in_dim ? x[row * in_dim + k] : 0.f;
@@ -108,8 +118,10 @@ __global__ void input_proj_kernel(const float* __restrict__ x, int64_t n, int in
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             float s = 0.f;
-            for (int k = 0; k < in_dim; ++k) s = fmaf(xv[k], w[(c + q) * in_dim + k], s);
-            o[q] = s + b[c + q];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (k < in_dim) s = fmaf(xv[k], wr[q][k], s);
+            o[q] = s + bq[q];
         }
         st4(out + row * ldo + c, make_float4(o[0], o[1], o[2], o[3]));
     }
@@ -134,6 +146,12 @@ extern "C" int mignn_linear(const float* a, int64_t lda, int64_t m, int k, const
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_RESIDUAL) || residual, "linear: residual flag without R");
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "linear: affine w/o params");
     if (m == 0) return MIGNN_OK;
+    if (k2 == 0) {
+        bool handled = false;
+        const int rc = tile_linear(a, lda, m, k, w, n, bias, residual, ldr, scale, shift, flags,
+                                   c, ldc, as_stream(stream), &handled);
+        if (handled) return rc;
+    }
     const int64_t gm = (m + BM - 1) / BM;
     MIGNN_REQUIRE(gm < (int64_t(1) << 31), "linear: m too large");
     dim3 grid(static_cast<unsigned>(gm), static_cast<unsigned>((n + BN - 1) / BN));
@@ -148,7 +166,11 @@ extern "C" int mignn_input_proj(const float* x, int64_t n, int in_dim, const flo
                   "input_proj: in_dim=%d h=%d", in_dim, h);
     MIGNN_REQUIRE(x && w && b && out && aligned16(out), "input_proj: null/unaligned");
     if (n == 0) return MIGNN_OK;
-    hipLaunchKernelGGL(input_proj_kernel, dim3(grid_for(n * (h / 4), 256, 65536)), dim3(256), 0,
-                       as_stream(stream), x, n, in_dim, w, b, h, out, ldo);
+    MIGNN_REQUIRE(h / 4 <= 1024, "input_proj: h too large");
+    const int h4 = h / 4;
+    const int block = h4 >= 256 ? h4 : (256 / h4) * h4;
+    const int64_t rpi = block / h4;
+    hipLaunchKernelGGL(input_proj_kernel, dim3(grid_for((n + rpi - 1) / rpi, 1, 16384)),
+                       dim3(block), 0, as_stream(stream), x, n, in_dim, w, b, h, out, ldo);
     return launch_status("input_proj_kernel");
 }

@@ -42,6 +42,8 @@ SIGNATURES = {
                                             c_int, c_int, c_float, _P, c_int64, _P]),
     "mignn_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P, _P,
                                 c_int, _P, c_int64, _P]),
+    "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
+                                _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),
     "mignn_rows_gather": (c_int, [_P, c_int64, _P, c_int64, c_int, _P, c_int64, _P]),
     "mignn_grid_graph": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, _P, _P]),
 }

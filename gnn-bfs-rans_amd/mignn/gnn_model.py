@@ -406,6 +406,13 @@ class FlowGNN(nn.Module):
             nn0, nn2 = layer.nn[0], layer.nn[2]
             eps = self._cached("eps", i, (layer.eps,), lambda: float(layer.eps.reshape(-1)[0]))
             agg = torch.empty((n, H), dtype=torch.float32, device=x.device)
+            if H in (64, 128):
+                _lib.check(L.mignn_gin_layer(P(csr.row_ptr), P(csr.col), P(x), x.stride(0), rb, re,
+                                             H, eps, P(nn0.weight), P(nn0.bias), P(nn2.weight),
+                                             P(nn2.bias), P(scale), P(shift), epi, P(agg),
+                                             agg.stride(0), P(out), out.stride(0), st),
+                           "mignn_gin_layer")
+                return
             _lib.check(L.mignn_sum_aggregate(P(csr.row_ptr), P(csr.col), P(x), x.stride(0),
                                              1.0 + eps, rb, re, H,
                                              P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st),

@@ -124,12 +124,22 @@ int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t* col, cons
  * i.e. GCNConv + residual + BatchNorm(eval) + ReLU of gnn_model.py:166,184-191
  * in one pass: CSR gather into an LDS tile, MFMA transform, fused epilogue.
  * flags: MIGNN_EPI_* (BIAS|RESIDUAL|AFFINE|RELU as the model configures).
- * h in {64, 128, 256}.
+ * h in {64, 128} (other h: mignn_gcn_aggregate + mignn_linear).
  * ------------------------------------------------------------------------ */
 int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* dinv,
                     const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
                     const float* w, const float* bias, const float* scale, const float* shift,
                     int flags, float* out, int64_t ldo, void* stream);
+
+/* Fused GIN layer (gnn_model.py:70-75, :166, :184-191), h in {64, 128}:
+ *   tmp_i = relu(nn.0( sum_{j in row i} x_j + (1 + eps) x_i ))      (rows rb..re -> tmp[0..])
+ *   out_i = epi( nn.2(tmp_i) ) with residual x_i, BN affine, ReLU   (flags as above)
+ * tmp: caller scratch of (re - rb) rows, stride ldt. */
+int mignn_gin_layer(const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx,
+                    int64_t row_begin, int64_t row_end, int h, float eps,
+                    const float* w1, const float* b1, const float* w2, const float* b2,
+                    const float* scale, const float* shift, int flags,
+                    float* tmp, int64_t ldt, float* out, int64_t ldo, void* stream);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU halo helpers and synthetic inputs.

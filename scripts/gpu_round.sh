@@ -14,4 +14,12 @@ rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+if [ -n "${PROFILE:-}" ]; then
+  export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench \
+      --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --no-bfs \
+      > gpurun_out/prof.log 2>&1
+  rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
+fi
 exit $rc
