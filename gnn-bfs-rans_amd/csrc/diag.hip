@@ -1,0 +1,105 @@
+// Diagnostic kernels (timing studies only; declared in include/mignn_diag.h,
+// not part of the product ABI): what the memory system delivers for the GCN
+// gather pattern with and without CSR index traffic.
+//
+//   mode 0  CSR gather, half-wave per row, all edges of a row in flight
+//           (deg <= 8), weights from ew -> out[i] = sum w_e x[col_e]
+//   mode 1  stencil gather on the periodic (nx, ny, nz) grid: neighbour ids
+//           computed from the row id (no index loads) -> the memory system's
+//           best case for this access pattern
+//   mode 2  streaming copy out[i] = x[i] (16 B per lane)
+//   | 4     XCD-aware block -> row remap (contiguous row chunks per XCD per step)
+//   | 8     non-temporal output stores
+#include "common.hpp"
+
+namespace mignn {
+namespace {
+
+template <int MODE, bool REMAP, bool NT>
+__global__ __launch_bounds__(256) void diag_gather_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ ew, const float* __restrict__ x, int64_t n, int nx, int ny, int nz,
+    float* __restrict__ out) {
+    constexpr int H = 128, LPR = 32;
+    const int lane = threadIdx.x & 63;
+    const int c = lane % LPR;
+    const int64_t nrow_groups = ((int64_t)gridDim.x * blockDim.x) / LPR;
+    int64_t blk = blockIdx.x;
+    if (REMAP) {   // steps of S = 8 * 256 blocks; XCD group x gets a contiguous run of 256
+        constexpr int64_t S = 8 * 256;
+        const int64_t step = blk / S, i = blk % S;
+        blk = step * S + (i % 8) * 256 + i / 8;
+    }
+    for (int64_t row = (blk * blockDim.x + threadIdx.x) / LPR; row < n; row += nrow_groups) {
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (MODE == 0) {
+            const int beg = row_ptr[row], deg = row_ptr[row + 1] - beg;
+            int j[8];
+            float w[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                j[u] = u < deg ? col[beg + u] : static_cast<int>(row);
+                w[u] = u < deg ? ew[beg + u] : 0.f;
+            }
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = ld4(x + (int64_t)j[u] * H + 4 * c);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = fma4(w[u], v[u], acc);
+        } else if constexpr (MODE == 1) {
+            const int64_t plane = (int64_t)nx * ny;
+            const int i = static_cast<int>(row % nx);
+            const int jj = static_cast<int>((row / nx) % ny);
+            const int k = static_cast<int>(row / plane);
+            const int64_t nb[7] = {
+                row,
+                (int64_t)k * plane + (int64_t)jj * nx + (i + nx - 1) % nx,
+                (int64_t)k * plane + (int64_t)jj * nx + (i + 1) % nx,
+                (int64_t)k * plane + (int64_t)((jj + ny - 1) % ny) * nx + i,
+                (int64_t)k * plane + (int64_t)((jj + 1) % ny) * nx + i,
+                (int64_t)((k + nz - 1) % nz) * plane + (int64_t)jj * nx + i,
+                (int64_t)((k + 1) % nz) * plane + (int64_t)jj * nx + i};
+            float4 v[7];
+#pragma unroll
+            for (int u = 0; u < 7; ++u) v[u] = ld4(x + nb[u] * H + 4 * c);
+#pragma unroll
+            for (int u = 0; u < 7; ++u) acc = fma4(0.14285715f, v[u], acc);
+        } else {
+            acc = ld4(x + row * H + 4 * c);
+        }
+        if (NT) {
+            const f32x4 v = {acc.x, acc.y, acc.z, acc.w};
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + row * H + 4 * c));
+        } else {
+            st4(out + row * H + 4 * c, acc);
+        }
+    }
+}
+
+}  // namespace
+}  // namespace mignn
+
+using namespace mignn;
+
+extern "C" int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t* col,
+                                 const float* ew, const float* x, int64_t n, int nx, int ny,
+                                 int nz, int blocks, float* out, void* stream) {
+    hipStream_t st = as_stream(stream);
+    const int g = blocks > 0 ? blocks : static_cast<int>(grid_for(n * 32, 256, 1 << 20));
+#define MIGNN_DIAG(M, R, T) \
+    hipLaunchKernelGGL((diag_gather_kernel<M, R, T>), dim3(g), dim3(256), 0, st, row_ptr, col, ew, x, n, nx, ny, nz, out)
+    const int base = mode & 3;
+    const bool remap = mode & 4, nt = mode & 8;
+    if (remap && blocks > 0) { set_error("diag: remap needs a full grid"); return MIGNN_ERR_ARG; }
+    if (base == 0) {
+        if (remap) { if (nt) MIGNN_DIAG(0, true, true); else MIGNN_DIAG(0, true, false); }
+        else { if (nt) MIGNN_DIAG(0, false, true); else MIGNN_DIAG(0, false, false); }
+    } else if (base == 1) {
+        if (remap) { if (nt) MIGNN_DIAG(1, true, true); else MIGNN_DIAG(1, true, false); }
+        else { if (nt) MIGNN_DIAG(1, false, true); else MIGNN_DIAG(1, false, false); }
+    } else {
+        if (nt) MIGNN_DIAG(2, false, true); else MIGNN_DIAG(2, false, false);
+    }
+#undef MIGNN_DIAG
+    return launch_status("diag_gather_kernel");
+}

@@ -206,6 +206,17 @@ __global__ void bn_fold_kernel(const float* __restrict__ w, const float* __restr
     }
 }
 
+// PyG gcn_norm edge weights per CSR entry: w_e = dinv[src] * 1 * dinv[dst].
+__global__ void gcn_norm_kernel(const int32_t* __restrict__ row_ptr,
+                                const int32_t* __restrict__ col, const float* __restrict__ dinv,
+                                int64_t rb, int64_t re, float* __restrict__ ew) {
+    for (int64_t i = rb + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < re;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float di = dinv[i];
+        for (int e = row_ptr[i]; e < row_ptr[i + 1]; ++e) ew[e] = dinv[col[e]] * di;
+    }
+}
+
 __global__ void rows_gather_kernel(const float* __restrict__ src, int64_t lds,
                                    const int32_t* __restrict__ idx, int64_t n, int h4,
                                    float* __restrict__ dst, int64_t ldd) {
@@ -311,6 +322,15 @@ extern "C" int mignn_bn_fold(const float* weight, const float* bias, const float
     hipLaunchKernelGGL(bn_fold_kernel, dim3((h + 255) / 256), dim3(256), 0, as_stream(stream),
                        weight, bias, mean, var, eps, h, scale, shift);
     return launch_status("bn_fold_kernel");
+}
+
+extern "C" int mignn_gcn_norm(const int32_t* row_ptr, const int32_t* col, const float* dinv,
+                              int64_t rb, int64_t re, float* ew, void* stream) {
+    MIGNN_REQUIRE(row_ptr && col && dinv && ew && rb >= 0 && re >= rb, "gcn_norm: bad args");
+    if (re == rb) return MIGNN_OK;
+    hipLaunchKernelGGL(gcn_norm_kernel, dim3(grid_for(re - rb, kBlock, 65536)), dim3(kBlock), 0,
+                       as_stream(stream), row_ptr, col, dinv, rb, re, ew);
+    return launch_status("gcn_norm_kernel");
 }
 
 extern "C" int mignn_rows_gather(const float* src, int64_t lds, const int32_t* idx, int64_t n,

@@ -1,9 +1,10 @@
-// Persistent row-tile GEMM with a fused A-tile producer and epilogue:
+// Persistent, wave-specialized row-tile GEMM with a fused A-tile producer and
+// epilogue:
 //
 //   out[i, :] = epi( A_i . W^T ),   A_i = one of
-//     AGG_GCN : sum_{j in row i} dinv_j dinv_i x_j          (GCNConv, gnn_model.py:63)
-//     AGG_SUM : sum_{j in row i} x_j + (1 + eps) x_i         (GINConv, gnn_model.py:70-75)
-//     ROWS    : a[i, :]                                      (nn.Linear)
+//     AGG_GCN : sum_{e in row i} w_e x_{col e}     w_e = dinv_src dinv_dst  (GCNConv, gnn_model.py:63)
+//     AGG_SUM : sum_{e in row i} x_{col e} + (1 + eps) x_i              (GINConv, gnn_model.py:70-75)
+//     ROWS    : a[i, :]                                                 (nn.Linear)
 //   epi = +bias -> +residual -> *scale+shift (BatchNorm eval) -> ReLU (flags).
 //
 // The AGG_GCN instance is the north-star hot kernel: GCNConv + residual +
@@ -12,25 +13,29 @@
 // aggregate-then-transform order (A x) W^T == A (x W^T) needs no [N, H]
 // intermediate.
 //
-// Workgroup = 8 waves (512 threads), row tile BM = 64, two workgroups per CU
-// (4 waves per SIMD, <= 128 VGPRs), persistent grid = CUs x 2 (multiple of 8):
-//   * Every wave owns 8 rows of the tile for the gather and a 16-column (or
-//     WROWS x 16) slice of the output for the MFMA; its slice of W lives in
-//     VGPRs for the whole launch (32 VGPRs at K = 128).
-//   * CSR indices never touch LDS: lanes 0..8 hold the wave's row_ptr, lane t
-//     holds the t-th (neighbour id, dinv_j) of the wave's rows; row groups
-//     fetch them with ds_bpermute.  The next tile's indices are loaded while
-//     this tile's MFMAs run, so a tile costs only its x-row round trips
-//     (2 at K = 128: 16 neighbour rows in flight per row group).
-//   * Gathered rows are summed in CSR order (== edge_index order): bitwise
-//     deterministic.  The aggregated tile goes to LDS [64][K+8] (row stride
-//     8 mod 64 floats: conflict-free quad-interleaved ds_read_b128).
-//   * MFMA v_mfma_f32_16x16x4_f32 (exact fp32): lane (r, g) = (l & 15, l >> 4)
-//     reads A[16 ib + r][16 kc + 4g .. +3] and feeds k = 16 kc + 4g + u at step
-//     u -- the permutation its W registers were loaded in; the IB accumulator
-//     chains are interleaved so back-to-back MFMAs are independent.
-//   * Epilogue from the accumulators (residual prefetched before the MFMAs):
-//     each store instruction writes 4 rows x 64 B.
+// One 12-wave workgroup per CU (persistent, grid = #CUs rounded to 8), row
+// tile BM = 64, one barrier per tile:
+//   * waves 4..11 PRODUCE tile s+1 into LDS buffer (s+1)&1 while waves 0..3
+//     CONSUME tile s from buffer s&1 -- gather latency and MFMA overlap inside
+//     the workgroup (measured: two co-resident workgroups that each alternate
+//     gather and MFMA phases run in lockstep and overlap nothing).  A
+//     producer keeps all 32 neighbour rows of its slice in flight: the gather
+//     is bound by bytes in flight (Infinity-Cache latency x rate), not issue.
+//   * producer wave p owns rows 8p..8p+7.  Its CSR indices never touch LDS:
+//     lanes 0..8 hold row_ptr, lane t holds entry t (and t+64) of the rows'
+//     (column id, edge weight) -- fetched by ds_bpermute.  The index chain is
+//     pipelined: row_ptr of tile s+3 and the entries of tile s+2 load during
+//     the gather of tile s+1, so a tile costs its x-row round trips only.
+//     Rows are summed in CSR order (== edge_index order): bitwise
+//     deterministic.  A row group of K/4 lanes (16 B per lane) owns one row.
+//   * consumer waves (WM x WN) hold nothing big in registers: W [N, K] is
+//     staged in LDS once per launch; A and B fragments are read with
+//     ds_read_b128 from row stride K+8 (= 8 mod 64 floats: the
+//     quad-interleaved pattern is bank-conflict free).  MFMA is
+//     v_mfma_f32_16x16x4_f32 (exact fp32); lane (r, g) = (l & 15, l >> 4)
+//     feeds k = 16 kc + 4g + u at step u for both operands.  The residual is
+//     prefetched before the MFMAs; the epilogue runs from the accumulators
+//     with non-temporal stores (the 5 GB of output must not evict x rows).
 //   * XCD-aware tile order: at step t the chip covers tiles [tG, (t+1)G); the
 //     workgroups of XCD group x = blockIdx % 8 take one contiguous run of G/8
 //     tiles, so the +-1 / +-row neighbours a run gathers share that XCD's L2
@@ -41,74 +46,80 @@
 namespace mignn {
 namespace {
 
-constexpr int BM = 64;
-constexpr int NW = 8;               // waves per workgroup
-constexpr int NTHREADS = NW * 64;
-constexpr int GROWS = BM / NW;      // rows gathered per wave (8)
+constexpr int BM = 48;                 // rows per tile
+constexpr int NCW = 4;                 // consumer waves (one per SIMD: MFMA issue saturates)
+constexpr int NPW = 12;                // producer waves
+constexpr int NTHREADS = (NCW + NPW) * 64;
+constexpr int PROWS = BM / NPW;        // rows per producer wave (4)
+constexpr int IREG = 1;                // index registers per lane: 64 CSR entries per wave
 
 enum { AGG_GCN = 0, AGG_SUM = 1, ROWS = 2 };
 
 template <int K, int N, int MODE>
 struct Cfg {
-    static_assert(K % 16 == 0 && K <= 256, "K in 16..256, multiple of 16");
-    static constexpr int WN = N / 16 < NW ? N / 16 : NW;   // column slices
-    static constexpr int WM_ = NW / WN;
-    static constexpr int WM = WM_ > 4 ? 4 : WM_;           // row slices (>= 16 rows each)
-    static constexpr int MW = WM * WN;                     // waves doing MFMA
+    static_assert(K % 16 == 0 && K <= 256 && N % 16 == 0, "K, N multiples of 16, K <= 256");
+    static constexpr int WN = N / 16 < NCW ? N / 16 : NCW;    // consumer column slices
+    static constexpr int WM = 1;                               // consumers own all 48 rows
+    static constexpr int MW = WM * WN;                         // consumer waves with work
     static constexpr int WROWS = BM / WM;
     static constexpr int WCOLS = N / WN;
-    static_assert(WCOLS % 16 == 0 && WROWS % 16 == 0, "wave tile must be 16-aligned");
     static constexpr int IB = WROWS / 16;
     static constexpr int JB = WCOLS / 16;
     static constexpr int KC = K / 16;
-    static constexpr int LPR = K / 4;                      // lanes per A row (16 B each)
-    static constexpr int RPW = 64 / LPR;                   // rows per wave instruction
-    static constexpr int RSTEPS = GROWS / RPW;             // row steps per wave
-    static constexpr int RIF = (RSTEPS < 2 || K > 64 || MODE == AGG_GCN) ? 1 : 2;   // VGPR cap 128
-    static constexpr int A_LD = K + 8;
-    static constexpr int A_FLOATS = BM * A_LD;
+    static constexpr int LPR = K / 4;                          // lanes per A row (16 B each)
+    static constexpr int RPW = 64 / LPR;                       // rows per wave instruction
+    static constexpr int RSTEPS = PROWS >= RPW ? PROWS / RPW : 1;   // row steps per producer wave
+    static constexpr int RIF = RSTEPS;                         // every row step in flight
+    static constexpr int LD = K + 8;                           // LDS row stride (floats)
+    static constexpr int A_FLOATS = BM * LD;
+    static constexpr int W_FLOATS = N * LD;
+    static constexpr int LDS_FLOATS = 2 * A_FLOATS + W_FLOATS;
+    static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
 };
 
-struct WaveIdx {        // CSR indices of a wave's 8 rows, in lane registers
-    int rp;             // lanes 0..8: row_ptr[r0 + lane] (clamped)
-    float dr;           // lanes 0..7: dinv[r0 + lane]
-    int j;              // lane t < ne: col[e0 + t]
-    float dj;           // lane t < ne: dinv[col[e0 + t]]
+struct TileIdx {            // CSR indices of one producer wave's 8 rows, in lane registers
+    int rp;                 // lanes 0..8: row_ptr[r0 + lane] (clamped to row_end)
+    int j[IREG];            // lane t: col[e0 + t + 64 q]
+    float w[IREG];          // lane t: ew[e0 + t + 64 q]  (GCN weights)
 };
 
-template <int MODE>
-__device__ __forceinline__ void load_rp(WaveIdx& w, const int32_t* __restrict__ row_ptr,
-                                        const float* __restrict__ dinv, int64_t r0,
-                                        int64_t row_end, int lane) {
+__device__ __forceinline__ int load_rp(const int32_t* __restrict__ row_ptr, int64_t r0,
+                                       int64_t row_end, int lane) {
     const int64_t rr = r0 + lane < row_end ? r0 + lane : row_end;
-    w.rp = lane <= GROWS ? row_ptr[rr] : 0;
-    w.dr = (MODE == AGG_GCN && lane < GROWS && r0 + lane < row_end) ? dinv[r0 + lane] : 0.f;
+    return (r0 < row_end && lane <= PROWS) ? row_ptr[rr] : 0;
 }
 
 template <int MODE>
-__device__ __forceinline__ void load_cols(WaveIdx& w, const int32_t* __restrict__ col,
-                                          const float* __restrict__ dinv, int lane) {
-    const int e0 = __shfl(w.rp, 0, 64);
-    const int ne = __shfl(w.rp, GROWS, 64) - e0;
-    w.j = lane < ne ? col[e0 + lane] : 0;
-    w.dj = 1.f;
-    if constexpr (MODE == AGG_GCN) w.dj = lane < ne ? dinv[w.j] : 0.f;
+__device__ __forceinline__ void load_entries(TileIdx& t, const int32_t* __restrict__ col,
+                                             const float* __restrict__ ew, int lane) {
+    const int e0 = __shfl(t.rp, 0, 64);
+    const int ne = __shfl(t.rp, PROWS, 64) - e0;
+#pragma unroll
+    for (int q = 0; q < IREG; ++q) {
+        const int e = lane + 64 * q;
+        t.j[q] = e < ne ? col[e0 + e] : 0;
+        t.w[q] = (MODE == AGG_GCN && e < ne) ? ew[e0 + e] : 1.f;
+    }
 }
 
 template <int K, int N, int MODE>
+// 16 waves per CU = 4 per SIMD -> <= 128 VGPRs: 16 gathered rows in flight per
+// producer wave (12 producers: 192 KB per CU)
 __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ dinv, float self_scale, const float* __restrict__ x, int64_t ldx,
+    const float* __restrict__ ew, float self_scale, const float* __restrict__ x, int64_t ldx,
     int64_t row_begin, int64_t row_end, const float* __restrict__ W,
     const float* __restrict__ bias, const float* __restrict__ R, int64_t ldr,
     const float* __restrict__ scale, const float* __restrict__ shift, int flags, int n_valid,
     float* __restrict__ out, int64_t ldo) {
     using C = Cfg<K, N, MODE>;
-    __shared__ __attribute__((aligned(16))) float A[C::A_FLOATS];
+    __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
+    float* const A0 = lds;
+    float* const Wl = lds + 2 * C::A_FLOATS;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // SGPR: uniform bases below
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     const int64_t nrows = row_end - row_begin;
     const int64_t ntiles = (nrows + BM - 1) / BM;
@@ -116,154 +127,223 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
     const int xcd = blockIdx.x & 7;
     const int slot = blockIdx.x >> 3;
     const int per_xcd = G >> 3;
+    const int64_t nsteps = (ntiles + G - 1) / G;
     auto tile_of = [&](int64_t s) -> int64_t { return s * G + (int64_t)xcd * per_xcd + slot; };
 
-    // MFMA role
-    const bool mw = wave < C::MW;
-    const int r = lane & 15, g = lane >> 4;
-    const int wm = wave / C::WN, wn = wave % C::WN;
-    float4 breg[C::JB][C::KC];
-#pragma unroll
-    for (int jb = 0; jb < C::JB; ++jb) {
-        const int n = wn * C::WCOLS + jb * 16 + r;
-        const bool ok = mw && n < n_valid;
-#pragma unroll
-        for (int kc = 0; kc < C::KC; ++kc)
-            breg[jb][kc] = ok ? ld4(W + (int64_t)n * K + kc * 16 + 4 * g)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    // W -> LDS (rows n >= n_valid padded with zeros)
+    for (int i = tid; i < N * (K / 4); i += NTHREADS) {
+        const int n = i / (K / 4), k4 = i % (K / 4);
+        st4(&Wl[n * C::LD + 4 * k4], n < n_valid ? ld4(W + (int64_t)n * K + 4 * k4)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f));
     }
 
-    WaveIdx idx{0, 0.f, 0, 0.f};
-    int64_t tile = tile_of(0);
-    if (MODE != ROWS && tile < ntiles) {
-        const int64_t r0 = row_begin + tile * BM + wave * GROWS;
-        load_rp<MODE>(idx, row_ptr, dinv, r0, row_end, lane);
-        load_cols<MODE>(idx, col, dinv, lane);
-    }
+    if (wave >= NCW) {
+        // ============================================================ producer
+        const int pw = wave - NCW;
+        auto first_row = [&](int64_t tile) { return row_begin + tile * BM + pw * PROWS; };
 
-    for (int64_t s = 0; tile < ntiles; ++s) {
-        // Opaque per-iteration copies of the lane coordinates: stops LICM from
-        // hoisting dozens of lane-dependent address offsets out of the tile
-        // loop (they would pin VGPRs for the whole launch and spill at the
-        // 128-VGPR cap of two workgroups per CU).
-        int lane_ = lane;
-        asm volatile("" : "+v"(lane_));
-        const int r = lane_ & 15, g = lane_ >> 4;
-        const int c = lane_ % C::LPR;
-        const int grp = lane_ / C::LPR;
-        const int64_t t0 = row_begin + tile * BM;
-        const int64_t r0 = t0 + wave * GROWS;          // first gathered row of this wave
-
-        // ------------------------------------------------ A tile -> LDS
-        if constexpr (MODE == ROWS) {
-            constexpr int CH = GROWS * C::LPR;                 // 16-B chunks per wave
-            constexpr int NQ = (CH + 63) / 64;
-            float4 v[NQ];
-            const float* xb = x + r0 * ldx;                    // uniform base, 32-bit offsets
-            const int nr = static_cast<int>(row_end - r0 < GROWS ? row_end - r0 : GROWS);
+        auto gather = [&](int64_t tile, const TileIdx& ix, float* A) {
+            int lane_ = lane;
+            asm volatile("" : "+v"(lane_));   // keep lane-derived offsets out of LICM
+            const int c = lane_ % C::LPR, grp = lane_ / C::LPR;
+            const int64_t r0 = first_row(tile);
+            if constexpr (MODE == ROWS) {
+                constexpr int CH = PROWS * C::LPR;
+                constexpr int NQ = (CH + 63) / 64;
+                const float* xb = x + r0 * ldx;
+                const int nr = static_cast<int>(row_end - r0 < PROWS ? row_end - r0 : PROWS);
+                float4 v[NQ];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int id = q * 64 + lane_;
-                const int lr = id / C::LPR, cc = id % C::LPR;
-                v[q] = (id < CH && lr < nr) ? ld4(xb + (lr * static_cast<int>(ldx) + 4 * cc))
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int id = q * 64 + lane_;
-                const int lr = id / C::LPR, cc = id % C::LPR;
-                if (id < CH) st4(&A[(wave * GROWS + lr) * C::A_LD + 4 * cc], v[q]);
-            }
-        } else {
-            const int e0 = __shfl(idx.rp, 0, 64);
-            const int ne = __shfl(idx.rp, GROWS, 64) - e0;
-            const bool in_regs = ne <= 64;                     // wave-uniform
-            // Wave-uniform edge-loop bound: the ids live in lanes across the
-            // whole wave, so every lane must stay in the loop while any row
-            // group still reads them through ds_bpermute.
-            int dmax = lane_ < GROWS ? __shfl(idx.rp, lane_ + 1, 64) - idx.rp : 0;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o, 64));
-#pragma unroll 1
-            for (int st = 0; st < C::RSTEPS; st += C::RIF) {
-                int lrow[C::RIF], beg[C::RIF], deg[C::RIF];
-                float di[C::RIF];
-                float4 acc[C::RIF];
-#pragma unroll
-                for (int q = 0; q < C::RIF; ++q) {
-                    lrow[q] = (st + q) * C::RPW + grp;         // row inside the wave slice
-                    const int b = __shfl(idx.rp, lrow[q], 64);
-                    beg[q] = b - e0;
-                    deg[q] = __shfl(idx.rp, lrow[q] + 1, 64) - b;
-                    di[q] = __shfl(idx.dr, lrow[q], 64);
-                    acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-                for (int u0 = 0; u0 < dmax; u0 += 8) {
-                    float4 v[C::RIF][8];
-                    float w[C::RIF][8];
-#pragma unroll
-                    for (int q = 0; q < C::RIF; ++q)
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) {
-                            const bool ok = u0 + u < deg[q];
-                            const int e = beg[q] + (ok ? u0 + u : 0);
-                            int jj;
-                            float dj;
-                            if (in_regs) {
-                                jj = __shfl(idx.j, e, 64);
-                                dj = __shfl(idx.dj, e, 64);
-                            } else {
-                                jj = col[e0 + e];
-                                dj = MODE == AGG_GCN ? dinv[jj] : 1.f;
-                            }
-                            // PyG gcn_norm: dinv[src] * 1 * dinv[dst]
-                            w[q][u] = ok ? (MODE == AGG_GCN ? dj * di[q] : 1.f) : 0.f;
-                            v[q][u] = ok ? ld4(x + (int64_t)jj * ldx + 4 * c)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-                        }
-#pragma unroll
-                    for (int q = 0; q < C::RIF; ++q)
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) {
-                            if (u0 + u < deg[q]) {
-                                if constexpr (MODE == AGG_GCN) {
-                                    acc[q] = fma4(w[q][u], v[q][u], acc[q]);
-                                } else {
-                                    acc[q].x += v[q][u].x; acc[q].y += v[q][u].y;
-                                    acc[q].z += v[q][u].z; acc[q].w += v[q][u].w;
-                                }
-                            }
-                        }
+                for (int q = 0; q < NQ; ++q) {
+                    const int id = q * 64 + lane_;
+                    const int lr = id / C::LPR, cc = id % C::LPR;
+                    v[q] = (id < CH && lr < nr) ? ld4(xb + (lr * static_cast<int>(ldx) + 4 * cc))
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
-                for (int q = 0; q < C::RIF; ++q) {
-                    const int64_t row = r0 + lrow[q];
-                    if constexpr (MODE == AGG_SUM) {
-                        // GINConv: out = sum_j x_j; out = out + (1 + eps) * x_i
-                        if (row < row_end) {
-                            const float4 xi = ld4(x + row * ldx + 4 * c);
-                            acc[q].x = acc[q].x + self_scale * xi.x;
-                            acc[q].y = acc[q].y + self_scale * xi.y;
-                            acc[q].z = acc[q].z + self_scale * xi.z;
-                            acc[q].w = acc[q].w + self_scale * xi.w;
-                        }
+                for (int q = 0; q < NQ; ++q) {
+                    const int id = q * 64 + lane_;
+                    const int lr = id / C::LPR, cc = id % C::LPR;
+                    if (id < CH) st4(&A[(pw * PROWS + lr) * C::LD + 4 * cc], v[q]);
+                }
+            } else {
+                const int e0 = __shfl(ix.rp, 0, 64);
+                const int ne = __shfl(ix.rp, PROWS, 64) - e0;
+                const int safe_row = static_cast<int>(row_end - 1);   // valid x row
+                const bool in_regs = ne <= 64 * IREG;              // wave-uniform
+                // wave-uniform edge-loop bound: ids live in lanes across the whole
+                // wave, so every lane stays in the loop while any row reads them
+                int dmax = lane_ < PROWS ? __shfl(ix.rp, lane_ + 1, 64) - ix.rp : 0;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o, 64));
+                if (in_regs) {
+#pragma unroll
+                for (int st = 0; st < C::RSTEPS; st += C::RIF) {
+                    int lrow[C::RIF], beg[C::RIF], deg[C::RIF];
+                    float4 acc[C::RIF];
+#pragma unroll
+                    for (int q = 0; q < C::RIF; ++q) {
+                        lrow[q] = (st + q) * C::RPW + grp;
+                        const int lq = lrow[q] < PROWS ? lrow[q] : PROWS - 1;
+                        const int bq = __shfl(ix.rp, lq, 64);
+                        beg[q] = bq - e0;
+                        deg[q] = lrow[q] < PROWS ? __shfl(ix.rp, lq + 1, 64) - bq : 0;
+                        acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
                     }
-                    st4(&A[(wave * GROWS + lrow[q]) * C::A_LD + 4 * c], acc[q]);
+                    for (int u0 = 0; u0 < dmax; u0 += 8) {
+                        // (1) issue every neighbour-row load of the RIF row steps; invalid
+                        //     slots re-read a valid entry and get weight 0 below, so the
+                        //     loads need no select and only the data stays live
+                        float4 v[C::RIF][8];
+#pragma unroll
+                        for (int q = 0; q < C::RIF; ++q)
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
+                                const int s0 = __shfl(ix.j[0], e & 63, 64);
+                                const int s1 = IREG > 1 ? __shfl(ix.j[IREG - 1], e & 63, 64) : s0;
+                                // empty / masked row: re-read a valid row (row_end-1), weight 0
+                                const int jj = deg[q] > 0 ? (e < 64 ? s0 : s1) : safe_row;
+                                v[q][u] = ld4(x + (int64_t)jj * ldx + 4 * c);
+                            }
+                        // (2) weights after the loads are in flight; accumulate in CSR order
+#pragma unroll
+                        for (int q = 0; q < C::RIF; ++q)
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const bool ok = u0 + u < deg[q];
+                                float ww = 1.f;
+                                if constexpr (MODE == AGG_GCN) {
+                                    const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
+                                    const float w0 = __shfl(ix.w[0], e & 63, 64);
+                                    const float w1 = IREG > 1 ? __shfl(ix.w[IREG - 1], e & 63, 64) : w0;
+                                    ww = e < 64 ? w0 : w1;
+                                }
+                                // invalid slot: weight 0 (GIN: fma(1, x, acc) == acc + x exactly)
+                                acc[q] = fma4(ok ? ww : 0.f, v[q][u], acc[q]);
+                            }
+                    }
+#pragma unroll
+                    for (int q = 0; q < C::RIF; ++q) {
+                        if constexpr (MODE == AGG_SUM) {
+                            // GINConv: out = sum_j x_j; out = out + (1 + eps) * x_i
+                            const int64_t row = r0 + lrow[q];
+                            if (row < row_end) {
+                                const float4 xi = ld4(x + row * ldx + 4 * c);
+                                acc[q].x = acc[q].x + self_scale * xi.x;
+                                acc[q].y = acc[q].y + self_scale * xi.y;
+                                acc[q].z = acc[q].z + self_scale * xi.z;
+                                acc[q].w = acc[q].w + self_scale * xi.w;
+                            }
+                        }
+                        if (lrow[q] < PROWS) st4(&A[(pw * PROWS + lrow[q]) * C::LD + 4 * c], acc[q]);
+                    }
+                }
+                } else {   // > 64 CSR entries in this wave's rows: indices from memory
+#pragma unroll
+                for (int st = 0; st < C::RSTEPS; st += 1) {
+                    int lrow[1], beg[1], deg[1];
+                    float4 acc[1];
+#pragma unroll
+                    for (int q = 0; q < 1; ++q) {
+                        lrow[q] = (st + q) * C::RPW + grp;
+                        const int lq = lrow[q] < PROWS ? lrow[q] : PROWS - 1;
+                        const int bq = __shfl(ix.rp, lq, 64);
+                        beg[q] = bq - e0;
+                        deg[q] = lrow[q] < PROWS ? __shfl(ix.rp, lq + 1, 64) - bq : 0;
+                        acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                    for (int u0 = 0; u0 < dmax; u0 += 8) {
+                        // (1) issue every neighbour-row load of the RIF row steps; invalid
+                        //     slots re-read a valid entry and get weight 0 below, so the
+                        //     loads need no select and only the data stays live
+                        float4 v[1][8];
+#pragma unroll
+                        for (int q = 0; q < 1; ++q)
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
+                                const int jj = deg[q] > 0 ? col[e0 + e] : safe_row;
+                                v[q][u] = ld4(x + (int64_t)jj * ldx + 4 * c);
+                            }
+                        // (2) weights after the loads are in flight; accumulate in CSR order
+#pragma unroll
+                        for (int q = 0; q < 1; ++q)
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const bool ok = u0 + u < deg[q];
+                                float ww = 1.f;
+                                if constexpr (MODE == AGG_GCN) {
+                                    const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
+                                    ww = ok ? ew[e0 + e] : 0.f;
+                                }
+                                // invalid slot: weight 0 (GIN: fma(1, x, acc) == acc + x exactly)
+                                acc[q] = fma4(ok ? ww : 0.f, v[q][u], acc[q]);
+                            }
+                    }
+#pragma unroll
+                    for (int q = 0; q < 1; ++q) {
+                        if constexpr (MODE == AGG_SUM) {
+                            // GINConv: out = sum_j x_j; out = out + (1 + eps) * x_i
+                            const int64_t row = r0 + lrow[q];
+                            if (row < row_end) {
+                                const float4 xi = ld4(x + row * ldx + 4 * c);
+                                acc[q].x = acc[q].x + self_scale * xi.x;
+                                acc[q].y = acc[q].y + self_scale * xi.y;
+                                acc[q].z = acc[q].z + self_scale * xi.z;
+                                acc[q].w = acc[q].w + self_scale * xi.w;
+                            }
+                        }
+                        if (lrow[q] < PROWS) st4(&A[(pw * PROWS + lrow[q]) * C::LD + 4 * c], acc[q]);
+                    }
+                }
                 }
             }
+        };
+
+        // index pipeline: cur = tile s+1 entries, nrp = row_ptr of tile s+2
+        TileIdx cur{}, nxt{};
+        int rp2 = 0;
+        const bool prod = !(flags & MIGNN_DIAG_NO_PRODUCE);
+        if (MODE != ROWS) {
+            cur.rp = load_rp(row_ptr, first_row(tile_of(0)), row_end, lane);
+            nxt.rp = load_rp(row_ptr, first_row(tile_of(1)), row_end, lane);
+            load_entries<MODE>(cur, col, ew, lane);
+            load_entries<MODE>(nxt, col, ew, lane);
+            rp2 = load_rp(row_ptr, first_row(tile_of(2)), row_end, lane);
         }
+        if (prod && tile_of(0) < ntiles) gather(tile_of(0), cur, A0);
         __syncthreads();
+        for (int64_t s = 0; s < nsteps; ++s) {
+            const int64_t tn = tile_of(s + 1);
+            TileIdx nn{};
+            if (MODE != ROWS) {
+                nn.rp = rp2;                                          // tile s+2
+                load_entries<MODE>(nn, col, ew, lane);
+                rp2 = load_rp(row_ptr, first_row(tile_of(s + 3)), row_end, lane);
+            }
+            if (prod && s + 1 < nsteps && tn < ntiles)
+                gather(tn, nxt, A0 + ((s + 1) & 1) * C::A_FLOATS);
+            nxt = nn;
+            __syncthreads();
+        }
+        return;
+    }
 
-        // next tile's CSR indices: row_ptr now, neighbour ids after the MFMAs
-        const int64_t tile_next = tile_of(s + 1);
-        if (MODE != ROWS && tile_next < ntiles)
-            load_rp<MODE>(idx, row_ptr, dinv, row_begin + tile_next * BM + wave * GROWS, row_end,
-                          lane);
-
-        if (mw) {
-            // residual prefetch: D[row = 4g + q][col = r] of every (ib, jb)
-            const int64_t m0 = t0 + wm * C::WROWS;            // uniform
+    // ================================================================ consumer
+    const int wm = wave / C::WN, wn = wave % C::WN;
+    const bool mw = wave < C::MW && !(flags & MIGNN_DIAG_NO_MFMA);
+    __syncthreads();   // W staged, tile 0 produced
+    for (int64_t s = 0; s < nsteps; ++s) {
+        const int64_t tile = tile_of(s);
+        if (mw && tile < ntiles) {
+            const float* A = A0 + (s & 1) * C::A_FLOATS;
+            int lane_ = lane;
+            asm volatile("" : "+v"(lane_));
+            const int rr = lane_ & 15, gg = lane_ >> 4;
+            const int64_t m0 = row_begin + tile * BM + wm * C::WROWS;      // uniform
             const int mr = static_cast<int>(row_end - m0 < C::WROWS ? row_end - m0 : C::WROWS);
+            // residual prefetch for D[row = 4g + q][col = r]
             float res[C::IB][C::JB][4];
             const float* Rb = (flags & MIGNN_EPI_RESIDUAL) ? R + m0 * ldr : nullptr;
 #pragma unroll
@@ -272,65 +352,70 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
                 for (int jb = 0; jb < C::JB; ++jb)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const int lr = ib * 16 + 4 * g + q;
-                        const int n = wn * C::WCOLS + jb * 16 + r;
+                        const int lr = ib * 16 + 4 * gg + q;
+                        const int n = wn * C::WCOLS + jb * 16 + rr;
                         res[ib][jb][q] = (Rb && lr < mr && n < n_valid)
                                              ? Rb[lr * static_cast<int>(ldr) + n] : 0.f;
                     }
-            f32x4 accm[C::IB][C::JB];
+            f32x4 acc[C::IB][C::JB];
 #pragma unroll
             for (int ib = 0; ib < C::IB; ++ib)
 #pragma unroll
-                for (int jb = 0; jb < C::JB; ++jb) accm[ib][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int jb = 0; jb < C::JB; ++jb) acc[ib][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kc = 0; kc < C::KC; ++kc) {
-                float4 a[C::IB];
+                float4 a[C::IB], b[C::JB];
 #pragma unroll
                 for (int ib = 0; ib < C::IB; ++ib)
                     a[ib] = *reinterpret_cast<const float4*>(
-                        &A[(wm * C::WROWS + ib * 16 + r) * C::A_LD + kc * 16 + 4 * g]);
+                        &A[(wm * C::WROWS + ib * 16 + rr) * C::LD + kc * 16 + 4 * gg]);
 #pragma unroll
-                for (int jb = 0; jb < C::JB; ++jb) {
+                for (int jb = 0; jb < C::JB; ++jb)
+                    b[jb] = *reinterpret_cast<const float4*>(
+                        &Wl[(wn * C::WCOLS + jb * 16 + rr) * C::LD + kc * 16 + 4 * gg]);
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) accm[ib][jb] = mfma16x16x4(a[ib].x, breg[jb][kc].x, accm[ib][jb]);
+                for (int jb = 0; jb < C::JB; ++jb)
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) accm[ib][jb] = mfma16x16x4(a[ib].y, breg[jb][kc].y, accm[ib][jb]);
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].x, b[jb].x, acc[ib][jb]);
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) accm[ib][jb] = mfma16x16x4(a[ib].z, breg[jb][kc].z, accm[ib][jb]);
+                for (int jb = 0; jb < C::JB; ++jb)
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) accm[ib][jb] = mfma16x16x4(a[ib].w, breg[jb][kc].w, accm[ib][jb]);
-                }
-                // keep the A fragments of one k-chunk live at a time (VGPR cap 128)
-                __builtin_amdgcn_sched_barrier(0);
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].y, b[jb].y, acc[ib][jb]);
+#pragma unroll
+                for (int jb = 0; jb < C::JB; ++jb)
+#pragma unroll
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].z, b[jb].z, acc[ib][jb]);
+#pragma unroll
+                for (int jb = 0; jb < C::JB; ++jb)
+#pragma unroll
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].w, b[jb].w, acc[ib][jb]);
             }
-            // epilogue straight from the accumulators
+            float* ob = out + m0 * ldo;
 #pragma unroll
             for (int jb = 0; jb < C::JB; ++jb) {
-                const int n = wn * C::WCOLS + jb * 16 + r;
+                const int n = wn * C::WCOLS + jb * 16 + rr;
                 if (n >= n_valid) continue;
                 const float bv = (flags & MIGNN_EPI_BIAS) ? bias[n] : 0.f;
                 const float sc = (flags & MIGNN_EPI_AFFINE) ? scale[n] : 1.f;
                 const float sh = (flags & MIGNN_EPI_AFFINE) ? shift[n] : 0.f;
-                float* ob = out + m0 * ldo;
 #pragma unroll
                 for (int ib = 0; ib < C::IB; ++ib)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const int lr = ib * 16 + 4 * g + q;
-                        if (lr < mr)
-                            ob[lr * static_cast<int>(ldo) + n] =
-                                epilogue(accm[ib][jb][q], flags, bv, res[ib][jb][q], sc, sh);
+                        const int lr = ib * 16 + 4 * gg + q;
+                        if (lr < mr)   // non-temporal: keep L2 / MALL for the gathered rows
+                            __builtin_nontemporal_store(
+                                epilogue(acc[ib][jb][q], flags, bv, res[ib][jb][q], sc, sh),
+                                ob + lr * static_cast<int>(ldo) + n);
                     }
             }
         }
-        if (MODE != ROWS && tile_next < ntiles) load_cols<MODE>(idx, col, dinv, lane);
         __syncthreads();
-        tile = tile_next;
     }
 }
 
 struct TileArgs {
-    const int32_t* row_ptr; const int32_t* col; const float* dinv; float self_scale;
+    const int32_t* row_ptr; const int32_t* col; const float* ew; float self_scale;
     const float* x; int64_t ldx; int64_t rb, re;
     const float* W; const float* bias; const float* R; int64_t ldr;
     const float* scale; const float* shift; int flags; int n_valid; float* out; int64_t ldo;
@@ -354,7 +439,7 @@ int launch_tile(const TileArgs& a, hipStream_t st) {
     const int64_t ntiles = (a.re - a.rb + BM - 1) / BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHREADS), 0, st, a.row_ptr, a.col, a.dinv,
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHREADS), 0, st, a.row_ptr, a.col, a.ew,
                        a.self_scale, a.x, a.ldx, a.rb, a.re, a.W, a.bias, a.R, a.ldr, a.scale,
                        a.shift, a.flags, a.n_valid, a.out, a.ldo);
     return launch_status("fused_tile_kernel");
@@ -405,12 +490,12 @@ int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, i
 
 using namespace mignn;
 
-extern "C" int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* dinv,
+extern "C" int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
                                const float* x, int64_t ldx, int64_t rb, int64_t re, int h,
                                const float* w, const float* bias, const float* scale,
                                const float* shift, int flags, float* out, int64_t ldo,
                                void* stream) {
-    MIGNN_REQUIRE(row_ptr && col && dinv && x && w && out, "gcn_layer: null pointer");
+    MIGNN_REQUIRE(row_ptr && col && ew && x && w && out, "gcn_layer: null pointer");
     MIGNN_REQUIRE(aligned16(x) && aligned16(w), "gcn_layer: unaligned x / w");
     MIGNN_REQUIRE(ldx % 4 == 0 && ldx >= h && ldo >= h, "gcn_layer: bad strides");
     MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_layer: bad row range");
@@ -423,7 +508,7 @@ extern "C" int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const
                   "mignn_gcn_aggregate + mignn_linear", h);
         return MIGNN_ERR_UNSUPPORTED;
     }
-    TileArgs t{row_ptr, col, dinv, 1.f, x, ldx, rb, re, w, bias, x, ldx, scale, shift, flags, h,
+    TileArgs t{row_ptr, col, ew, 1.f, x, ldx, rb, re, w, bias, x, ldx, scale, shift, flags, h,
                out, ldo};
     return dispatch_tile<AGG_GCN>(h, h, t, as_stream(stream));
 }

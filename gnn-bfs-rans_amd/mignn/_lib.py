@@ -44,8 +44,15 @@ SIGNATURES = {
                                 c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),
+    "mignn_gcn_norm": (c_int, [_P, _P, _P, c_int64, c_int64, _P, _P]),
     "mignn_rows_gather": (c_int, [_P, c_int64, _P, c_int64, c_int, _P, c_int64, _P]),
     "mignn_grid_graph": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, _P, _P]),
+}
+
+# diagnostic entry points (include/mignn_diag.h; timing studies only)
+DIAG_SIGNATURES = {
+    "mignn_diag_gather": (c_int, [c_int, _P, _P, _P, _P, c_int64, c_int, c_int, c_int, c_int, _P,
+                                  _P]),
 }
 
 _lib = None
@@ -65,7 +72,7 @@ def lib():
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
                 "There is no CPU fallback.")
         h = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in {**SIGNATURES, **DIAG_SIGNATURES}.items():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args

@@ -126,7 +126,7 @@ def sharded_forward(ex: LayerExecutor, part: SlabPartition, x_own: torch.Tensor,
     """Forward of one rank's slab; returns the rank's [n_own, out] rows."""
     H = ex.hidden_dim
     dev = x_own.device
-    a = torch.empty((part.n_total, H), dtype=torch.float32, device=dev)
+    a = torch.empty((part.n_total, H), dtype=x_own.dtype, device=dev)
     b = torch.empty_like(a)
     ex.input_proj(x_own, a[:part.n_own])
     cur, nxt = a, b
@@ -166,6 +166,7 @@ class FlowGNNExecutor(LayerExecutor):
             d = self.csr.dinv[:part.n_total].view(-1, 1)
             for w in halo_exchange(d, part, group):
                 w.wait()
+            self.csr.compute_gcn_weights(0, part.n_own)   # entries of owned rows, true ghost dinv
 
     def input_proj(self, x_own, out):
         self.model._input_proj(x_own.contiguous(), out)

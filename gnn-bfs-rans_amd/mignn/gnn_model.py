@@ -112,11 +112,22 @@ class BatchNorm(nn.Module):
 # ---------------------------------------------------------------------------
 
 class Csr:
-    __slots__ = ("row_ptr", "col", "dinv", "info", "num_nodes", "num_edges", "edge_index")
+    __slots__ = ("row_ptr", "col", "dinv", "ew", "info", "num_nodes", "num_edges", "edge_index")
 
-    def __init__(self, row_ptr, col, dinv, info, num_nodes, num_edges, edge_index):
+    def __init__(self, row_ptr, col, dinv, info, num_nodes, num_edges, edge_index, ew=None):
         self.row_ptr, self.col, self.dinv, self.info = row_ptr, col, dinv, info
         self.num_nodes, self.num_edges, self.edge_index = num_nodes, num_edges, edge_index
+        self.ew = ew
+
+    def compute_gcn_weights(self, row_begin: int = 0, row_end: Optional[int] = None):
+        """Per-entry PyG gcn_norm weights (mignn_gcn_norm); call again after the
+        halo dinv exchange of a sharded graph."""
+        re = self.num_nodes if row_end is None else row_end
+        if self.ew is None:
+            self.ew = torch.empty_like(self.col, dtype=torch.float32)
+        _lib.check(_lib.lib().mignn_gcn_norm(_lib.ptr(self.row_ptr), _lib.ptr(self.col),
+                                             _lib.ptr(self.dinv), row_begin, re, _lib.ptr(self.ew),
+                                             _lib.stream(self.col.device)), "mignn_gcn_norm")
 
 
 def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
@@ -139,7 +150,10 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
     _lib.check(L.mignn_csr_build(_lib.ptr(ei), E, N, mode, _lib.ptr(row_ptr), _lib.ptr(col),
                                  _lib.ptr(dinv), _lib.ptr(info), _lib.ptr(scratch), nbytes,
                                  _lib.stream(dev)), "mignn_csr_build")
-    return Csr(row_ptr, col, dinv, info, N, E, ei)
+    csr = Csr(row_ptr, col, dinv, info, N, E, ei)
+    if mode == CSR_ONE_SELF_LOOP:
+        csr.compute_gcn_weights()
+    return csr
 
 
 class _CsrCache:
@@ -390,7 +404,7 @@ class FlowGNN(nn.Module):
         if self.layer_type == "GCN":
             w, b = layer.lin.weight, layer.bias
             if H in (64, 128):
-                _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.dinv), P(x),
+                _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x),
                                              x.stride(0), rb, re, H, P(w), P(b), P(scale),
                                              P(shift), epi, P(out), out.stride(0), st),
                            "mignn_gcn_layer")

@@ -74,7 +74,11 @@ enum {
     MIGNN_EPI_BIAS = 1,
     MIGNN_EPI_RESIDUAL = 2,
     MIGNN_EPI_AFFINE = 4, /* BatchNorm eval affine: v*scale + shift */
-    MIGNN_EPI_RELU = 8
+    MIGNN_EPI_RELU = 8,
+    /* diagnostic ablations of the fused tile kernels (timing studies only;
+     * results are wrong by design): skip the A-tile producer / the MFMA+store */
+    MIGNN_DIAG_NO_PRODUCE = 256,
+    MIGNN_DIAG_NO_MFMA = 512
 };
 int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
                  const float* a2, int64_t lda2, int k2,
@@ -118,15 +122,21 @@ int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t* col, cons
                                 int64_t row_end, int h, int heads, float score_scale,
                                 float* out, int64_t ldo, void* stream);
 
+/* PyG gcn_norm edge weights per CSR entry (rows [row_begin, row_end)):
+ *   ew[e] = dinv[col[e]] * dinv[i]   (= dinv[src] * 1 * dinv[dst], GCNConv gnn_model.py:63) */
+int mignn_gcn_norm(const int32_t* row_ptr, const int32_t* col, const float* dinv,
+                   int64_t row_begin, int64_t row_end, float* ew, void* stream);
+
 /* ------------------------------------------------------------------------
  * Fused GCN layer (the north-star hot kernel):
- *   out_i = relu( ((x_i + (sum_j w_ji x_j) W^T + bias) * scale + shift) )
+ *   out_i = relu( ((x_i + (sum_{e in row i} ew_e x_{col e}) W^T + bias) * scale + shift) )
  * i.e. GCNConv + residual + BatchNorm(eval) + ReLU of gnn_model.py:166,184-191
  * in one pass: CSR gather into an LDS tile, MFMA transform, fused epilogue.
+ * ew: per-CSR-entry weights from mignn_gcn_norm.
  * flags: MIGNN_EPI_* (BIAS|RESIDUAL|AFFINE|RELU as the model configures).
  * h in {64, 128} (other h: mignn_gcn_aggregate + mignn_linear).
  * ------------------------------------------------------------------------ */
-int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* dinv,
+int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
                     const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
                     const float* w, const float* bias, const float* scale, const float* shift,
                     int flags, float* out, int64_t ldo, void* stream);

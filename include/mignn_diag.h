@@ -1,0 +1,17 @@
+/* Diagnostic entry points of libmignn.so (timing studies only, not product
+ * ABI).  See gnn-bfs-rans_amd/csrc/diag.hip. */
+#ifndef MIGNN_DIAG_H
+#define MIGNN_DIAG_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* mode 0: CSR gather (h = 128); 1: stencil gather on the periodic grid;
+ * 2: streaming copy.  blocks <= 0: one row group per row. */
+int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t* col, const float* ew,
+                      const float* x, int64_t n, int nx, int ny, int nz, int blocks, float* out,
+                      void* stream);
+#ifdef __cplusplus
+}
+#endif
+#endif

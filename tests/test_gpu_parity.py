@@ -126,7 +126,7 @@ def test_gcn_fused_layer_vs_fp64(H):
     P = _lib.ptr
     for rb, re in ((0, n), (17, n - 100)):
         out.fill_(float("nan"))
-        _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.dinv), P(X), H, rb, re, H,
+        _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, rb, re, H,
                                      P(W), P(b), P(sc), P(sh), 15, P(out), H, _lib.stream()),
                    "gcn_layer")
         Xd = X.double().cpu()
