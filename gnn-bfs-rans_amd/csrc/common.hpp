@@ -63,6 +63,54 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
+// Raw buffer loads through a hand-built 128-bit descriptor (the clang
+// __builtin_amdgcn_raw_buffer_load_b64 of this toolchain lowers to a 4-byte
+// load, so the LLVM intrinsics are bound directly).  Descriptor: base (48
+// bit, stride 0), num_records = bytes, dword3 = 0x00020000 (gfx9 raw buffer).
+using i32x4 = __attribute__((ext_vector_type(4))) int;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+__device__ f32x2 raw_buffer_load_f32x2(i32x4 rsrc, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.raw.buffer.load.v2f32");
+__device__ float raw_buffer_load_f32(i32x4 rsrc, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.raw.buffer.load.f32");
+
+__device__ __forceinline__ i32x4 buffer_rsrc(uint64_t base, uint32_t bytes) {
+    return i32x4{static_cast<int>(static_cast<uint32_t>(base)),
+                 static_cast<int>(static_cast<uint32_t>(base >> 32) & 0xffffu),
+                 static_cast<int>(bytes), 0x00020000};
+}
+
+// VPL (1 or 2) consecutive floats, one 4-/8-B access
+template <int VPL>
+__device__ __forceinline__ void ldv(const float* p, float (&v)[VPL]) {
+    static_assert(VPL == 1 || VPL == 2, "VPL");
+    if constexpr (VPL == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(p);
+        v[0] = t.x;
+        v[1] = t.y;
+    } else {
+        v[0] = *p;
+    }
+}
+template <int VPL>
+__device__ __forceinline__ void stv(float* p, const float (&v)[VPL]) {
+    if constexpr (VPL == 2) *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+    else *p = v[0];
+}
+
+// p[n .. n+3] with components >= n_valid read as 0; a 16-B load when all four
+// are valid and p + n is 16-B aligned, scalar loads otherwise.
+__device__ __forceinline__ float4 ld4_masked(const float* p, int n, int n_valid) {
+    const float* q = p + n;
+    if (n + 4 <= n_valid && (reinterpret_cast<uintptr_t>(q) & 15u) == 0) return ld4(q);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n + 0 < n_valid) v.x = q[0];
+    if (n + 1 < n_valid) v.y = q[1];
+    if (n + 2 < n_valid) v.z = q[2];
+    if (n + 3 < n_valid) v.w = q[3];
+    return v;
+}
+
 __device__ __forceinline__ float4 fma4(float s, float4 x, float4 acc) {
     acc.x = fmaf(s, x.x, acc.x);
     acc.y = fmaf(s, x.y, acc.y);

@@ -41,68 +41,85 @@
 //     tiles, so the +-1 / +-row neighbours a run gathers share that XCD's L2
 //     and the chip sweeps a single front (+-plane neighbours stay in the
 //     256 MB Infinity Cache).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace mignn {
 namespace {
 
 constexpr int BM = 48;                 // rows per tile
-constexpr int NCW = 4;                 // consumer waves (one per SIMD: MFMA issue saturates)
-constexpr int NPW = 12;                // producer waves
+constexpr int NCW = 8;                 // consumer (MFMA) waves: two per SIMD
+constexpr int NPW = 8;                 // producer (gather) waves
 constexpr int NTHREADS = (NCW + NPW) * 64;
-constexpr int PROWS = BM / NPW;        // rows per producer wave (4)
-constexpr int IREG = 1;                // index registers per lane: 64 CSR entries per wave
+constexpr int PROWS = BM / NPW;        // rows per producer wave (6)
+static_assert(NCW * PROWS == BM, "consumer waves store PROWS rows each");
+constexpr int SLOTS = 7;               // neighbour rows per row and chunk: 42 loads in flight
 
 enum { AGG_GCN = 0, AGG_SUM = 1, ROWS = 2 };
+
+// Diagnostic timeline (MIGNN_DIAG_TRACE): s_memtime stamps of one producer and
+// one consumer wave of workgroups 0..7, steps 0..63 -> g_trace[(b*64+s)*8+slot]
+__device__ unsigned long long* g_trace = nullptr;
+__device__ __forceinline__ void stamp(int flags, int lane, int64_t s, int slot) {
+    if ((flags & MIGNN_DIAG_TRACE) && blockIdx.x < 8 && s < 64 && lane == 0 && g_trace)
+        g_trace[(blockIdx.x * 64 + s) * 8 + slot] = __builtin_amdgcn_s_memtime();
+}
 
 template <int K, int N, int MODE>
 struct Cfg {
     static_assert(K % 16 == 0 && K <= 256 && N % 16 == 0, "K, N multiples of 16, K <= 256");
     static constexpr int WN = N / 16 < NCW ? N / 16 : NCW;    // consumer column slices
-    static constexpr int WM = 1;                               // consumers own all 48 rows
+    static constexpr int WM = 1;                               // consumers own all BM rows
     static constexpr int MW = WM * WN;                         // consumer waves with work
     static constexpr int WROWS = BM / WM;
     static constexpr int WCOLS = N / WN;
     static constexpr int IB = WROWS / 16;
     static constexpr int JB = WCOLS / 16;
     static constexpr int KC = K / 16;
-    static constexpr int LPR = K / 4;                          // lanes per A row (16 B each)
+    static constexpr int LPR = K / 4;                          // ROWS: lanes per A row (16 B each)
+    static constexpr int VPL = K / 64;                         // AGG: floats per lane of a row
     static constexpr int RPW = 64 / LPR;                       // rows per wave instruction
     static constexpr int RSTEPS = PROWS >= RPW ? PROWS / RPW : 1;   // row steps per producer wave
     static constexpr int RIF = RSTEPS;                         // every row step in flight
     static constexpr int LD = K + 8;                           // LDS row stride (floats)
     static constexpr int A_FLOATS = BM * LD;
-    static constexpr int W_FLOATS = N * LD;
-    static constexpr int LDS_FLOATS = 2 * A_FLOATS + W_FLOATS;
+    static constexpr int LDN = N + 8;                          // R / C tile row stride
+    static constexpr int R_FLOATS = BM * LDN;
+    static constexpr int NC4 = N / 4;                          // 16-B chunks per R / C row
+    // double-buffered A tile; 3-deep ring of R/C tiles (residual in, result
+    // out): at step s the producers fill R[(s+1)%3], the consumers compute in
+    // R[s%3] and store the finished R[(s-1)%3]
+    static constexpr int LDS_FLOATS = 2 * A_FLOATS + 3 * R_FLOATS;
     static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
 };
 
-struct TileIdx {            // CSR indices of one producer wave's 8 rows, in lane registers
-    int rp;                 // lanes 0..8: row_ptr[r0 + lane] (clamped to row_end)
-    int j[IREG];            // lane t: col[e0 + t + 64 q]
-    float w[IREG];          // lane t: ew[e0 + t + 64 q]  (GCN weights)
+// Per-producer-wave CSR indices of one tile, one CSR entry per lane:
+// lanes 0..PROWS of rpv hold row_ptr[r0 + lane] (clamped to row_end); lane t of
+// ej / ew holds entry e0 + t of the wave's rows (t < 64).  Loaded one tile
+// ahead (rpv two ahead), read with v_readlane at wave-uniform lane ids.
+struct WaveIdx {
+    int rpv;
+    int ej;
+    float ew;
 };
 
-__device__ __forceinline__ int load_rp(const int32_t* __restrict__ row_ptr, int64_t r0,
-                                       int64_t row_end, int lane) {
-    const int64_t rr = r0 + lane < row_end ? r0 + lane : row_end;
-    return (r0 < row_end && lane <= PROWS) ? row_ptr[rr] : 0;
+__device__ __forceinline__ int load_rpv(const int32_t* __restrict__ row_ptr, int64_t r0,
+                                        int64_t row_end, int lane) {
+    const int64_t r = r0 + lane < row_end ? r0 + lane : row_end;
+    return lane <= PROWS ? row_ptr[r] : 0;
 }
 
 template <int MODE>
-__device__ __forceinline__ void load_entries(TileIdx& t, const int32_t* __restrict__ col,
-                                             const float* __restrict__ ew, int lane) {
-    const int e0 = __shfl(t.rp, 0, 64);
-    const int ne = __shfl(t.rp, PROWS, 64) - e0;
-#pragma unroll
-    for (int q = 0; q < IREG; ++q) {
-        const int e = lane + 64 * q;
-        t.j[q] = e < ne ? col[e0 + e] : 0;
-        t.w[q] = (MODE == AGG_GCN && e < ne) ? ew[e0 + e] : 1.f;
-    }
+__device__ __forceinline__ void load_wave_entries(WaveIdx& t, const int32_t* __restrict__ col,
+                                                  const float* __restrict__ ew, int lane) {
+    const int e0 = __builtin_amdgcn_readlane(t.rpv, 0);
+    const int ne = __builtin_amdgcn_readlane(t.rpv, PROWS) - e0;
+    t.ej = lane < ne ? col[e0 + lane] : 0;
+    t.ew = (MODE == AGG_GCN && lane < ne) ? ew[e0 + lane] : 1.f;
 }
 
-template <int K, int N, int MODE>
+template <int K, int N, int MODE, bool VEC>
 // 16 waves per CU = 4 per SIMD -> <= 128 VGPRs: 16 gathered rows in flight per
 // producer wave (12 producers: 192 KB per CU)
 __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
@@ -115,7 +132,8 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
     using C = Cfg<K, N, MODE>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
     float* const A0 = lds;
-    float* const Wl = lds + 2 * C::A_FLOATS;
+    float* const R0 = lds + 2 * C::A_FLOATS;
+    const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -127,22 +145,26 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
     const int xcd = blockIdx.x & 7;
     const int slot = blockIdx.x >> 3;
     const int per_xcd = G >> 3;
-    const int64_t nsteps = (ntiles + G - 1) / G;
-    auto tile_of = [&](int64_t s) -> int64_t { return s * G + (int64_t)xcd * per_xcd + slot; };
-
-    // W -> LDS (rows n >= n_valid padded with zeros)
-    for (int i = tid; i < N * (K / 4); i += NTHREADS) {
-        const int n = i / (K / 4), k4 = i % (K / 4);
-        st4(&Wl[n * C::LD + 4 * k4], n < n_valid ? ld4(W + (int64_t)n * K + 4 * k4)
-                                               : make_float4(0.f, 0.f, 0.f, 0.f));
-    }
+    // interleaved (default): at step s the chip covers tiles [sG, (s+1)G), XCD x a
+    // contiguous run of G/8 of them.  XCD-major: XCD x sweeps its own contiguous
+    // 1/8 of the tiles, G/8 per step (a locality-ordered graph keeps each XCD's
+    // working set in its own L2).  Tiles past the range map to ntiles (skipped).
+    const bool xmajor = (flags & MIGNN_SCHED_XCD_MAJOR) != 0;
+    const int64_t tx = (ntiles + 7) / 8;
+    const int64_t nsteps = xmajor ? (tx + per_xcd - 1) / per_xcd : (ntiles + G - 1) / G;
+    auto tile_of = [&](int64_t s) -> int64_t {
+        if (!xmajor) return s * G + (int64_t)xcd * per_xcd + slot;
+        const int64_t l = s * per_xcd + slot;
+        const int64_t t = (int64_t)xcd * tx + l;
+        return l < tx && t < ntiles ? t : ntiles;
+    };
 
     if (wave >= NCW) {
         // ============================================================ producer
         const int pw = wave - NCW;
         auto first_row = [&](int64_t tile) { return row_begin + tile * BM + pw * PROWS; };
 
-        auto gather = [&](int64_t tile, const TileIdx& ix, float* A) {
+        auto gather = [&](int64_t tile, const WaveIdx& ix, float* A, float* Rt) {
             int lane_ = lane;
             asm volatile("" : "+v"(lane_));   // keep lane-derived offsets out of LICM
             const int c = lane_ % C::LPR, grp = lane_ / C::LPR;
@@ -167,163 +189,184 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
                     if (id < CH) st4(&A[(pw * PROWS + lr) * C::LD + 4 * cc], v[q]);
                 }
             } else {
-                const int e0 = __shfl(ix.rp, 0, 64);
-                const int ne = __shfl(ix.rp, PROWS, 64) - e0;
+                // one row per wave instruction: row bounds, column ids and edge
+                // weights are wave-uniform (scalar loads into SGPRs, SALU address
+                // arithmetic); per neighbour row the vector work is one 8-B load
+                // and VPL fmas per lane.  All PROWS x 8 loads are issued before
+                // the first fma.
+                constexpr int VPL = C::VPL;
                 const int safe_row = static_cast<int>(row_end - 1);   // valid x row
-                const bool in_regs = ne <= 64 * IREG;              // wave-uniform
-                // wave-uniform edge-loop bound: ids live in lanes across the whole
-                // wave, so every lane stays in the loop while any row reads them
-                int dmax = lane_ < PROWS ? __shfl(ix.rp, lane_ + 1, 64) - ix.rp : 0;
+                int rp[PROWS + 1];
 #pragma unroll
-                for (int o = 32; o > 0; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o, 64));
+                for (int q = 0; q <= PROWS; ++q) rp[q] = __builtin_amdgcn_readlane(ix.rpv, q);
+                const int e0 = rp[0];
+                // wave-uniform: every entry of the wave's rows in lanes 0..62; lanes
+                // past them hold column 0 / weight 0 (a valid row, never summed)
+                const bool in_regs = rp[PROWS] - e0 < 64;
+                int deg[PROWS], dmax = 0;
+#pragma unroll
+                for (int q = 0; q < PROWS; ++q) {
+                    deg[q] = rp[q + 1] - rp[q];
+                    dmax = max(dmax, deg[q]);
+                }
+                float acc[PROWS][VPL];
+#pragma unroll
+                for (int q = 0; q < PROWS; ++q)
+#pragma unroll
+                    for (int t = 0; t < VPL; ++t) acc[q][t] = 0.f;
+                const int loff = lane_ * (4 * VPL);   // byte offset of this lane's floats
+                const uint32_t ldxb = static_cast<uint32_t>(ldx) * 4u;
+                // one buffer descriptor per gathered row, built with SALU only: the
+                // row base (32x32->64-bit product) is wave-uniform, the lane offset
+                // is the 32-bit voffset
+                const uint64_t xbase = reinterpret_cast<uint64_t>(x);
+                auto xload = [&](uint32_t r, float (&v)[VPL]) {
+                    const i32x4 rs = buffer_rsrc(xbase + (uint64_t)r * ldxb, K * 4);
+                    if constexpr (VPL == 2) {
+                        const f32x2 t = raw_buffer_load_f32x2(rs, loff, 0, 0);
+                        v[0] = t[0];
+                        v[1] = t[1];
+                    } else {
+                        v[0] = raw_buffer_load_f32(rs, loff, 0, 0);
+                    }
+                };
+                // slot u of row q reads entry rp[q] + min(u, deg-1): slots past the row
+                // re-read its last entry (loads stay unconditional), weight 0
+                int tq[PROWS], dm1[PROWS];
+#pragma unroll
+                for (int q = 0; q < PROWS; ++q) {
+                    tq[q] = rp[q] - e0;
+                    dm1[q] = max(deg[q] - 1, 0);
+                }
                 if (in_regs) {
+                    for (int u0 = 0; u0 < dmax; u0 += SLOTS) {   // dmax > 0: the range has entries
+                        float v[PROWS][SLOTS][VPL];
 #pragma unroll
-                for (int st = 0; st < C::RSTEPS; st += C::RIF) {
-                    int lrow[C::RIF], beg[C::RIF], deg[C::RIF];
-                    float4 acc[C::RIF];
+                        for (int q = 0; q < PROWS; ++q)
 #pragma unroll
-                    for (int q = 0; q < C::RIF; ++q) {
-                        lrow[q] = (st + q) * C::RPW + grp;
-                        const int lq = lrow[q] < PROWS ? lrow[q] : PROWS - 1;
-                        const int bq = __shfl(ix.rp, lq, 64);
-                        beg[q] = bq - e0;
-                        deg[q] = lrow[q] < PROWS ? __shfl(ix.rp, lq + 1, 64) - bq : 0;
-                        acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                    for (int u0 = 0; u0 < dmax; u0 += 8) {
-                        // (1) issue every neighbour-row load of the RIF row steps; invalid
-                        //     slots re-read a valid entry and get weight 0 below, so the
-                        //     loads need no select and only the data stays live
-                        float4 v[C::RIF][8];
-#pragma unroll
-                        for (int q = 0; q < C::RIF; ++q)
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
-                                const int s0 = __shfl(ix.j[0], e & 63, 64);
-                                const int s1 = IREG > 1 ? __shfl(ix.j[IREG - 1], e & 63, 64) : s0;
-                                // empty / masked row: re-read a valid row (row_end-1), weight 0
-                                const int jj = deg[q] > 0 ? (e < 64 ? s0 : s1) : safe_row;
-                                v[q][u] = ld4(x + (int64_t)jj * ldx + 4 * c);
+                            for (int u = 0; u < SLOTS; ++u) {
+                                const int t = tq[q] + min(u0 + u, dm1[q]);
+                                xload(static_cast<uint32_t>(__builtin_amdgcn_readlane(ix.ej, t)),
+                                      v[q][u]);
                             }
-                        // (2) weights after the loads are in flight; accumulate in CSR order
+                        // CSR order; weight-0 slots leave acc unchanged (finite x);
+                        // GIN: fma(1, x, acc) == acc + x exactly
 #pragma unroll
-                        for (int q = 0; q < C::RIF; ++q)
+                        for (int q = 0; q < PROWS; ++q) {
+                            // one row's weights at a time (keeps SGPR pressure low)
+                            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                const bool ok = u0 + u < deg[q];
-                                float ww = 1.f;
+                            for (int u = 0; u < SLOTS; ++u) {
+                                float we = 1.f;
                                 if constexpr (MODE == AGG_GCN) {
-                                    const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
-                                    const float w0 = __shfl(ix.w[0], e & 63, 64);
-                                    const float w1 = IREG > 1 ? __shfl(ix.w[IREG - 1], e & 63, 64) : w0;
-                                    ww = e < 64 ? w0 : w1;
+                                    const int t = tq[q] + min(u0 + u, dm1[q]);
+                                    we = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                                       __builtin_bit_cast(int, ix.ew), t));
                                 }
-                                // invalid slot: weight 0 (GIN: fma(1, x, acc) == acc + x exactly)
-                                acc[q] = fma4(ok ? ww : 0.f, v[q][u], acc[q]);
-                            }
-                    }
+                                const float w = u0 + u < deg[q] ? we : 0.f;
 #pragma unroll
-                    for (int q = 0; q < C::RIF; ++q) {
-                        if constexpr (MODE == AGG_SUM) {
-                            // GINConv: out = sum_j x_j; out = out + (1 + eps) * x_i
-                            const int64_t row = r0 + lrow[q];
-                            if (row < row_end) {
-                                const float4 xi = ld4(x + row * ldx + 4 * c);
-                                acc[q].x = acc[q].x + self_scale * xi.x;
-                                acc[q].y = acc[q].y + self_scale * xi.y;
-                                acc[q].z = acc[q].z + self_scale * xi.z;
-                                acc[q].w = acc[q].w + self_scale * xi.w;
+                                for (int t = 0; t < VPL; ++t)
+                                    acc[q][t] = fmaf(w, v[q][u][t], acc[q][t]);
                             }
                         }
-                        if (lrow[q] < PROWS) st4(&A[(pw * PROWS + lrow[q]) * C::LD + 4 * c], acc[q]);
-                    }
-                }
-                } else {   // > 64 CSR entries in this wave's rows: indices from memory
+                        // GCN residual x_i: the last slot re-reads the row's last entry,
+                        // which in the CSR the layer takes (MIGNN_CSR_ONE_SELF_LOOP,
+                        // mignn.h) is its self loop, appended after the edges as
+                        // add_remaining_self_loops does
+                        if (MODE == AGG_GCN && has_res) {
 #pragma unroll
-                for (int st = 0; st < C::RSTEPS; st += 1) {
-                    int lrow[1], beg[1], deg[1];
-                    float4 acc[1];
-#pragma unroll
-                    for (int q = 0; q < 1; ++q) {
-                        lrow[q] = (st + q) * C::RPW + grp;
-                        const int lq = lrow[q] < PROWS ? lrow[q] : PROWS - 1;
-                        const int bq = __shfl(ix.rp, lq, 64);
-                        beg[q] = bq - e0;
-                        deg[q] = lrow[q] < PROWS ? __shfl(ix.rp, lq + 1, 64) - bq : 0;
-                        acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                    for (int u0 = 0; u0 < dmax; u0 += 8) {
-                        // (1) issue every neighbour-row load of the RIF row steps; invalid
-                        //     slots re-read a valid entry and get weight 0 below, so the
-                        //     loads need no select and only the data stays live
-                        float4 v[1][8];
-#pragma unroll
-                        for (int q = 0; q < 1; ++q)
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
-                                const int jj = deg[q] > 0 ? col[e0 + e] : safe_row;
-                                v[q][u] = ld4(x + (int64_t)jj * ldx + 4 * c);
-                            }
-                        // (2) weights after the loads are in flight; accumulate in CSR order
-#pragma unroll
-                        for (int q = 0; q < 1; ++q)
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                const bool ok = u0 + u < deg[q];
-                                float ww = 1.f;
-                                if constexpr (MODE == AGG_GCN) {
-                                    const int e = beg[q] + min(u0 + u, max(deg[q] - 1, 0));
-                                    ww = ok ? ew[e0 + e] : 0.f;
-                                }
-                                // invalid slot: weight 0 (GIN: fma(1, x, acc) == acc + x exactly)
-                                acc[q] = fma4(ok ? ww : 0.f, v[q][u], acc[q]);
-                            }
-                    }
-#pragma unroll
-                    for (int q = 0; q < 1; ++q) {
-                        if constexpr (MODE == AGG_SUM) {
-                            // GINConv: out = sum_j x_j; out = out + (1 + eps) * x_i
-                            const int64_t row = r0 + lrow[q];
-                            if (row < row_end) {
-                                const float4 xi = ld4(x + row * ldx + 4 * c);
-                                acc[q].x = acc[q].x + self_scale * xi.x;
-                                acc[q].y = acc[q].y + self_scale * xi.y;
-                                acc[q].z = acc[q].z + self_scale * xi.z;
-                                acc[q].w = acc[q].w + self_scale * xi.w;
-                            }
+                            for (int q = 0; q < PROWS; ++q)
+                                stv<VPL>(&Rt[(pw * PROWS + q) * C::LDN + VPL * lane_],
+                                         v[q][SLOTS - 1]);
                         }
-                        if (lrow[q] < PROWS) st4(&A[(pw * PROWS + lrow[q]) * C::LD + 4 * c], acc[q]);
+                    }
+                } else {
+                    // > 63 entries in the wave's rows (hubs): one neighbour row at a
+                    // time, indices by scalar loads -- correct, not fast
+#pragma unroll 1
+                    for (int q = 0; q < PROWS; ++q) {
+#pragma unroll 1
+                        for (int u = 0; u < deg[q]; ++u) {
+                            const int e = rp[q] + u;
+                            float vv[VPL];
+                            xload(static_cast<uint32_t>(col[e]), vv);
+                            const float w = MODE == AGG_GCN ? ew[e] : 1.f;
+#pragma unroll
+                            for (int t = 0; t < VPL; ++t) acc[q][t] = fmaf(w, vv[t], acc[q][t]);
+                            if (MODE == AGG_GCN && has_res && u == deg[q] - 1)
+                                stv<VPL>(&Rt[(pw * PROWS + q) * C::LDN + VPL * lane_], vv);
+                        }
                     }
                 }
+#pragma unroll
+                for (int q = 0; q < PROWS; ++q) {
+                    const int64_t row = r0 + q;
+                    if constexpr (MODE == AGG_SUM) {
+                        // GINConv: out = sum_j x_j; out = out + (1 + eps) * x_i
+                        if (row < row_end) {
+                            float xi[VPL];
+                            xload(static_cast<uint32_t>(row), xi);
+#pragma unroll
+                            for (int t = 0; t < VPL; ++t) acc[q][t] = acc[q][t] + self_scale * xi[t];
+                        }
+                    }
+                    stv<VPL>(&A[(pw * PROWS + q) * C::LD + VPL * lane_], acc[q]);
+                }
+            }
+            // residual rows -> R tile (contiguous 16-B chunks); GCN: copied from
+            // the self-loop slot of the gather above (R == x, one self loop per row)
+            if (MODE != AGG_GCN && has_res) {
+                constexpr int CH = PROWS * C::NC4;
+                constexpr int NQ = (CH + 63) / 64;
+                float4 v[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int id = q * 64 + lane_;
+                    const int lr = id / C::NC4, cc = id % C::NC4;
+                    const int64_t row = r0 + lr;
+                    v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (id < CH && row < row_end) {
+                        if constexpr (VEC) v[q] = ld4(R + row * ldr + 4 * cc);
+                        else v[q] = ld4_masked(R + row * ldr, 4 * cc, n_valid);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int id = q * 64 + lane_;
+                    const int lr = id / C::NC4, cc = id % C::NC4;
+                    if (id < CH) st4(&Rt[(pw * PROWS + lr) * C::LDN + 4 * cc], v[q]);
                 }
             }
         };
 
-        // index pipeline: cur = tile s+1 entries, nrp = row_ptr of tile s+2
-        TileIdx cur{}, nxt{};
-        int rp2 = 0;
+        // index pipeline: x rows of tile s+1 gather while the entries of tile s+2
+        // and row_ptr of tile s+3 load
         const bool prod = !(flags & MIGNN_DIAG_NO_PRODUCE);
-        if (MODE != ROWS) {
-            cur.rp = load_rp(row_ptr, first_row(tile_of(0)), row_end, lane);
-            nxt.rp = load_rp(row_ptr, first_row(tile_of(1)), row_end, lane);
-            load_entries<MODE>(cur, col, ew, lane);
-            load_entries<MODE>(nxt, col, ew, lane);
-            rp2 = load_rp(row_ptr, first_row(tile_of(2)), row_end, lane);
+        WaveIdx cur{}, nxt{};
+        int rp3 = 0;
+        if constexpr (MODE != ROWS) {   // cur = tile 0, nxt = tile 1, rp3 = tile 2
+            cur.rpv = load_rpv(row_ptr, first_row(tile_of(0)), row_end, lane);
+            rp3 = load_rpv(row_ptr, first_row(tile_of(1)), row_end, lane);
+            load_wave_entries<MODE>(cur, col, ew, lane);
+            nxt.rpv = rp3;
+            load_wave_entries<MODE>(nxt, col, ew, lane);
+            rp3 = load_rpv(row_ptr, first_row(tile_of(2)), row_end, lane);
         }
-        if (prod && tile_of(0) < ntiles) gather(tile_of(0), cur, A0);
-        __syncthreads();
-        for (int64_t s = 0; s < nsteps; ++s) {
+        // step s gathers tile s+1 (s = -1: the prologue), stores tile s-1
+        for (int64_t s = -1; s < nsteps; ++s) {
             const int64_t tn = tile_of(s + 1);
-            TileIdx nn{};
-            if (MODE != ROWS) {
-                nn.rp = rp2;                                          // tile s+2
-                load_entries<MODE>(nn, col, ew, lane);
-                rp2 = load_rp(row_ptr, first_row(tile_of(s + 3)), row_end, lane);
+            if (pw == 0 && s >= 0) stamp(flags, lane, s, 0);
+            WaveIdx nn{};
+            if constexpr (MODE != ROWS) {
+                nn.rpv = rp3;                                         // tile s+2
+                load_wave_entries<MODE>(nn, col, ew, lane);
+                rp3 = load_rpv(row_ptr, first_row(tile_of(s + 4)), row_end, lane);
             }
+            float* const Rn = R0 + ((s + 1) % 3) * C::R_FLOATS;
             if (prod && s + 1 < nsteps && tn < ntiles)
-                gather(tn, nxt, A0 + ((s + 1) & 1) * C::A_FLOATS);
+                gather(tn, cur, A0 + ((s + 1) & 1) * C::A_FLOATS, Rn);
+            if (pw == 0 && s >= 0) stamp(flags, lane, s, 1);
+            cur = nxt;
             nxt = nn;
             __syncthreads();
         }
@@ -331,87 +374,142 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
     }
 
     // ================================================================ consumer
+    // No global memory traffic here: A and the residual come from LDS, the
+    // result goes back to LDS (the producers store whole rows next step).
     const int wm = wave / C::WN, wn = wave % C::WN;
     const bool mw = wave < C::MW && !(flags & MIGNN_DIAG_NO_MFMA);
-    __syncthreads();   // W staged, tile 0 produced
+    int lane_ = lane;
+    asm volatile("" : "+v"(lane_));
+    const int rr = lane_ & 15, gg = lane_ >> 4;
+    // this wave's W slice as MFMA A-operand fragments, held for the whole launch:
+    // lane (r, g) holds W[n = slice + 16 jb + r][k = 16 kc + 4 g .. +3]; operands
+    // swapped (acc = W_slice . A^T): lane (r, g) owns output row 16 ib + r,
+    // columns 16 jb + 4 g .. +3
+    float4 wf[C::JB][C::KC];
+    float4 bv[C::JB], sc[C::JB], sh[C::JB];
+#pragma unroll
+    for (int jb = 0; jb < C::JB; ++jb) {
+        const int nw = wn * C::WCOLS + jb * 16 + rr;
+#pragma unroll
+        for (int kc = 0; kc < C::KC; ++kc)
+            wf[jb][kc] = (mw && nw < n_valid) ? ld4(W + (int64_t)nw * K + kc * 16 + 4 * gg)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int n = wn * C::WCOLS + jb * 16 + 4 * gg;
+        bv[jb] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sc[jb] = make_float4(1.f, 1.f, 1.f, 1.f);
+        sh[jb] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (mw) {
+            if constexpr (VEC) {
+                if (flags & MIGNN_EPI_BIAS) bv[jb] = ld4(bias + n);
+                if (flags & MIGNN_EPI_AFFINE) { sc[jb] = ld4(scale + n); sh[jb] = ld4(shift + n); }
+            } else {
+                if (flags & MIGNN_EPI_BIAS) bv[jb] = ld4_masked(bias, n, n_valid);
+                if (flags & MIGNN_EPI_AFFINE) {
+                    sc[jb] = ld4_masked(scale, n, n_valid);
+                    sh[jb] = ld4_masked(shift, n, n_valid);
+                }
+            }
+        }
+    }
+// consumer wave w stores rows 6w..6w+5 of a finished tile: C tile (LDS) ->
+// out, whole rows.  Consumers issue no loads, so these stores never sit
+// in front of a vmcnt wait (loads and stores share the in-order counter)
+    auto store_out = [&](int64_t tile, const float* Ct) {
+        int lane_ = lane;
+        asm volatile("" : "+v"(lane_));
+        const int64_t r0 = row_begin + tile * BM + wave * PROWS;
+        constexpr int CH = PROWS * C::NC4;
+        constexpr int NQ = (CH + 63) / 64;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int id = q * 64 + lane_;
+            const int lr = id / C::NC4, cc = id % C::NC4;
+            const int64_t row = r0 + lr;
+            if (id < CH && row < row_end) {
+                const float4 t = ld4(&Ct[(wave * PROWS + lr) * C::LDN + 4 * cc]);
+                float* o = out + row * ldo + 4 * cc;
+                if constexpr (VEC) {
+                    // non-temporal: keep L2 / MALL for the gathered rows
+                    __builtin_nontemporal_store(f32x4{t.x, t.y, t.z, t.w},
+                                                reinterpret_cast<f32x4*>(o));
+                } else {
+                    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (4 * cc + u < n_valid) __builtin_nontemporal_store(tv[u], o + u);
+                }
+            }
+        }
+    };
+
+    __syncthreads();   // tile 0 produced
     for (int64_t s = 0; s < nsteps; ++s) {
+        if (wave == 0) stamp(flags, lane, s, 2);
+        if (s >= 1 && tile_of(s - 1) < ntiles)
+            store_out(tile_of(s - 1), R0 + ((s + 2) % 3) * C::R_FLOATS);   // (s-1)%3
         const int64_t tile = tile_of(s);
         if (mw && tile < ntiles) {
             const float* A = A0 + (s & 1) * C::A_FLOATS;
-            int lane_ = lane;
-            asm volatile("" : "+v"(lane_));
-            const int rr = lane_ & 15, gg = lane_ >> 4;
-            const int64_t m0 = row_begin + tile * BM + wm * C::WROWS;      // uniform
-            const int mr = static_cast<int>(row_end - m0 < C::WROWS ? row_end - m0 : C::WROWS);
-            // residual prefetch for D[row = 4g + q][col = r]
-            float res[C::IB][C::JB][4];
-            const float* Rb = (flags & MIGNN_EPI_RESIDUAL) ? R + m0 * ldr : nullptr;
-#pragma unroll
-            for (int ib = 0; ib < C::IB; ++ib)
-#pragma unroll
-                for (int jb = 0; jb < C::JB; ++jb)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int lr = ib * 16 + 4 * gg + q;
-                        const int n = wn * C::WCOLS + jb * 16 + rr;
-                        res[ib][jb][q] = (Rb && lr < mr && n < n_valid)
-                                             ? Rb[lr * static_cast<int>(ldr) + n] : 0.f;
-                    }
+            float* const Rt = R0 + (s % 3) * C::R_FLOATS;
             f32x4 acc[C::IB][C::JB];
 #pragma unroll
             for (int ib = 0; ib < C::IB; ++ib)
 #pragma unroll
                 for (int jb = 0; jb < C::JB; ++jb) acc[ib][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // A fragments of step kc + 1 are read while step kc's MFMAs run
+            float4 fa[2][C::IB];
+            auto load_frag = [&](int buf, int kc) {
+#pragma unroll
+                for (int ib = 0; ib < C::IB; ++ib)
+                    fa[buf][ib] = *reinterpret_cast<const float4*>(
+                        &A[(wm * C::WROWS + ib * 16 + rr) * C::LD + kc * 16 + 4 * gg]);
+            };
+            load_frag(0, 0);
 #pragma unroll
             for (int kc = 0; kc < C::KC; ++kc) {
-                float4 a[C::IB], b[C::JB];
-#pragma unroll
-                for (int ib = 0; ib < C::IB; ++ib)
-                    a[ib] = *reinterpret_cast<const float4*>(
-                        &A[(wm * C::WROWS + ib * 16 + rr) * C::LD + kc * 16 + 4 * gg]);
-#pragma unroll
-                for (int jb = 0; jb < C::JB; ++jb)
-                    b[jb] = *reinterpret_cast<const float4*>(
-                        &Wl[(wn * C::WCOLS + jb * 16 + rr) * C::LD + kc * 16 + 4 * gg]);
+                const int cb = kc & 1;
+                if (kc + 1 < C::KC) load_frag(cb ^ 1, kc + 1);
 #pragma unroll
                 for (int jb = 0; jb < C::JB; ++jb)
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].x, b[jb].x, acc[ib][jb]);
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(wf[jb][kc].x, fa[cb][ib].x, acc[ib][jb]);
 #pragma unroll
                 for (int jb = 0; jb < C::JB; ++jb)
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].y, b[jb].y, acc[ib][jb]);
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(wf[jb][kc].y, fa[cb][ib].y, acc[ib][jb]);
 #pragma unroll
                 for (int jb = 0; jb < C::JB; ++jb)
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].z, b[jb].z, acc[ib][jb]);
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(wf[jb][kc].z, fa[cb][ib].z, acc[ib][jb]);
 #pragma unroll
                 for (int jb = 0; jb < C::JB; ++jb)
 #pragma unroll
-                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(a[ib].w, b[jb].w, acc[ib][jb]);
+                    for (int ib = 0; ib < C::IB; ++ib) acc[ib][jb] = mfma16x16x4(wf[jb][kc].w, fa[cb][ib].w, acc[ib][jb]);
             }
-            float* ob = out + m0 * ldo;
+            if (wave == 0) stamp(flags, lane, s, 3);
+            // epilogue in place in the R/C tile: each lane reads its residual
+            // chunk and writes the result to the same 16 B (no other wave
+            // touches them this step)
 #pragma unroll
             for (int jb = 0; jb < C::JB; ++jb) {
-                const int n = wn * C::WCOLS + jb * 16 + rr;
-                if (n >= n_valid) continue;
-                const float bv = (flags & MIGNN_EPI_BIAS) ? bias[n] : 0.f;
-                const float sc = (flags & MIGNN_EPI_AFFINE) ? scale[n] : 1.f;
-                const float sh = (flags & MIGNN_EPI_AFFINE) ? shift[n] : 0.f;
+                const int n = wn * C::WCOLS + jb * 16 + 4 * gg;
 #pragma unroll
-                for (int ib = 0; ib < C::IB; ++ib)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int lr = ib * 16 + 4 * gg + q;
-                        if (lr < mr)   // non-temporal: keep L2 / MALL for the gathered rows
-                            __builtin_nontemporal_store(
-                                epilogue(acc[ib][jb][q], flags, bv, res[ib][jb][q], sc, sh),
-                                ob + lr * static_cast<int>(ldo) + n);
-                    }
+                for (int ib = 0; ib < C::IB; ++ib) {
+                    float* const rc = &Rt[(wm * C::WROWS + ib * 16 + rr) * C::LDN + n];
+                    const float4 rv = has_res ? ld4(rc) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    st4(rc, make_float4(
+                                epilogue(acc[ib][jb][0], flags, bv[jb].x, rv.x, sc[jb].x, sh[jb].x),
+                                epilogue(acc[ib][jb][1], flags, bv[jb].y, rv.y, sc[jb].y, sh[jb].y),
+                                epilogue(acc[ib][jb][2], flags, bv[jb].z, rv.z, sc[jb].z, sh[jb].z),
+                                epilogue(acc[ib][jb][3], flags, bv[jb].w, rv.w, sc[jb].w, sh[jb].w)));
+                }
             }
+            if (wave == 0) stamp(flags, lane, s, 4);
         }
         __syncthreads();
     }
+    if (nsteps >= 1 && tile_of(nsteps - 1) < ntiles)
+        store_out(tile_of(nsteps - 1), R0 + ((nsteps - 1) % 3) * C::R_FLOATS);
 }
 
 struct TileArgs {
@@ -421,9 +519,9 @@ struct TileArgs {
     const float* scale; const float* shift; int flags; int n_valid; float* out; int64_t ldo;
 };
 
-template <int K, int N, int MODE>
-int launch_tile(const TileArgs& a, hipStream_t st) {
-    auto kern = fused_tile_kernel<K, N, MODE>;
+template <int K, int N, int MODE, bool VEC>
+int launch_tile_v(const TileArgs& a, hipStream_t st) {
+    auto kern = fused_tile_kernel<K, N, MODE, VEC>;
     static int grid_cache[64] = {0};
     int dev = 0;
     MIGNN_HIP(hipGetDevice(&dev));
@@ -443,6 +541,23 @@ int launch_tile(const TileArgs& a, hipStream_t st) {
                        a.self_scale, a.x, a.ldx, a.rb, a.re, a.W, a.bias, a.R, a.ldr, a.scale,
                        a.shift, a.flags, a.n_valid, a.out, a.ldo);
     return launch_status("fused_tile_kernel");
+}
+
+template <int K, int N, int MODE>
+int launch_tile(const TileArgs& a, hipStream_t st) {
+    // VEC: 16-B epilogue (every column valid, 16-B aligned rows and vectors)
+    auto al = [](const void* p) { return p == nullptr || aligned16(p); };
+    const bool vec = a.n_valid == N && al(a.out) && (a.ldo & 3) == 0 && al(a.R) &&
+                     (a.ldr & 3) == 0 && al(a.bias) && al(a.scale) && al(a.shift);
+    if constexpr (MODE == ROWS) {
+        return vec ? launch_tile_v<K, N, MODE, true>(a, st) : launch_tile_v<K, N, MODE, false>(a, st);
+    } else {
+        if (!vec) {
+            set_error("fused layer: out / bias / scale / shift must be 16-B aligned, ld %% 4 == 0");
+            return MIGNN_ERR_ARG;
+        }
+        return launch_tile_v<K, N, MODE, true>(a, st);
+    }
 }
 
 // Instances: (K, N) shapes of FlowGNN at hidden 64 / 128 (layers and output MLP).
@@ -489,6 +604,11 @@ int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, i
 }  // namespace mignn
 
 using namespace mignn;
+
+extern "C" int mignn_diag_set_trace(void* buf) {
+    MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)));
+    return MIGNN_OK;
+}
 
 extern "C" int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
                                const float* x, int64_t ldx, int64_t rb, int64_t re, int h,

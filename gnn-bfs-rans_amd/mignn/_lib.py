@@ -53,6 +53,7 @@ SIGNATURES = {
 DIAG_SIGNATURES = {
     "mignn_diag_gather": (c_int, [c_int, _P, _P, _P, _P, c_int64, c_int, c_int, c_int, c_int, _P,
                                   _P]),
+    "mignn_diag_set_trace": (c_int, [_P]),
 }
 
 _lib = None

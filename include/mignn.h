@@ -78,7 +78,9 @@ enum {
     /* diagnostic ablations of the fused tile kernels (timing studies only;
      * results are wrong by design): skip the A-tile producer / the MFMA+store */
     MIGNN_DIAG_NO_PRODUCE = 256,
-    MIGNN_DIAG_NO_MFMA = 512
+    MIGNN_DIAG_NO_MFMA = 512,
+    MIGNN_SCHED_XCD_MAJOR = 1024,
+    MIGNN_DIAG_TRACE = 2048
 };
 int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
                  const float* a2, int64_t lda2, int k2,

@@ -11,6 +11,11 @@ extern "C" {
 int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t* col, const float* ew,
                       const float* x, int64_t n, int nx, int ny, int nz, int blocks, float* out,
                       void* stream);
+/* Timeline buffer (uint64 [8 * 64 * 8], device memory) for launches with
+ * MIGNN_DIAG_TRACE: s_memtime stamps per workgroup 0..7 and step 0..63 --
+ * slot 0/1 producer step start / gather done, 2/3/4 consumer step start /
+ * MFMA done / epilogue done.  NULL disables. */
+int mignn_diag_set_trace(void* buf);
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,17 @@ nx, ny, nz = (int(v) for v in os.environ.get("KB_GRID", "250,200,200").split(","
 H = int(os.environ.get("KB_H", "128"))
 x0, ei = grid_graph(nx, ny, nz, device=dev, permute_seed=int(os.environ["KB_SHUFFLE"]) if os.environ.get("KB_SHUFFLE") else None)
 n = x0.shape[0]
+if os.environ.get("KB_PERM"):
+    # relabel the mesh into k-pencils of BI x BJ columns (locality experiment)
+    bi, bj = (int(v) for v in os.environ["KB_PERM"].split(","))
+    assert nx % bi == 0 and ny % bj == 0
+    ids = torch.arange(n, device=dev)
+    i, j, k = ids % nx, (ids // nx) % ny, ids // (nx * ny)
+    npi = nx // bi
+    key = ((((j // bj) * npi + (i // bi)) * nz + k) * bj + (j % bj)) * bi + (i % bi)
+    pos = torch.empty_like(ids)
+    pos[torch.argsort(key)] = ids
+    ei = pos[ei]
 csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
 del ei
 g = torch.Generator(device=dev).manual_seed(0)
@@ -61,6 +72,7 @@ def diag(mode_blocks):
 
 cases = {
     "gcn_full": (gcn, 15), "gcn_no_mfma": (gcn, 15 | 512), "gcn_no_gather": (gcn, 15 | 256),
+    "gcn_xmaj": (gcn, 15 | 1024), "gcn_xmaj_no_mfma": (gcn, 15 | 1024 | 512),
     "gcn_aggregate_only(simple)": (agg, 0), "linear_rows": (lin, 9),
     "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0),
     "diag_csr_gather": (diag, (0, 0)), "diag_csr_gather_g2048": (diag, (0, 2048)),
