@@ -151,20 +151,27 @@ class FlowGNNExecutor(LayerExecutor):
     """GPU executor: FlowGNN's native layers on a rank-local CSR."""
 
     def __init__(self, model, part: SlabPartition, edge_index_local: torch.Tensor, group=None):
-        from ._lib import CSR_ONE_SELF_LOOP, CSR_VERBATIM
-        from .gnn_model import build_csr
-
         self.model = model
         self.part = part
+        self.group = group
+        self.edge_index_local = edge_index_local
         self.num_layers = model.num_layers
         self.hidden_dim = model.hidden_dim
         self.overlap_ok = model.layer_type != "GAT"   # GAT logits read ghost rows
-        mode = CSR_ONE_SELF_LOOP if model.layer_type in ("GCN", "GAT") else CSR_VERBATIM
-        self.csr = build_csr(edge_index_local, part.n_total, mode)
+        self.build_graph()
+
+    def build_graph(self):
+        """Rank-local CSR (+ GCN norm with the ghost rows' true degrees)."""
+        from ._lib import CSR_ONE_SELF_LOOP, CSR_VERBATIM
+        from .gnn_model import build_csr
+
+        part = self.part
+        mode = CSR_ONE_SELF_LOOP if self.model.layer_type in ("GCN", "GAT") else CSR_VERBATIM
+        self.csr = build_csr(self.edge_index_local, part.n_total, mode)
         if self.csr.dinv is not None and part.world > 1:
-            # ghost rows' true deg^-1/2 comes from their owner (static, once)
+            # ghost rows' true deg^-1/2 comes from their owner
             d = self.csr.dinv[:part.n_total].view(-1, 1)
-            for w in halo_exchange(d, part, group):
+            for w in halo_exchange(d, part, self.group):
                 w.wait()
             self.csr.compute_gcn_weights(0, part.n_own)   # entries of owned rows, true ghost dinv
 

@@ -165,6 +165,8 @@ class _CsrCache:
         self.entries: Dict[Tuple, Csr] = {}
 
     def get(self, edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
+        if self.capacity <= 0:        # caching off: rebuild every forward
+            return build_csr(edge_index, num_nodes, mode)
         key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
                tuple(edge_index.stride()), edge_index.dtype, int(num_nodes), mode,
                str(edge_index.device))
