@@ -74,6 +74,20 @@ __device__ f32x2 raw_buffer_load_f32x2(i32x4 rsrc, int voffset, int soffset, int
 __device__ float raw_buffer_load_f32(i32x4 rsrc, int voffset, int soffset, int aux) __asm(
     "llvm.amdgcn.raw.buffer.load.f32");
 
+// Structured buffer (idxen): address = base + vindex * stride + voffset; a
+// lane whose vindex >= num_records reads zeros and generates no memory
+// request (per-lane range check: a branch-free "no load" for empty slots).
+__device__ f32x4 struct_buffer_load_f32x4(i32x4 rsrc, int vindex, int voffset, int soffset,
+                                          int aux) __asm("llvm.amdgcn.struct.buffer.load.v4f32");
+
+__device__ __forceinline__ i32x4 struct_rsrc(uint64_t base, uint32_t stride_bytes,
+                                             uint32_t num_records) {
+    return i32x4{static_cast<int>(static_cast<uint32_t>(base)),
+                 static_cast<int>((static_cast<uint32_t>(base >> 32) & 0xffffu) |
+                                  ((stride_bytes & 0x3fffu) << 16)),
+                 static_cast<int>(num_records), 0x00020000};
+}
+
 __device__ __forceinline__ i32x4 buffer_rsrc(uint64_t base, uint32_t bytes) {
     return i32x4{static_cast<int>(static_cast<uint32_t>(base)),
                  static_cast<int>(static_cast<uint32_t>(base >> 32) & 0xffffu),

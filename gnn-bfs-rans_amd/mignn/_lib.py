@@ -42,6 +42,8 @@ SIGNATURES = {
                                             c_int, c_int, c_float, _P, c_int64, _P]),
     "mignn_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P, _P,
                                 c_int, _P, c_int64, _P]),
+    "mignn_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
+                                      _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),
     "mignn_gcn_norm": (c_int, [_P, _P, _P, c_int64, c_int64, _P, _P]),
@@ -54,6 +56,7 @@ DIAG_SIGNATURES = {
     "mignn_diag_gather": (c_int, [c_int, _P, _P, _P, _P, c_int64, c_int, c_int, c_int, c_int, _P,
                                   _P]),
     "mignn_diag_set_trace": (c_int, [_P]),
+    "mignn_diag_set_trace_f16x3": (c_int, [_P]),
 }
 
 _lib = None

@@ -16,7 +16,15 @@ Drop-in for `gnn_model.FlowGNN` (reference gnn_model.py:14-220) and
 
 Every arithmetic step of `forward` runs in the HIP library (CSR build,
 aggregation, MFMA transforms, fused epilogues); PyTorch only allocates device
-memory and provides the stream.  There is no CPU path: tensors must be on a
+memory and provides the stream.
+
+Precision (`FlowGNN.precision`, default from $MIGNN_PRECISION, else
+"f16x3"): "f32" runs the node transforms on the exact-fp32 MFMA
+(v_mfma_f32_16x16x4_f32, a k-ordered fmaf chain); "f16x3" runs them as three
+fp16 MFMAs on power-of-two-scaled hi/lo splits of both operands with fp32
+accumulation (relative error per product ~2^-22, 16x the f32 MFMA rate),
+where a kernel exists for the shape (fused GCN layer, H in {64, 128}); the
+measured field error stays well inside the north star's 1e-5 either way.  There is no CPU path: tensors must be on a
 ROCm device and the library must be built.  Eval mode only (training /
 backward is SURVEY.md §8f-3, not built yet).
 
@@ -31,6 +39,7 @@ Weight re-association (one-time per weight version, float64 on the device):
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -281,6 +290,7 @@ class FlowGNN(nn.Module):
             nn.Linear(hidden_dim, hidden_dim // 2), nn.ReLU(),
             nn.Linear(hidden_dim // 2, output_dim))
         self.dropout = nn.Dropout(dropout)
+        self.precision = os.environ.get("MIGNN_PRECISION", "f16x3")
         self._csr = _CsrCache()
         self._prep: Dict[Tuple, object] = {}
 
@@ -348,6 +358,8 @@ class FlowGNN(nn.Module):
                 raise RuntimeError("mignn FlowGNN computes in fp32; parameters must be float32")
         if self.hidden_dim % 8 != 0:
             raise RuntimeError("mignn FlowGNN requires hidden_dim % 8 == 0")
+        if self.precision not in ("f32", "f16x3"):
+            raise ValueError(f"precision must be 'f32' or 'f16x3', got {self.precision!r}")
 
     def _layer_error(self, i, e, num_nodes, edge_index, x, edge_attr):
         E = edge_index.shape[1]
@@ -406,9 +418,9 @@ class FlowGNN(nn.Module):
         if self.layer_type == "GCN":
             w, b = layer.lin.weight, layer.bias
             if H in (64, 128):
-                _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x),
-                                             x.stride(0), rb, re, H, P(w), P(b), P(scale),
-                                             P(shift), epi, P(out), out.stride(0), st),
+                fn = L.mignn_gcn_layer_f16x3 if self.precision == "f16x3" else L.mignn_gcn_layer
+                _lib.check(fn(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
+                              P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),
                            "mignn_gcn_layer")
             else:
                 agg = torch.empty((n, H), dtype=torch.float32, device=x.device)

@@ -80,7 +80,11 @@ enum {
     MIGNN_DIAG_NO_PRODUCE = 256,
     MIGNN_DIAG_NO_MFMA = 512,
     MIGNN_SCHED_XCD_MAJOR = 1024,
-    MIGNN_DIAG_TRACE = 2048
+    MIGNN_DIAG_TRACE = 2048,
+    MIGNN_DIAG_NO_EXT = 4096,   /* f16x3 GCN layer: skip the out-of-tile gathers */
+    MIGNN_DIAG_NO_LOCAL = 8192,  /* f16x3 GCN layer: skip the in-tile (LDS) pass */
+    MIGNN_DIAG_NO_TABLES = 16384, /* f16x3 GCN layer: skip the lookup-table build */
+    MIGNN_DIAG_PLAIN_STORE = 32768 /* f16x3 GCN layer: plain (not non-temporal) row stores */
 };
 int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
                  const float* a2, int64_t lda2, int k2,
@@ -142,6 +146,20 @@ int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
                     const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
                     const float* w, const float* bias, const float* scale, const float* shift,
                     int flags, float* out, int64_t ldo, void* stream);
+
+/* Same layer, split-precision transform ("f16x3"): every fp32 operand of the
+ * node transform is split into two power-of-two-scaled fp16 halves and the
+ * product is formed by three fp16 MFMAs with fp32 accumulation (relative
+ * error per product ~2^-22, i.e. within a few fp32 ulps; 16x the f32 MFMA
+ * rate).  In-tile CSR entries (a locality order, mignn_locality_order, puts
+ * most of a mesh's entries there) are read from an LDS image of the tile's
+ * own rows; the rest are gathered.  Sum order: a row's in-tile entries in CSR
+ * order, then its out-of-tile entries in CSR order.  h in {64, 128}; same
+ * arguments and flags as mignn_gcn_layer. */
+int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                          const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                          const float* w, const float* bias, const float* scale,
+                          const float* shift, int flags, float* out, int64_t ldo, void* stream);
 
 /* Fused GIN layer (gnn_model.py:70-75, :166, :184-191), h in {64, 128}:
  *   tmp_i = relu(nn.0( sum_{j in row i} x_j + (1 + eps) x_i ))      (rows rb..re -> tmp[0..])

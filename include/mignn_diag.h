@@ -16,6 +16,10 @@ int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t* col, cons
  * slot 0/1 producer step start / gather done, 2/3/4 consumer step start /
  * MFMA done / epilogue done.  NULL disables. */
 int mignn_diag_set_trace(void* buf);
+/* The same for mignn_gcn_layer_f16x3 (uint64 [8 * 64 * 4]): slot 0/1 producer
+ * wave 0 step start / aggregation done, 2/3 consumer wave 0 after the
+ * residual hand-off / before the step's barrier. */
+int mignn_diag_set_trace_f16x3(void* buf);
 #ifdef __cplusplus
 }
 #endif

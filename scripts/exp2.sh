@@ -1,0 +1,11 @@
+set -u
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 120 python scripts/check_f16x3.py > gpurun_out/check.log 2>&1
+rc=$?; cat gpurun_out/check.log; if [ $rc -ne 0 ]; then exit $rc; fi
+export KB_ONLY=gcn_full,gcn16_full,copy KB_CHECK=1
+timeout -k 10 240 python scripts/kbench.py > gpurun_out/kb2_nat.json 2> gpurun_out/kb2_nat.err && \
+KB_MORTON=1 timeout -k 10 240 python scripts/kbench.py > gpurun_out/kb2_morton.json 2> gpurun_out/kb2_morton.err
+rc=$?
+cat gpurun_out/kb2_*.json; tail -3 gpurun_out/kb2_*.err
+exit $rc

@@ -31,6 +31,31 @@ if os.environ.get("KB_PERM"):
     pos = torch.empty_like(ids)
     pos[torch.argsort(key)] = ids
     ei = pos[ei]
+if os.environ.get("KB_MORTON"):
+    # relabel nodes in Morton (Z-curve) order of their grid cell (locality experiment)
+    ids = torch.arange(n, device=dev)
+    c = [ids % nx, (ids // nx) % ny, ids // (nx * ny)]
+
+    def spread(v):
+        v = v.to(torch.int64)
+        out = torch.zeros_like(v)
+        for bit in range(11):
+            out |= ((v >> bit) & 1) << (3 * bit)
+        return out
+    key = spread(c[0]) | (spread(c[1]) << 1) | (spread(c[2]) << 2)
+    pos = torch.empty_like(ids)
+    pos[torch.argsort(key, stable=True)] = ids
+    ei = pos[ei]
+if os.environ.get("KB_BLOCK"):
+    # relabel: 4x4x4 cell blocks in lexicographic block order, cells of a block consecutive
+    bs = int(os.environ["KB_BLOCK"])
+    ids = torch.arange(n, device=dev)
+    i, j, k = ids % nx, (ids // nx) % ny, ids // (nx * ny)
+    nbi, nbj = (nx + bs - 1) // bs, (ny + bs - 1) // bs
+    key = (((k // bs) * nbj + j // bs) * nbi + i // bs) * (bs ** 3) + ((k % bs) * bs + j % bs) * bs + i % bs
+    pos = torch.empty_like(ids)
+    pos[torch.argsort(key, stable=True)] = ids
+    ei = pos[ei]
 csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
 del ei
 g = torch.Generator(device=dev).manual_seed(0)
@@ -40,6 +65,7 @@ W = torch.randn(H, H, device=dev, generator=g) * 0.05
 b = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
+csum0 = [float(t.double().sum()) for t in (X, W, csr.ew, csr.col, csr.row_ptr)]
 L = _lib.lib()
 P = _lib.ptr
 st = _lib.stream()
@@ -48,6 +74,11 @@ st = _lib.stream()
 def gcn(flags):
     _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
                                  P(b), P(sc), P(sh), flags, P(Y), H, st), "gcn")
+
+
+def gcn16(flags):
+    _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                       P(W), P(b), P(sc), P(sh), flags, P(Y), H, st), "gcn16")
 
 
 def agg(_):
@@ -71,7 +102,13 @@ def diag(mode_blocks):
 
 
 cases = {
-    "gcn_full": (gcn, 15), "gcn_no_mfma": (gcn, 15 | 512), "gcn_no_gather": (gcn, 15 | 256),
+    "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_no_produce": (gcn16, 15 | 256),
+    "gcn16_no_mfma": (gcn16, 15 | 512), "gcn16_no_ext": (gcn16, 15 | 4096),
+    "gcn16_no_tables_ext": (gcn16, 15 | 4096 | 16384),
+    "gcn16_plain": (gcn16, 15 | 32768), "gcn16_no_produce_plain": (gcn16, 15 | 256 | 32768),
+    "gcn16_no_tables_ext_local": (gcn16, 15 | 4096 | 16384 | 8192),
+    "gcn16_no_local": (gcn16, 15 | 8192), "gcn16_no_ext_local": (gcn16, 15 | 4096 | 8192),
+    "gcn16_only_dma": (gcn16, 15 | 256 | 512), "gcn_no_mfma": (gcn, 15 | 512), "gcn_no_gather": (gcn, 15 | 256),
     "gcn_xmaj": (gcn, 15 | 1024), "gcn_xmaj_no_mfma": (gcn, 15 | 1024 | 512),
     "gcn_aggregate_only(simple)": (agg, 0), "linear_rows": (lin, 9),
     "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0),
@@ -97,4 +134,58 @@ for rnd in range(5):
         if rnd > 0:
             times[k].append(e0.elapsed_time(e1) / 3)
 res = {k: round(statistics.median(v), 4) for k, v in times.items()}
+if os.environ.get("KB_TRACE"):
+    buf = torch.zeros(8 * 64 * 8, dtype=torch.int64, device=dev)
+    _lib.check(L.mignn_diag_set_trace_f16x3(P(buf)), "trace")
+    gcn16(15 | 2048)
+    torch.cuda.synchronize()
+    _lib.check(L.mignn_diag_set_trace_f16x3(None), "trace")
+    t = buf.view(8, 64, 8).cpu().double()
+    d = {"p_tables_ext_issue": t[:, 1:60, 1] - t[:, 1:60, 0],
+         "p_quad0": t[:, 1:60, 2] - t[:, 1:60, 1],
+         "p_quad1": t[:, 1:60, 3] - t[:, 1:60, 2],
+         "p_barrier_wait": t[:, 2:61, 0] - t[:, 1:60, 3],
+         "c_start_to_spin_done": t[:, 1:60, 4] - t[:, 0:59, 7],
+         "c_dma_issue": t[:, 1:60, 5] - t[:, 1:60, 4],
+         "c_mfma": t[:, 1:60, 6] - t[:, 1:60, 5],
+         "c_epilogue": t[:, 1:60, 7] - t[:, 1:60, 6],
+         "step": t[:, 2:61, 0] - t[:, 1:60, 0]}
+    res["trace_cycles_median"] = {k: float(v.median()) for k, v in d.items()}
+if os.environ.get("KB_CHECK"):
+    # fresh outputs: the fp32 kernel into zeros, the f16x3 kernel into NaNs; fp64
+    # reference on 4096 sampled rows (CSR on the CPU)
+    Y32 = torch.zeros_like(X)
+    _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
+                                 P(b), P(sc), P(sh), 15, P(Y32), H, st), "gcn")
+    Y16 = torch.full_like(X, float("nan"))
+    _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                       P(W), P(b), P(sc), P(sh), 15, P(Y16), H, st), "gcn16")
+    torch.cuda.synchronize()
+    rows = torch.randint(0, n, (4096,), generator=torch.Generator().manual_seed(5))
+    rp = csr.row_ptr.cpu().long()
+    colc = csr.col.cpu().long()
+    ewc = csr.ew.cpu().double()
+    Xd = X.double()
+    ref = []
+    for r in rows.tolist():
+        e = slice(int(rp[r]), int(rp[r + 1]))
+        a = (ewc[e].to(dev)[:, None] * Xd[colc[e].to(dev)]).sum(0)
+        ref.append(a)
+    A = torch.stack(ref)
+    rr = rows.to(dev)
+    Yr = ((Xd[rr] + b.double() + A @ W.double().t()) * sc.double() + sh.double()).clamp_min(0)
+    csum1 = [float(t.double().sum()) for t in (X, W, csr.ew, csr.col, csr.row_ptr)]
+    bad = (Y32.abs() > 100).any(1).nonzero().flatten()[:8].tolist()
+    res["check_inputs_unchanged"] = csum0 == csum1
+    res["check_bad_rows"] = bad
+    if bad:
+        r = bad[0]
+        e = slice(int(csr.row_ptr[r]), int(csr.row_ptr[r + 1]))
+        res["check_bad_row0"] = {"cols": csr.col[e].tolist(), "ew": csr.ew[e].tolist(),
+                                 "y32": Y32[r, :4].tolist()}
+    res["check"] = {"f32_vs_ref_max": (Y32[rr].double() - Yr).abs().max().item(),
+                    "f16x3_vs_ref_max": (Y16[rr].double() - Yr).abs().max().item(),
+                    "f16x3_vs_f32_max": (Y16 - Y32).abs().max().item(),
+                    "f16x3_nan_rows": int(torch.isnan(Y16).any(1).sum().item()),
+                    "f32_max": Y32.abs().max().item(), "X_max": X.abs().max().item()}
 print(json.dumps({"grid": [nx, ny, nz], "H": H, "ms": res}))

@@ -7,7 +7,7 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmcsq"
 agg = collections.defaultdict(list)
-for f in glob.glob(f"{root}/p*/*counter_collection.csv"):
+for f in glob.glob(f"{root}/p*/*counter_collection.csv") + glob.glob(f"{root}/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         m = re.search(r"(\w+_kernel)<([^>]*)>", name)

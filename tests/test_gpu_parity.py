@@ -2,8 +2,9 @@
 golden vectors made from the reference's own code.
 
 Tolerance: the north star's 1e-5 max-abs error on the raw [N, 7] forward
-output (BASELINE.json); kernels are exact-fp32 (MFMA f32 / VALU fp32) so the
-observed error is ~1e-7, and integer work (grid graph, CSR) is bit-exact.
+output (BASELINE.json).  The exact-fp32 path (MFMA f32 / VALU fp32) shows
+~1e-7; the split-fp16 ("f16x3") GCN transform ~1e-6; integer work (grid
+graph, CSR) is bit-exact.  Model-level tests run at both precisions.
 """
 
 import math
@@ -35,10 +36,14 @@ def _gpu():
 DEV = "cuda"
 
 
-def make_model(cfg, sd):
+def make_model(cfg, sd, precision="f16x3"):
     m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
     m.load_state_dict(sd)
+    m.precision = precision
     return m.to(DEV).eval()
+
+
+PRECISIONS = ["f32", "f16x3"]
 
 
 # ------------------------------------------------------------------ integer work
@@ -137,11 +142,61 @@ def test_gcn_fused_layer_vs_fp64(H):
         assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
 
 
+def _gcn_layer_ref(csr, X, W, b, sc, sh):
+    """fp64 evaluation of the fused layer on the CSR the kernel reads."""
+    rp = csr.row_ptr.cpu().long()
+    n = csr.num_nodes
+    nnz = int(rp[-1])
+    rows = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+    Xd = X.cpu().double()
+    agg = torch.zeros(n, X.shape[1], dtype=torch.float64)
+    agg.index_add_(0, rows, csr.ew[:nnz].cpu().double()[:, None] * Xd[csr.col[:nnz].cpu().long()])
+    y = Xd[:n] + b.cpu().double() + agg @ W.cpu().double().t()
+    return torch.relu(y * sc.cpu().double() + sh.cpu().double())
+
+
+@pytest.mark.parametrize("H", [64, 128])
+@pytest.mark.parametrize("case", ["natural", "shuffled", "hub", "small", "strided"])
+def test_gcn_f16x3_layer_vs_fp64(H, case):
+    """Split-fp16 fused GCN layer: row ranges, partial tiles, in-/out-of-tile
+    entries in any mix (natural vs shuffled order), hub rows (> 64 entries per
+    producer wave: the slow path), one-step grids, strided x / out."""
+    dims = {"natural": (40, 30, 20), "shuffled": (40, 30, 20), "hub": (40, 30, 20),
+            "small": (13, 11, 3), "strided": (23, 7, 5)}[case]
+    x0, ei = grid_graph(*dims, device=DEV, permute_seed=3 if case == "shuffled" else None)
+    n = x0.shape[0]
+    if case == "hub":   # node 5 receives from 300 nodes
+        src = torch.arange(100, 400, device=DEV)
+        ei = torch.cat([ei, torch.stack([src, torch.full_like(src, 5)])], 1)
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
+    g = torch.Generator().manual_seed(H)
+    ld = H + 12 if case == "strided" else H
+    Xs = torch.randn(n, ld, generator=g).to(DEV)
+    X = Xs[:, :H]
+    W = (torch.randn(H, H, generator=g) * 0.05).to(DEV)
+    b = (torch.randn(H, generator=g) * 0.05).to(DEV)
+    sc, sh = (torch.rand(H, generator=g) + 0.5).to(DEV), (torch.randn(H, generator=g) * 0.1).to(DEV)
+    ref = _gcn_layer_ref(csr, X, W, b, sc, sh)
+    out = torch.full((n, ld), float("nan"), device=DEV)
+    P = _lib.ptr
+    for rb, re in ((0, n), (7, n - 3), (64, 64 + min(n - 64, 1000))):
+        out.fill_(float("nan"))
+        _lib.check(_lib.lib().mignn_gcn_layer_f16x3(
+            P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), ld, rb, re, H, P(W), P(b), P(sc), P(sh),
+            15, P(out), ld, _lib.stream()), "gcn_layer_f16x3")
+        got = out[:, :H].cpu().double()
+        err = (got[rb:re] - ref[rb:re]).abs().max().item()
+        assert err < 1e-5, err
+        assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
+        assert torch.isnan(out[:, H:]).all()   # stride padding untouched
+
+
 # ------------------------------------------------------------------ end-to-end parity
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", model_names())
-def test_flowgnn_bfs_parity(name):
+def test_flowgnn_bfs_parity(name, precision):
     cfg, sd, outs, err = model_fixture(name)
-    m = make_model(cfg, sd)
+    m = make_model(cfg, sd, precision)
     for gname, (y32, y64) in outs.items():
         x, ei, ea = bfs_graph(gname)
         ea_in = None if cfg["layer_type"] == "Transformer" else ea.to(DEV)
@@ -149,7 +204,7 @@ def test_flowgnn_bfs_parity(name):
             y = m(x.to(DEV), ei.to(DEV), ea_in).cpu()
         e32 = (y - y32).abs().max().item()
         e64 = (y.double() - y64).abs().max().item()
-        print(f"{name} {gname}: max|gpu-cpu32| {e32:.2e}  max|gpu-fp64| {e64:.2e}")
+        print(f"{name} {gname} {precision}: max|gpu-cpu32| {e32:.2e}  max|gpu-fp64| {e64:.2e}")
         assert e32 <= TOL and e64 <= TOL
     if err is not None:
         x, ei, ea = bfs_graph("train")
@@ -169,20 +224,22 @@ def test_flowgnn_tiny_edge_cases(name, lt):
     assert (y - y32).abs().max().item() <= TOL
 
 
-@pytest.mark.parametrize("lt,H", [("GCN", 128), ("GCN", 256), ("GAT", 64), ("GIN", 64),
-                                  ("Transformer", 64)])
-def test_synthetic_grid_vs_oracle(lt, H):
-    """Mid-size synthetic mesh (shuffled node order) vs the fp32 CPU oracle."""
+@pytest.mark.parametrize("lt,H,precision", [("GCN", 128, "f32"), ("GCN", 128, "f16x3"),
+                                            ("GCN", 64, "f16x3"), ("GCN", 256, "f16x3"),
+                                            ("GAT", 64, "f32"), ("GIN", 64, "f32"),
+                                            ("Transformer", 64, "f32")])
+def test_synthetic_grid_vs_oracle(lt, H, precision):
+    """Mid-size synthetic mesh (shuffled node order) vs the fp64 CPU oracle."""
     x, ei = grid_graph(40, 30, 25, device=DEV, permute_seed=1)
     cfg = dict(hidden_dim=H, num_layers=2, layer_type=lt)
     m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
     sd = seeded_state_dict(m.state_dict(), seed=11)
-    m = make_model(cfg, sd)
+    m = make_model(cfg, sd, precision)
     with torch.no_grad():
         y = m(x, ei).cpu()
     ref = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
     err = (y.double() - ref).abs().max().item()
-    print(f"{lt} H={H}: max err {err:.2e}")
+    print(f"{lt} H={H} {precision}: max err {err:.2e}")
     assert err <= TOL
 
 
