@@ -512,8 +512,28 @@ class FlowGNN(nn.Module):
         return wqk, bqk, wout, bout
 
     def _output_mlp(self, x, tmp, out):
-        """output_proj (gnn_model.py:90-100, :195): Lin-ReLU-Lin-ReLU-Lin-ReLU-Lin."""
+        """output_proj (gnn_model.py:90-100, :195): Lin-ReLU-Lin-ReLU-Lin-ReLU-Lin.
+        precision "f16x3" with H in {64, 128} and output_dim <= 8: one fused
+        launch (mignn_mlp_head, split-fp16 MFMA); otherwise four fp32 launches."""
         l0, l3, l6, l8 = (self.output_proj[i] for i in (0, 3, 6, 8))
+        H = self.hidden_dim
+        if self.precision == "f16x3" and H in (64, 128) and self.output_dim <= 8:
+            L = _lib.lib()
+            P = _lib.ptr
+            ts = (l0.weight, l0.bias, l3.weight, l3.bias, l6.weight, l6.bias, l8.weight,
+                  l8.bias)
+
+            def make():
+                img = torch.empty(L.mignn_mlp_head_prep_bytes(H), dtype=torch.uint8,
+                                  device=x.device)
+                _lib.check(L.mignn_mlp_head_prep(*(P(t) for t in ts), H, self.output_dim,
+                                                 P(img), img.numel(), _stream(x)),
+                           "mignn_mlp_head_prep")
+                return img
+            img = self._cached("head", 0, ts, make)
+            _lib.check(L.mignn_mlp_head(P(x), x.stride(0), x.shape[0], H, P(img), self.output_dim,
+                                        P(out), out.stride(0), _stream(x)), "mignn_mlp_head")
+            return
         h1 = linear(x, l0.weight, l0.bias, relu=True, out=tmp)
         h2 = linear(h1, l3.weight, l3.bias, relu=True, out=x)
         h3 = linear(h2, l6.weight, l6.bias, relu=True)

@@ -161,6 +161,23 @@ int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const floa
                           const float* w, const float* bias, const float* scale,
                           const float* shift, int flags, float* out, int64_t ldo, void* stream);
 
+/* Fused output head (output_proj, gnn_model.py:90-100, :195) in split-fp16
+ * MFMA arithmetic, h in {64, 128}, out_dim 1..8:
+ *   out = W4 relu(W3 relu(W2 relu(W1 x + b1) + b2) + b3) + b4
+ * with W1, W2: [h, h], W3: [h/2, h], W4: [out_dim, h/2] (torch Linear layout).
+ * mignn_mlp_head_prep writes the head image (fp16 hi/lo weight fragments,
+ * one scale exponent per matrix, biases in accumulator order) into `img`
+ * (mignn_mlp_head_prep_bytes(h) bytes, 16-B aligned, device memory); call
+ * it again whenever a weight or bias changes.  Replaces the four nn.Linear
+ * launches of FlowGNN.output_proj (eval mode: Dropout is the identity).
+ * Error vs fp64 ~1e-6 relative.  x: n rows of h floats, 16-B aligned rows. */
+size_t mignn_mlp_head_prep_bytes(int h);
+int mignn_mlp_head_prep(const float* w1, const float* b1, const float* w2, const float* b2,
+                        const float* w3, const float* b3, const float* w4, const float* b4,
+                        int h, int out_dim, void* img, size_t img_bytes, void* stream);
+int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, const void* img, int out_dim,
+                   float* out, int64_t ldo, void* stream);
+
 /* Fused GIN layer (gnn_model.py:70-75, :166, :184-191), h in {64, 128}:
  *   tmp_i = relu(nn.0( sum_{j in row i} x_j + (1 + eps) x_i ))      (rows rb..re -> tmp[0..])
  *   out_i = epi( nn.2(tmp_i) ) with residual x_i, BN affine, ReLU   (flags as above)

@@ -20,6 +20,11 @@ int mignn_diag_set_trace(void* buf);
  * wave 0 step start / aggregation done, 2/3 consumer wave 0 after the
  * residual hand-off / before the step's barrier. */
 int mignn_diag_set_trace_f16x3(void* buf);
+
+/* Fused output head (H = 128, out_dim 7) timing ablations: mode bit 1 = no x
+ * loads, bit 2 = no MFMAs (results wrong by design). */
+int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img, float* out,
+                        void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,31 @@ def lin(flags):
                               flags, P(Y), H, st), "lin")
 
 
+HW = [(torch.randn(o, i, device=dev, generator=g) / i ** 0.5) for o, i in
+      [(H, H), (H, H), (H // 2, H), (7, H // 2)]]
+HB = [torch.randn(w.shape[0], device=dev, generator=g) * 0.1 for w in HW]
+HIMG = torch.empty(L.mignn_mlp_head_prep_bytes(H), dtype=torch.uint8, device=dev)
+_lib.check(L.mignn_mlp_head_prep(*(P(t) for wb in zip(HW, HB) for t in wb), H, 7, P(HIMG),
+                                 HIMG.numel(), st), "prep")
+HOUT = torch.empty(n, 7, device=dev)
+
+
+def head16(_):
+    _lib.check(L.mignn_mlp_head(P(X), H, n, H, P(HIMG), 7, P(HOUT), 7, st), "head")
+
+
+def headdiag(mode):
+    _lib.check(L.mignn_diag_mlp_head(mode, P(X), n, P(HIMG), P(HOUT), st), "headdiag")
+
+
+def head32(_):
+    from mignn.gnn_model import linear
+    h1 = linear(X, HW[0], HB[0], relu=True, out=Y)
+    h2 = linear(h1, HW[1], HB[1], relu=True)
+    h3 = linear(h2, HW[2], HB[2], relu=True)
+    linear(h3, HW[3], HB[3], out=HOUT)
+
+
 def copy(_):
     Y.copy_(X)
 
@@ -110,6 +135,8 @@ cases = {
     "gcn16_no_local": (gcn16, 15 | 8192), "gcn16_no_ext_local": (gcn16, 15 | 4096 | 8192),
     "gcn16_only_dma": (gcn16, 15 | 256 | 512), "gcn_no_mfma": (gcn, 15 | 512), "gcn_no_gather": (gcn, 15 | 256),
     "gcn_xmaj": (gcn, 15 | 1024), "gcn_xmaj_no_mfma": (gcn, 15 | 1024 | 512),
+    "head16": (head16, 0), "head16_no_xload": (headdiag, 1), "head16_no_mfma": (headdiag, 2),
+    "head16_valu_only": (headdiag, 3), "head32(4 launches)": (head32, 0),
     "gcn_aggregate_only(simple)": (agg, 0), "linear_rows": (lin, 9),
     "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0),
     "diag_csr_gather": (diag, (0, 0)), "diag_csr_gather_g2048": (diag, (0, 2048)),
@@ -151,6 +178,16 @@ if os.environ.get("KB_TRACE"):
          "c_epilogue": t[:, 1:60, 7] - t[:, 1:60, 6],
          "step": t[:, 2:61, 0] - t[:, 1:60, 0]}
     res["trace_cycles_median"] = {k: float(v.median()) for k, v in d.items()}
+if os.environ.get("KB_CHECK_HEAD"):
+    head16(0)
+    torch.cuda.synchronize()
+    rows = torch.randint(0, n, (8192,), generator=torch.Generator().manual_seed(5)).to(dev)
+    h = X[rows].double()
+    for i, (w, bb) in enumerate(zip(HW, HB)):
+        h = h @ w.double().t() + bb.double()
+        h = h.clamp_min(0) if i < 3 else h
+    res["check_head"] = {"max_err": (HOUT[rows].double() - h).abs().max().item(),
+                         "max_ref": h.abs().max().item()}
 if os.environ.get("KB_CHECK"):
     # fresh outputs: the fp32 kernel into zeros, the f16x3 kernel into NaNs; fp64
     # reference on 4096 sampled rows (CSR on the CPU)

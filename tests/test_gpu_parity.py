@@ -191,6 +191,62 @@ def test_gcn_f16x3_layer_vs_fp64(H, case):
         assert torch.isnan(out[:, H:]).all()   # stride padding untouched
 
 
+def _head_ref(x, ws, bs):
+    """fp64 output_proj: Lin-ReLU-Lin-ReLU-Lin-ReLU-Lin (gnn_model.py:90-100)."""
+    h = x.cpu().double()
+    for i, (w, b) in enumerate(zip(ws, bs)):
+        h = h @ w.cpu().double().t() + b.cpu().double()
+        if i < 3:
+            h = torch.relu(h)
+    return h
+
+
+@pytest.mark.parametrize("H", [64, 128])
+@pytest.mark.parametrize("case", [(1000, 7, 0, 0), (37, 8, 0, 1), (1, 3, 4, 0), (20011, 7, 12, 5),
+                                  (64, 1, 0, 0), (4096, 7, 0, 0, "wide")])
+def test_mlp_head_f16x3_vs_fp64(H, case):
+    """Fused split-fp16 output head: partial 32-row blocks, 1..8 outputs,
+    strided x / out (padding left untouched), inputs spanning 2^+-8 in
+    magnitude ("wide": per-row exponents matter)."""
+    n, od, padx, pado = case[:4]
+    g = torch.Generator().manual_seed(n + H + od)
+    ld = H + padx
+    xs = torch.randn(n, ld, generator=g)
+    if len(case) > 4:
+        xs = xs * torch.exp2(torch.randint(-8, 9, (n, 1), generator=g).double()).float()
+    x = xs.to(DEV)[:, :H]
+    dims = [(H, H), (H, H), (H // 2, H), (od, H // 2)]
+    ws = [(torch.randn(o, i, generator=g) / math.sqrt(i)).to(DEV) for o, i in dims]
+    bs = [(torch.randn(o, generator=g) * 0.1).to(DEV) for o, _ in dims]
+    L, P = _lib.lib(), _lib.ptr
+    img = torch.empty(L.mignn_mlp_head_prep_bytes(H), dtype=torch.uint8, device=DEV)
+    wb = [P(t) for pair in zip(ws, bs) for t in pair]
+    _lib.check(L.mignn_mlp_head_prep(*wb, H, od, P(img), img.numel(), _lib.stream()),
+               "mlp_head_prep")
+    out = torch.full((n, od + pado), float("nan"), device=DEV)
+    _lib.check(L.mignn_mlp_head(P(x), ld, n, H, P(img), od, P(out), od + pado, _lib.stream()),
+               "mlp_head")
+    ref = _head_ref(x, ws, bs)
+    got = out.cpu().double()
+    scale = max(1.0, ref.abs().max().item())
+    err = (got[:, :od] - ref).abs().max().item()
+    assert err < 1e-5 * scale, (err, scale)
+    assert torch.isnan(got[:, od:]).all()
+
+
+def test_mlp_head_rejects_bad_shapes():
+    L, P = _lib.lib(), _lib.ptr
+    x = torch.zeros(4, 96, device=DEV)
+    img = torch.zeros(1 << 18, dtype=torch.uint8, device=DEV)
+    out = torch.zeros(4, 8, device=DEV)
+    rc = L.mignn_mlp_head(P(x), 96, 4, 96, P(img), 7, P(out), 8, _lib.stream())
+    assert rc == 1 and "h must be 64 or 128" in _lib.last_error()
+    rc = L.mignn_mlp_head(P(x), 96, 4, 64, P(img), 9, P(out), 8, _lib.stream())
+    assert rc == 1
+    rc = L.mignn_mlp_head(P(x) + 4, 96, 4, 64, P(img), 7, P(out), 8, _lib.stream())
+    assert rc == 1 and "16-B" in _lib.last_error()
+
+
 # ------------------------------------------------------------------ end-to-end parity
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", model_names())
