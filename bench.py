@@ -11,12 +11,17 @@ Workload (one "step" = one full eval-mode forward):
   ranks, GCN's implicit self-loops not counted), t = max over ranks.
 
 Extra objects on the same JSON line:
-  roofline     : the fused GCN layer kernel (mignn_gcn_layer), timed live with
-                 HIP events on the stream it is launched on; algorithmic bytes
-                 and flops per launch as in DESIGN.md §Roofline; the binding
-                 bound (HBM 8.0 TB/s vs f32 MFMA 157.3 TF) is reported, the
-                 other side is given too.  traffic = PMC-measured HBM bytes per
-                 launch from profiles/ (rocprofv3 --pmc run of this command).
+  roofline     : the fused GCN layer kernel (default precision "f16x3":
+                 mignn_gcn_layer_f16x3, split-fp16 MFMA with fp32 accumulation;
+                 "f32": mignn_gcn_layer on the f32 MFMA), timed live with HIP
+                 events on the stream it is launched on; algorithmic bytes and
+                 flops per launch as in DESIGN.md §Roofline; the binding bound
+                 (HBM 8.0 TB/s vs the compute time of the precision's MFMA +
+                 VALU work) is reported, the other side is given too.
+                 traffic = PMC-measured HBM bytes per launch from profiles/
+                 (rocprofv3 --pmc passes of this command, scripts/pmc.sh).
+  exact_f32    : the same forward in the exact-fp32 mode (MIGNN_PRECISION=f32),
+                 graph cached, for reference.
   cpu_baseline : the CPU oracle (pure-torch restatement of the reference
                  forward, the same op pattern PyG runs on the CPU) timed on
                  this box's host cores on a bounded 1M-node sample (rank 0, N=1).
@@ -45,6 +50,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "edges/s GNN forward (+MAE vs ref) on BFS mesh & 10M-node synthetic, 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12      # B/s, MI355X spec (MI355X_MICROARCH.md)
 F32_MFMA_PEAK = 157.3e12  # FLOP/s, dense f32 MFMA (= f32 vector peak)
+F16_MFMA_PEAK = 2.5e15     # FLOP/s, dense f16 MFMA (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -57,6 +63,8 @@ def parse():
     p.add_argument("--layer-type", default="GCN")
     p.add_argument("--grid", default="250,200,200", help="per-GPU nx,ny,nz")
     p.add_argument("--shuffle", action="store_true", help="seeded random node order (N=1)")
+    p.add_argument("--precision", default="f16x3", choices=["f16x3", "f32"],
+                   help="GCN transform / output head arithmetic (FlowGNN.precision)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-bfs", action="store_true")
     p.add_argument("--cpu-grid", default="100,100,100")
@@ -95,6 +103,7 @@ def main():
     sd = seeded_state_dict(model.state_dict(), seed=0)
     model.load_state_dict(sd)
     model = model.to(dev).eval()
+    model.precision = args.precision
 
     part = SlabPartition(nx, ny, nz, rank, world)
     if world == 1:
@@ -165,7 +174,6 @@ def main():
 
     elapsed = timed_loop(cache_graph=False)
     elapsed_cached = timed_loop(cache_graph=True)
-    model._layer = orig_layer
 
     # ---- roofline of the fused GCN layer kernel (this rank's launches)
     deg_plus_self = E_local / N_local + 1.0
@@ -180,9 +188,19 @@ def main():
     if launches and args.layer_type == "GCN":
         t_s = tot_ms / 1e3
         gbs = tot_bytes / t_s
-        tfs = tot_flops / t_s
         t_hbm = tot_bytes / HBM_PEAK
-        t_mfma = tot_flops / F32_MFMA_PEAK
+        n_rows = sum(n for _, _, n in launches)
+        if model.precision == "f16x3":
+            # 3 fp16 MFMA products per fp32 product on the transform; the
+            # gather-aggregate FMAs on the fp32 VALU
+            t_comp = (3 * 2 * n_rows * H * H / F16_MFMA_PEAK
+                      + 2 * n_rows * deg_plus_self * H / F32_MFMA_PEAK)
+            kname = "gcn_f16x3_kernel<%d> (mignn_gcn_layer_f16x3)" % H
+            comp_peak, comp_note = F16_MFMA_PEAK, "f16 MFMA x3 (split fp32) + f32 VALU aggregate"
+        else:
+            t_comp = tot_flops / F32_MFMA_PEAK
+            kname = "fused_tile_kernel<%d, %d, 0, true> (mignn_gcn_layer)" % (H, H)
+            comp_peak, comp_note = F32_MFMA_PEAK, "f32 MFMA"
         per_launch_bytes = tot_bytes / len(launches)
         traffic = None
         tf = os.path.join(HERE, "profiles", "gcn_layer_traffic.json")
@@ -190,28 +208,39 @@ def main():
             try:
                 with open(tf) as fh:
                     tj = json.load(fh)
-                if tj.get("config") == f"{args.layer_type}_L{L}_H{H}_{nx}x{ny}x{nz}":
+                if (tj.get("config") == f"{args.layer_type}_L{L}_H{H}_{nx}x{ny}x{nz}"
+                        and tj.get("kernel", "").split("<")[0] in kname):
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        mfma_bound = t_mfma >= t_hbm
+        bound_hbm = t_hbm >= t_comp
+        t_bound = max(t_hbm, t_comp)
         roofline = {
-            "kernel": "gcn_layer_kernel<%d> (mignn_gcn_layer)" % H,
-            "bound": "mfma" if mfma_bound else "hbm",
-            "achieved": round((tfs / 1e12) if mfma_bound else (gbs / 1e9), 3),
-            "peak": round((F32_MFMA_PEAK / 1e12) if mfma_bound else (HBM_PEAK / 1e9), 1),
-            "unit": "TFLOP/s" if mfma_bound else "GB/s",
-            "frac": round((tfs / F32_MFMA_PEAK) if mfma_bound else (gbs / HBM_PEAK), 4),
+            "kernel": kname,
+            "bound": "hbm" if bound_hbm else "mfma",
+            "achieved": round((gbs / 1e9) if bound_hbm else (tot_flops / t_s / 1e12), 3),
+            "peak": round((HBM_PEAK / 1e9) if bound_hbm else (comp_peak / 1e12), 1),
+            "unit": "GB/s" if bound_hbm else "TFLOP/s",
+            "frac": round(t_bound / t_s, 4),
             "traffic": traffic,
             "avg_launch_ms": round(tot_ms / len(launches), 4),
             "launches": len(launches),
             "algorithmic_bytes_per_launch": int(per_launch_bytes),
             "algorithmic_flops_per_launch": int(tot_flops / len(launches)),
             "hbm_side": {"achieved_GBps": round(gbs / 1e9, 1), "peak_GBps": HBM_PEAK / 1e9,
-                         "frac": round(gbs / HBM_PEAK, 4)},
-            "mfma_side": {"achieved_TFps": round(tfs / 1e12, 2),
-                          "peak_TFps": F32_MFMA_PEAK / 1e12, "frac": round(tfs / F32_MFMA_PEAK, 4)},
+                         "frac": round(gbs / HBM_PEAK, 4), "t_min_ms": round(1e3 * t_hbm / len(launches), 4)},
+            "compute_side": {"model": comp_note, "t_min_ms": round(1e3 * t_comp / len(launches), 4),
+                             "frac": round(t_comp / t_s, 4)},
         }
+
+    model._layer = orig_layer
+    exact = None
+    if model.precision != "f32":
+        model.precision = "f32"
+        el32 = timed_loop(cache_graph=True) if args.steps > 0 else 0.0
+        model.precision = args.precision
+        exact = {"ms_per_step_graph_cached": 1e3 * el32 / args.steps,
+                 "value_graph_cached": L * E_local * world * args.steps / el32}
 
     E_total = E_local * world
     value = L * E_total * args.steps / elapsed
@@ -222,6 +251,10 @@ def main():
         "graph_setup_in_step": True,
         "ms_per_step_graph_cached": 1e3 * elapsed_cached / args.steps,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "arithmetic": ("f16x3: fp32 values split into fp16 hi+lo, 3 fp16 MFMA products, fp32 "
+                       "accumulate (GCN transform, output head); gathers / norms / biases fp32; "
+                       "max-abs error <= 1e-5 (BASELINE tolerance)")
+                      if model.precision == "f16x3" else "exact fp32 (f32 MFMA / VALU)",
         "config": {
             "workload": f"{args.layer_type.lower()}_L{L}_H{H}_periodic_hex_{nx}x{ny}x{nz}_per_gpu"
                         + ("_shuffled" if args.shuffle else ""),
@@ -229,8 +262,12 @@ def main():
                      "seeded random weights",
             "nodes_per_gpu": N_local, "edges_per_gpu": E_local, "global_batch": 1,
             "parallelism": "single" if world == 1 else f"kslab{world}+rccl_halo",
+            "internal_node_order": ("locality (4x4-cell pencils, mignn_locality_order; part of "
+                                    "the per-step graph setup)")
+                                   if (world == 1 and model._use_reorder(x)) else "as given",
         },
         "roofline": roofline,
+        "exact_f32": exact,
     }
     if world > 1:
         dist.barrier()

@@ -38,6 +38,7 @@ namespace {
 constexpr int kBlock = 256;
 
 __global__ void csr_keys_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t N, int mode,
+                                const int32_t* __restrict__ relabel,
                                 uint32_t* __restrict__ keys, int32_t* __restrict__ vals,
                                 unsigned long long* __restrict__ counters) {
     __shared__ unsigned int s_kept, s_bad;
@@ -51,8 +52,13 @@ __global__ void csr_keys_kernel(const int64_t* __restrict__ ei, int64_t E, int64
         const bool valid = (s >= 0) & (s < N) & (d >= 0) & (d < N);
         bool keep = valid;
         if (mode == MIGNN_CSR_ONE_SELF_LOOP && s == d) keep = false;
-        keys[e] = keep ? static_cast<uint32_t>(d) : static_cast<uint32_t>(N);
-        vals[e] = valid ? static_cast<int32_t>(s) : 0;
+        int64_t sn = s, dn = d;
+        if (relabel != nullptr && valid) {   // node ids in the internal (relabelled) order
+            sn = relabel[s];
+            dn = relabel[d];
+        }
+        keys[e] = keep ? static_cast<uint32_t>(dn) : static_cast<uint32_t>(N);
+        vals[e] = valid ? static_cast<int32_t>(sn) : 0;
         kept += keep ? 1u : 0u;
         bad += valid ? 0u : 1u;
     }
@@ -229,6 +235,19 @@ __global__ void rows_gather_kernel(const float* __restrict__ src, int64_t lds,
     }
 }
 
+// any width / alignment (the head output, 7 columns)
+__global__ void rows_gather1_kernel(const float* __restrict__ src, int64_t lds,
+                                    const int32_t* __restrict__ idx, int64_t n, int h,
+                                    float* __restrict__ dst, int64_t ldd) {
+    const int64_t total = n * h;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / h;
+        const int c = static_cast<int>(t % h);
+        dst[r * ldd + c] = src[(int64_t)idx[r] * lds + c];
+    }
+}
+
 }  // namespace
 }  // namespace mignn
 
@@ -246,6 +265,14 @@ extern "C" size_t mignn_csr_scratch_bytes(int64_t num_edges, int64_t num_nodes) 
 extern "C" int mignn_csr_build(const int64_t* edge_index, int64_t E, int64_t N, int mode,
                                int32_t* row_ptr, int32_t* col, float* dinv, int64_t* info,
                                void* scratch, size_t scratch_bytes, void* stream_) {
+    return mignn_csr_build_relabeled(edge_index, E, N, mode, nullptr, row_ptr, col, dinv, info,
+                                     scratch, scratch_bytes, stream_);
+}
+
+extern "C" int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t E, int64_t N,
+                                         int mode, const int32_t* relabel, int32_t* row_ptr,
+                                         int32_t* col, float* dinv, int64_t* info, void* scratch,
+                                         size_t scratch_bytes, void* stream_) {
     MIGNN_REQUIRE(N >= 0 && E >= 0, "csr_build: negative sizes (E=%lld N=%lld)", (long long)E,
                   (long long)N);
     MIGNN_REQUIRE(E + N < (int64_t(1) << 31) - 1, "csr_build: E+N exceeds int32 CSR range");
@@ -271,7 +298,7 @@ extern "C" int mignn_csr_build(const int64_t* edge_index, int64_t E, int64_t N, 
     MIGNN_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), st));
     if (E > 0) {
         hipLaunchKernelGGL(csr_keys_kernel, dim3(grid_for(E, kBlock, 4096)), dim3(kBlock), 0, st,
-                           edge_index, E, N, mode, keys_in, vals_in, counters);
+                           edge_index, E, N, mode, relabel, keys_in, vals_in, counters);
         if ((rc = launch_status("csr_keys_kernel"))) return rc;
         const unsigned bits = key_bits(N);
         size_t temp = L.temp_bytes;
@@ -335,9 +362,14 @@ extern "C" int mignn_gcn_norm(const int32_t* row_ptr, const int32_t* col, const 
 
 extern "C" int mignn_rows_gather(const float* src, int64_t lds, const int32_t* idx, int64_t n,
                                  int h, float* dst, int64_t ldd, void* stream) {
-    MIGNN_REQUIRE(h % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, "rows_gather: h/ld not /4");
-    MIGNN_REQUIRE(aligned16(src) && aligned16(dst), "rows_gather: unaligned");
-    if (n == 0) return MIGNN_OK;
+    MIGNN_REQUIRE(h >= 0 && lds >= h && ldd >= h, "rows_gather: bad widths");
+    MIGNN_REQUIRE((src && dst && idx) || n == 0, "rows_gather: null pointer");
+    if (n == 0 || h == 0) return MIGNN_OK;
+    if (h % 4 != 0 || lds % 4 != 0 || ldd % 4 != 0 || !aligned16(src) || !aligned16(dst)) {
+        hipLaunchKernelGGL(rows_gather1_kernel, dim3(grid_for(n * h, kBlock, 65536)),
+                           dim3(kBlock), 0, as_stream(stream), src, lds, idx, n, h, dst, ldd);
+        return launch_status("rows_gather1_kernel");
+    }
     hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_for(n * (h / 4), kBlock, 65536)),
                        dim3(kBlock), 0, as_stream(stream), src, lds, idx, n, h / 4, dst, ldd);
     return launch_status("rows_gather_kernel");

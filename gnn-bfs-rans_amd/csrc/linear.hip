@@ -96,8 +96,9 @@ __global__ __launch_bounds__(256) void linear_kernel(
 // its 4 W rows and biases in registers; 32-bit index math only (a 64-bit
 // div/mod per element made this store-bound kernel 6x slower).
 __global__ __launch_bounds__(256) void input_proj_kernel(
-    const float* __restrict__ x, int64_t n, int in_dim, const float* __restrict__ w,
-    const float* __restrict__ b, int h, float* __restrict__ out, int64_t ldo) {
+    const float* __restrict__ x, int64_t n, int in_dim, const int32_t* __restrict__ rows,
+    const float* __restrict__ w, const float* __restrict__ b, int h, float* __restrict__ out,
+    int64_t ldo) {
     const int h4 = h >> 2;
     const int rpi = blockDim.x / h4;                 // rows per block iteration
     const int slot = threadIdx.x / h4;
@@ -112,8 +113,9 @@ __global__ __launch_bounds__(256) void input_proj_kernel(
     }
     for (int64_t row = (int64_t)blockIdx.x * rpi + slot; row < n; row += (int64_t)gridDim.x * rpi) {
         float xv[8];
+        const int64_t src = rows != nullptr ? static_cast<int64_t>(rows[row]) : row;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) xv[k] = k < in_dim ? x[row * in_dim + k] : 0.f;
+        for (int k = 0; k < 8; ++k) xv[k] = k < in_dim ? x[src * in_dim + k] : 0.f;
         float o[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -162,6 +164,12 @@ extern "C" int mignn_linear(const float* a, int64_t lda, int64_t m, int k, const
 
 extern "C" int mignn_input_proj(const float* x, int64_t n, int in_dim, const float* w,
                                 const float* b, int h, float* out, int64_t ldo, void* stream) {
+    return mignn_input_proj_rows(x, n, in_dim, nullptr, w, b, h, out, ldo, stream);
+}
+
+extern "C" int mignn_input_proj_rows(const float* x, int64_t n, int in_dim, const int32_t* rows,
+                                     const float* w, const float* b, int h, float* out,
+                                     int64_t ldo, void* stream) {
     MIGNN_REQUIRE(in_dim > 0 && in_dim <= 8 && h % 4 == 0 && ldo % 4 == 0,
                   "input_proj: in_dim=%d h=%d", in_dim, h);
     MIGNN_REQUIRE(x && w && b && out && aligned16(out), "input_proj: null/unaligned");
@@ -171,6 +179,6 @@ extern "C" int mignn_input_proj(const float* x, int64_t n, int in_dim, const flo
     const int block = h4 >= 256 ? h4 : (256 / h4) * h4;
     const int64_t rpi = block / h4;
     hipLaunchKernelGGL(input_proj_kernel, dim3(grid_for((n + rpi - 1) / rpi, 1, 16384)),
-                       dim3(block), 0, as_stream(stream), x, n, in_dim, w, b, h, out, ldo);
+                       dim3(block), 0, as_stream(stream), x, n, in_dim, rows, w, b, h, out, ldo);
     return launch_status("input_proj_kernel");
 }

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void mlp_prep_kernel(
 template <int H, int DIAG = 0>
 __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t nrows, const unsigned char* __restrict__ img,
-    int out_dim, float* __restrict__ out, int64_t ldo) {
+    int out_dim, float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
     using C = MCfg<H>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
     const int lane = threadIdx.x & 63;
@@ -328,10 +328,11 @@ __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
         // lane (row, h) holds outputs 4 h .. 4 h + 3 in registers 0..3
         if (row < nrows) {
             const float un = exp2_int(max(-(p + q4), -126));
+            const int64_t orow = out_rows != nullptr ? static_cast<int64_t>(out_rows[row]) : row;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int oc = 4 * h + r;
-                if (oc < out_dim) out[row * ldo + oc] = o[r] * un;
+                if (oc < out_dim) out[orow * ldo + oc] = o[r] * un;
             }
         }
     }
@@ -369,7 +370,8 @@ extern "C" int mignn_mlp_head_prep(const float* w1, const float* b1, const float
 }
 
 extern "C" int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, const void* img,
-                              int out_dim, float* out, int64_t ldo, void* stream) {
+                              int out_dim, float* out, int64_t ldo, const int32_t* out_rows,
+                              void* stream) {
     MIGNN_REQUIRE(x && img && out, "mlp_head: null pointer");
     MIGNN_REQUIRE(h == 64 || h == 128, "mlp_head: h must be 64 or 128 (got %d)", h);
     MIGNN_REQUIRE(out_dim >= 1 && out_dim <= 8, "mlp_head: out_dim must be 1..8 (got %d)",
@@ -391,10 +393,10 @@ extern "C" int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, con
     const int grid = static_cast<int>(want < cap ? want : cap);
     if (h == 128)
         hipLaunchKernelGGL(mlp_head_kernel<128>, dim3(grid), dim3(MCfg<128>::NT), 0, st, x, ldx, n,
-                           static_cast<const unsigned char*>(img), out_dim, out, ldo);
+                           static_cast<const unsigned char*>(img), out_dim, out, ldo, out_rows);
     else
         hipLaunchKernelGGL(mlp_head_kernel<64>, dim3(grid), dim3(MCfg<64>::NT), 0, st, x, ldx, n,
-                           static_cast<const unsigned char*>(img), out_dim, out, ldo);
+                           static_cast<const unsigned char*>(img), out_dim, out, ldo, out_rows);
     return launch_status("mlp_head_kernel");
 }
 
@@ -409,10 +411,10 @@ extern "C" int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const vo
     const int grid = static_cast<int>(want < cus ? want : cus);
     const auto* im = static_cast<const unsigned char*>(img);
     switch (mode) {
-    case 0: hipLaunchKernelGGL((mlp_head_kernel<128, 0>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7); break;
-    case 1: hipLaunchKernelGGL((mlp_head_kernel<128, 1>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7); break;
-    case 2: hipLaunchKernelGGL((mlp_head_kernel<128, 2>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7); break;
-    default: hipLaunchKernelGGL((mlp_head_kernel<128, 3>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7); break;
+    case 0: hipLaunchKernelGGL((mlp_head_kernel<128, 0>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
+    case 1: hipLaunchKernelGGL((mlp_head_kernel<128, 1>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
+    case 2: hipLaunchKernelGGL((mlp_head_kernel<128, 2>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
+    default: hipLaunchKernelGGL((mlp_head_kernel<128, 3>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
     }
     return launch_status("mlp_head_kernel(diag)");
 }

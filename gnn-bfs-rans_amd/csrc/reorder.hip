@@ -1,0 +1,295 @@
+// Locality order of the mesh nodes (internal layout of the activations; the
+// forward's results are unchanged up to fp32 summation order, see
+// mignn.h:mignn_locality_order).
+//
+// Why: the fused GCN layer reads every CSR neighbour row once per layer.  In
+// the lexicographic cell order of a blockMesh / structured mesh (and of the
+// synthetic hex grid) the +-k neighbours of a 64-row tile sit
+// one plane (nx*ny rows, 25.6 MB at 250x200) away -- out of the 4 MB L2 of
+// the XCD, so they come from the MALL or from HBM: 2 of the 4 out-of-tile
+// rows per node.  Relabelled into 4x4-cell pencils swept along z, a 64-row
+// tile is a 4x4x4 block; its +-z neighbours are the adjacent tiles (just
+// read, in L2), its +-x neighbours one pencil (nz/4 tiles) away, and only
+// the +-y faces (2 of 6) are far: out-of-tile rows per node drop from 4 to
+// 1.5, far rows from 2 to 0.5.
+//
+// Node features of FlowGNN are the cell centres (reference
+// graph_constructor.py:259), so the order is computed from them:
+//   K1 bbox      : per-axis min / max (ordered-uint atomics)
+//   K2 cell size : per axis, the mean |delta| of the edges that run mainly
+//                  along that axis (periodic wrap edges, |delta| > extent/2,
+//                  excluded) -- the mesh spacing, also for anisotropic cells
+//   K3 keys      : c = round((pos - min) / h) per axis;
+//                  key = ((cy/4 * NBX + cx/4) * NZ + cz) * 16 + (cy%4)*4 + cx%4,
+//                  coarsened until the key range fits 32 bits
+//   K4 sort      : rocprim::radix_sort_pairs (stable: ties keep input order)
+//   K5 inverse   : inv[perm[p]] = p
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "common.hpp"
+
+namespace mignn {
+namespace {
+
+constexpr int kB = 256;
+
+struct OrderStats {
+    unsigned int lo[3], hi[3];        // ordered-uint encoded bbox
+    double sum[3];                    // sum of |delta| of axis-dominant edges
+    unsigned long long cnt[3];
+};
+
+__device__ __forceinline__ unsigned int f2ord(float f) {
+    const unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned int u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__global__ void order_init_kernel(OrderStats* st) {
+    if (threadIdx.x < 3) {
+        st->lo[threadIdx.x] = 0xffffffffu;
+        st->hi[threadIdx.x] = 0u;
+        st->sum[threadIdx.x] = 0.0;
+        st->cnt[threadIdx.x] = 0ull;
+    }
+}
+
+__global__ __launch_bounds__(kB) void bbox_kernel(const float* __restrict__ pos, int64_t ldp,
+                                                  int64_t n, OrderStats* st) {
+    unsigned int lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
+    for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = pos[i * ldp + a];
+            if (v == v) {   // NaN-free
+                lo[a] = min(lo[a], f2ord(v));
+                hi[a] = max(hi[a], f2ord(v));
+            }
+        }
+    }
+    __shared__ unsigned int s_lo[3], s_hi[3];
+    if (threadIdx.x < 3) { s_lo[threadIdx.x] = 0xffffffffu; s_hi[threadIdx.x] = 0u; }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[a] = min(lo[a], static_cast<unsigned>(__shfl_xor(static_cast<int>(lo[a]), o)));
+            hi[a] = max(hi[a], static_cast<unsigned>(__shfl_xor(static_cast<int>(hi[a]), o)));
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            atomicMin(&s_lo[a], lo[a]);
+            atomicMax(&s_hi[a], hi[a]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {   // one global atomic per block and value
+        atomicMin(&st->lo[threadIdx.x], s_lo[threadIdx.x]);
+        atomicMax(&st->hi[threadIdx.x], s_hi[threadIdx.x]);
+    }
+}
+
+__global__ __launch_bounds__(kB) void spacing_kernel(const float* __restrict__ pos, int64_t ldp,
+                                                     int64_t n, const int64_t* __restrict__ ei,
+                                                     int64_t E, OrderStats* st) {
+    float ext[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) ext[a] = ord2f(st->hi[a]) - ord2f(st->lo[a]);
+    double sum[3] = {0.0, 0.0, 0.0};
+    unsigned long long cnt[3] = {0ull, 0ull, 0ull};
+    const int64_t ns = E < (int64_t(1) << 22) ? E : (int64_t(1) << 22);
+    for (int64_t t = blockIdx.x * (int64_t)kB + threadIdx.x; t < ns; t += (int64_t)gridDim.x * kB) {
+        const int64_t e = ns == E ? t : (t * E) / ns;   // evenly strided sample
+        const int64_t s = ei[e], d = ei[E + e];
+        if (s < 0 || s >= n || d < 0 || d >= n || s == d) continue;
+        float dl[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) dl[a] = fabsf(pos[s * ldp + a] - pos[d * ldp + a]);
+        const int a = (dl[0] >= dl[1] && dl[0] >= dl[2]) ? 0 : (dl[1] >= dl[2] ? 1 : 2);
+        if (dl[a] > 0.f && dl[a] <= 0.5f * ext[a]) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (b == a) { sum[b] += dl[a]; cnt[b] += 1; }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        for (int o = 32; o > 0; o >>= 1) {
+            sum[a] += __shfl_xor(sum[a], o);
+            cnt[a] += __shfl_xor(cnt[a], o);
+        }
+    }
+    __shared__ double s_sum[3];
+    __shared__ unsigned long long s_cnt[3];
+    if (threadIdx.x < 3) { s_sum[threadIdx.x] = 0.0; s_cnt[threadIdx.x] = 0ull; }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (cnt[a]) {
+                atomicAdd(&s_sum[a], sum[a]);
+                atomicAdd(&s_cnt[a], cnt[a]);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 && s_cnt[threadIdx.x]) {
+        atomicAdd(&st->sum[threadIdx.x], s_sum[threadIdx.x]);
+        atomicAdd(&st->cnt[threadIdx.x], s_cnt[threadIdx.x]);
+    }
+}
+
+// per-axis spacing h (edge mean, else extent / cbrt(n)), cells per axis
+__device__ void order_grid(const OrderStats* st, int64_t n, float lo[3], float inv_h[3],
+                           int64_t cells[3]) {
+    const double fallback = cbrt(static_cast<double>(n > 0 ? n : 1));
+    double ih[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = ord2f(st->lo[a]);
+        double ext = static_cast<double>(ord2f(st->hi[a])) - lo[a];
+        if (!(ext >= 0.0) || !(ext < 3.0e38)) ext = 0.0;    // all-NaN / infinite coordinates
+        double h = st->cnt[a] ? st->sum[a] / static_cast<double>(st->cnt[a]) : ext / fallback;
+        if (!(h > 0.0) || !(ext >= 0.0)) h = 1.0;       // degenerate axis / NaN extents
+        ih[a] = 1.0 / h;
+        cells[a] = static_cast<int64_t>(fmin(ext * ih[a] + 0.5, 1.0e15)) + 1;
+    }
+    // coarsen until ceil(cy/4) * ceil(cx/4) * cz * 16 < 2^32
+    for (int it = 0; it < 8; ++it) {
+        const double range = static_cast<double>((cells[1] + 3) / 4) * ((cells[0] + 3) / 4) *
+                             static_cast<double>(cells[2]) * 16.0;
+        if (range < 4294967295.0) break;
+        const double f = cbrt(range / 2147483648.0) * 1.01;
+        for (int a = 0; a < 3; ++a) {
+            ih[a] /= f;
+            double ext = static_cast<double>(ord2f(st->hi[a])) - lo[a];
+            if (!(ext >= 0.0) || !(ext < 3.0e38)) ext = 0.0;
+            cells[a] = static_cast<int64_t>(fmin(ext * ih[a] + 0.5, 1.0e15)) + 1;
+        }
+    }
+    for (int a = 0; a < 3; ++a) inv_h[a] = static_cast<float>(ih[a]);
+}
+
+__global__ __launch_bounds__(kB) void order_keys_kernel(const float* __restrict__ pos,
+                                                        int64_t ldp, int64_t n,
+                                                        const OrderStats* st,
+                                                        uint32_t* __restrict__ keys,
+                                                        int32_t* __restrict__ ids) {
+    __shared__ float s_lo[3], s_ih[3];
+    __shared__ int64_t s_cells[3];
+    if (threadIdx.x == 0) {
+        float lo[3], ih[3];
+        int64_t cells[3];
+        order_grid(st, n, lo, ih, cells);
+        for (int a = 0; a < 3; ++a) { s_lo[a] = lo[a]; s_ih[a] = ih[a]; s_cells[a] = cells[a]; }
+    }
+    __syncthreads();
+    const int64_t nbx = (s_cells[0] + 3) / 4, nz = s_cells[2];
+    for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
+        int64_t c[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = (pos[i * ldp + a] - s_lo[a]) * s_ih[a] + 0.5f;
+            int64_t q = v >= 0.f ? static_cast<int64_t>(v) : 0;   // NaN -> 0
+            c[a] = q < s_cells[a] ? q : s_cells[a] - 1;
+        }
+        const uint64_t key = ((static_cast<uint64_t>(c[1] >> 2) * nbx + (c[0] >> 2)) * nz + c[2]) * 16 +
+                             (c[1] & 3) * 4 + (c[0] & 3);
+        keys[i] = static_cast<uint32_t>(key);
+        ids[i] = static_cast<int32_t>(i);
+    }
+}
+
+__global__ void inverse_kernel(const int32_t* __restrict__ perm, int64_t n,
+                               int32_t* __restrict__ inv) {
+    for (int64_t p = blockIdx.x * (int64_t)kB + threadIdx.x; p < n; p += (int64_t)gridDim.x * kB)
+        inv[perm[p]] = static_cast<int32_t>(p);
+}
+
+inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
+
+struct OrderScratch {
+    size_t keys_in, keys_out, ids, stats, temp, temp_bytes, total;
+};
+
+int order_layout(int64_t n, OrderScratch* L) {
+    const size_t m = static_cast<size_t>(n > 0 ? n : 1);
+    size_t o = 0;
+    L->keys_in = o; o = align256(o + m * 4);
+    L->keys_out = o; o = align256(o + m * 4);
+    L->ids = o; o = align256(o + m * 4);
+    L->stats = o; o = align256(o + sizeof(OrderStats));
+    L->temp = o;
+    size_t temp = 0;
+    hipError_t err = rocprim::radix_sort_pairs(nullptr, temp, (uint32_t*)nullptr,
+                                               (uint32_t*)nullptr, (int32_t*)nullptr,
+                                               (int32_t*)nullptr, m, 0u, 32u);
+    if (err != hipSuccess) {
+        set_error("rocprim::radix_sort_pairs size query: %s", hipGetErrorString(err));
+        return MIGNN_ERR_HIP;
+    }
+    L->temp_bytes = temp;
+    L->total = align256(o + temp);
+    return MIGNN_OK;
+}
+
+}  // namespace
+}  // namespace mignn
+
+using namespace mignn;
+
+extern "C" size_t mignn_locality_order_scratch_bytes(int64_t n) {
+    OrderScratch L;
+    return order_layout(n, &L) == MIGNN_OK ? L.total : 0;
+}
+
+extern "C" int mignn_locality_order(const float* pos, int64_t ldp, int64_t n,
+                                    const int64_t* edge_index, int64_t E, int32_t* perm,
+                                    int32_t* inv, void* scratch, size_t scratch_bytes,
+                                    void* stream) {
+    MIGNN_REQUIRE(n >= 0 && E >= 0 && n < (int64_t(1) << 31), "locality_order: bad sizes");
+    MIGNN_REQUIRE(ldp >= 3, "locality_order: pos needs 3 columns (ldp %lld)", (long long)ldp);
+    MIGNN_REQUIRE((pos && perm && inv && scratch) || n == 0, "locality_order: null pointer");
+    MIGNN_REQUIRE(E == 0 || edge_index, "locality_order: null edge_index");
+    if (n == 0) return MIGNN_OK;
+    OrderScratch L;
+    int rc = order_layout(n, &L);
+    if (rc) return rc;
+    if (scratch_bytes < L.total) {
+        set_error("locality_order: scratch %zu < required %zu", scratch_bytes, L.total);
+        return MIGNN_ERR_SCRATCH;
+    }
+    hipStream_t st = as_stream(stream);
+    char* base = static_cast<char*>(scratch);
+    auto* keys_in = reinterpret_cast<uint32_t*>(base + L.keys_in);
+    auto* keys_out = reinterpret_cast<uint32_t*>(base + L.keys_out);
+    auto* ids = reinterpret_cast<int32_t*>(base + L.ids);
+    auto* stats = reinterpret_cast<OrderStats*>(base + L.stats);
+    hipLaunchKernelGGL(order_init_kernel, dim3(1), dim3(64), 0, st, stats);
+    if ((rc = launch_status("order_init_kernel"))) return rc;
+    hipLaunchKernelGGL(bbox_kernel, dim3(grid_for(n, kB, 1024)), dim3(kB), 0, st, pos, ldp, n,
+                       stats);
+    if ((rc = launch_status("bbox_kernel"))) return rc;
+    if (E > 0) {
+        // the spacing is a mean over edges: a strided sample of <= 2^22 edges
+        // (every edge when fewer) is plenty and keeps the gathers off the step
+        hipLaunchKernelGGL(spacing_kernel, dim3(grid_for(E < (1 << 22) ? E : (1 << 22), kB, 1024)),
+                           dim3(kB), 0, st, pos, ldp, n, edge_index, E, stats);
+        if ((rc = launch_status("spacing_kernel"))) return rc;
+    }
+    hipLaunchKernelGGL(order_keys_kernel, dim3(grid_for(n, kB, 8192)), dim3(kB), 0, st, pos, ldp,
+                       n, stats, keys_in, ids);
+    if ((rc = launch_status("order_keys_kernel"))) return rc;
+    size_t temp = L.temp_bytes;
+    hipError_t err = rocprim::radix_sort_pairs(base + L.temp, temp, keys_in, keys_out, ids, perm,
+                                               static_cast<size_t>(n), 0u, 32u, st);
+    if (err != hipSuccess) {
+        set_error("rocprim::radix_sort_pairs: %s", hipGetErrorString(err));
+        return MIGNN_ERR_HIP;
+    }
+    hipLaunchKernelGGL(inverse_kernel, dim3(grid_for(n, kB, 8192)), dim3(kB), 0, st, perm, n, inv);
+    return launch_status("inverse_kernel");
+}

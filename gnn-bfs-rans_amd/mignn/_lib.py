@@ -47,7 +47,13 @@ SIGNATURES = {
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
     "mignn_mlp_head_prep": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int, c_int, _P, c_size_t,
                                     _P]),
-    "mignn_mlp_head": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int, _P, c_int64, _P]),
+    "mignn_mlp_head": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int, _P, c_int64, _P, _P]),
+    "mignn_csr_build_relabeled": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
+                                          c_size_t, _P]),
+    "mignn_locality_order_scratch_bytes": (c_size_t, [c_int64]),
+    "mignn_locality_order": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P, _P, c_size_t,
+                                     _P]),
+    "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),
     "mignn_gcn_norm": (c_int, [_P, _P, _P, c_int64, c_int64, _P, _P]),
@@ -61,6 +67,7 @@ DIAG_SIGNATURES = {
                                   _P]),
     "mignn_diag_set_trace": (c_int, [_P]),
     "mignn_diag_set_trace_f16x3": (c_int, [_P]),
+    "mignn_diag_clock": (c_int, [c_int, c_int, _P, _P]),
     "mignn_diag_mlp_head": (c_int, [c_int, _P, c_int64, _P, _P, _P]),
 }
 

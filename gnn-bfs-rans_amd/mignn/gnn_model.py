@@ -121,12 +121,17 @@ class BatchNorm(nn.Module):
 # ---------------------------------------------------------------------------
 
 class Csr:
-    __slots__ = ("row_ptr", "col", "dinv", "ew", "info", "num_nodes", "num_edges", "edge_index")
+    """Destination-major CSR.  With a locality order (`perm`, `inv` set), node
+    ids inside the CSR are the internal ids: internal row p is caller node
+    perm[p], caller node v is internal row inv[v]."""
+    __slots__ = ("row_ptr", "col", "dinv", "ew", "info", "num_nodes", "num_edges", "edge_index",
+                 "perm", "inv", "pos")
 
     def __init__(self, row_ptr, col, dinv, info, num_nodes, num_edges, edge_index, ew=None):
         self.row_ptr, self.col, self.dinv, self.info = row_ptr, col, dinv, info
         self.num_nodes, self.num_edges, self.edge_index = num_nodes, num_edges, edge_index
         self.ew = ew
+        self.perm = self.inv = self.pos = None
 
     def compute_gcn_weights(self, row_begin: int = 0, row_end: Optional[int] = None):
         """Per-entry PyG gcn_norm weights (mignn_gcn_norm); call again after the
@@ -139,8 +144,32 @@ class Csr:
                                              _lib.stream(self.col.device)), "mignn_gcn_norm")
 
 
-def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
-    """Destination-major CSR on the device (mignn_csr_build); no host sync."""
+def locality_order(pos: torch.Tensor, edge_index: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(perm, inv) of mignn_locality_order: 4x4-cell pencils of the mesh given
+    by the cell centres `pos` [N, >=3]; perm[new] = old id, inv[old] = new."""
+    dev = pos.device
+    n = int(pos.shape[0])
+    p = pos if (pos.dtype == torch.float32 and pos.stride(1) == 1) else pos.float().contiguous()
+    ei = edge_index
+    if ei.dtype != torch.int64 or not ei.is_contiguous():
+        ei = ei.to(torch.int64).contiguous()
+    perm = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    inv = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    nbytes = L.mignn_locality_order_scratch_bytes(n)
+    if nbytes == 0:
+        raise _lib.MignnError("locality order scratch query failed: " + _lib.last_error())
+    scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    _lib.check(L.mignn_locality_order(_lib.ptr(p), p.stride(0), n, _lib.ptr(ei), int(ei.shape[1]),
+                                      _lib.ptr(perm), _lib.ptr(inv), _lib.ptr(scratch), nbytes,
+                                      _lib.stream(dev)), "mignn_locality_order")
+    return perm[:n], inv[:n]
+
+
+def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int,
+              relabel: Optional[torch.Tensor] = None) -> Csr:
+    """Destination-major CSR on the device (mignn_csr_build); no host sync.
+    `relabel` (int32 [N], a permutation): node ids mapped through it."""
     dev = edge_index.device
     ei = edge_index
     if ei.dtype != torch.int64 or not ei.is_contiguous():
@@ -156,9 +185,10 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
     if nbytes == 0:
         raise _lib.MignnError("csr scratch query failed: " + _lib.last_error())
     scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    _lib.check(L.mignn_csr_build(_lib.ptr(ei), E, N, mode, _lib.ptr(row_ptr), _lib.ptr(col),
-                                 _lib.ptr(dinv), _lib.ptr(info), _lib.ptr(scratch), nbytes,
-                                 _lib.stream(dev)), "mignn_csr_build")
+    _lib.check(L.mignn_csr_build_relabeled(_lib.ptr(ei), E, N, mode, _lib.ptr(relabel),
+                                           _lib.ptr(row_ptr), _lib.ptr(col), _lib.ptr(dinv),
+                                           _lib.ptr(info), _lib.ptr(scratch), nbytes,
+                                           _lib.stream(dev)), "mignn_csr_build")
     csr = Csr(row_ptr, col, dinv, info, N, E, ei)
     if mode == CSR_ONE_SELF_LOOP:
         csr.compute_gcn_weights()
@@ -166,23 +196,37 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
 
 
 class _CsrCache:
-    """Keyed by (edge_index storage, version, shape, N, mode, device); holds a
-    reference to the edge_index so its storage cannot be recycled while cached."""
+    """Keyed by (edge_index storage, version, shape, N, mode, device) -- plus
+    the positions' storage / version when a locality order is requested;
+    holds references to the keyed tensors so their storage cannot be recycled
+    while cached."""
 
     def __init__(self, capacity: int = 4):
         self.capacity = capacity
         self.entries: Dict[Tuple, Csr] = {}
 
-    def get(self, edge_index: torch.Tensor, num_nodes: int, mode: int) -> Csr:
-        if self.capacity <= 0:        # caching off: rebuild every forward
+    @staticmethod
+    def _build(edge_index, num_nodes, mode, pos):
+        if pos is None:
             return build_csr(edge_index, num_nodes, mode)
+        perm, inv = locality_order(pos, edge_index)
+        csr = build_csr(edge_index, num_nodes, mode, relabel=inv)
+        csr.perm, csr.inv, csr.pos = perm, inv, pos
+        return csr
+
+    def get(self, edge_index: torch.Tensor, num_nodes: int, mode: int,
+            pos: Optional[torch.Tensor] = None) -> Csr:
+        if self.capacity <= 0:        # caching off: rebuild every forward
+            return self._build(edge_index, num_nodes, mode, pos)
         key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
                tuple(edge_index.stride()), edge_index.dtype, int(num_nodes), mode,
                str(edge_index.device))
+        if pos is not None:
+            key += (pos.data_ptr(), pos._version, tuple(pos.shape), tuple(pos.stride()))
         hit = self.entries.get(key)
         if hit is not None:
             return hit
-        csr = build_csr(edge_index, num_nodes, mode)
+        csr = self._build(edge_index, num_nodes, mode, pos)
         if len(self.entries) >= self.capacity:
             self.entries.pop(next(iter(self.entries)))
         self.entries[key] = csr
@@ -291,6 +335,9 @@ class FlowGNN(nn.Module):
             nn.Linear(hidden_dim // 2, output_dim))
         self.dropout = nn.Dropout(dropout)
         self.precision = os.environ.get("MIGNN_PRECISION", "f16x3")
+        # internal locality order of the nodes: "auto" (meshes of >= 2^20
+        # nodes with 3-D cell-centre features), "1" always, "0" never
+        self.reorder = os.environ.get("MIGNN_REORDER", "auto")
         self._csr = _CsrCache()
         self._prep: Dict[Tuple, object] = {}
 
@@ -322,10 +369,11 @@ class FlowGNN(nn.Module):
         xin = x.contiguous().float() if (x.dtype != torch.float32 or not x.is_contiguous()) else x
         buf_a = torch.empty((num_nodes, H), dtype=torch.float32, device=x.device)
         buf_b = torch.empty_like(buf_a)
-        # input_proj (gnn_model.py:159)
-        self._input_proj(xin, buf_a)
         mode = CSR_ONE_SELF_LOOP if self.layer_type in ("GCN", "GAT") else CSR_VERBATIM
-        csr = self._csr.get(edge_index, num_nodes, mode)
+        pos = xin if self._use_reorder(xin) else None
+        csr = self._csr.get(edge_index, num_nodes, mode, pos)
+        # input_proj (gnn_model.py:159), gathered into the CSR's node order
+        self._input_proj(xin, buf_a, rows=csr.perm)
         cur, nxt = buf_a, buf_b
         for i, layer in enumerate(self.gnn_layers):
             try:
@@ -337,7 +385,7 @@ class FlowGNN(nn.Module):
             except RuntimeError as e:
                 raise self._layer_error(i, e, num_nodes, edge_index, cur, edge_attr) from e
             cur, nxt = nxt, cur
-        self._output_mlp(cur, nxt, out)
+        self._output_mlp(cur, nxt, out, rows=csr.perm, inv=csr.inv)
         return out
 
     # ------------------------------------------------------------- internals
@@ -374,14 +422,21 @@ class FlowGNN(nn.Module):
             f"  x shape: {x.shape}, edge_attr shape: "
             f"{edge_attr.shape if edge_attr is not None else 'None'}")
 
-    def _input_proj(self, x, out):
+    def _use_reorder(self, x) -> bool:
+        if self.reorder not in ("auto", "0", "1"):
+            raise ValueError(f"MIGNN_REORDER must be auto, 0 or 1, got {self.reorder!r}")
+        if self.reorder == "0" or x.shape[1] < 3:
+            return False
+        return self.reorder == "1" or x.shape[0] >= (1 << 20)
+
+    def _input_proj(self, x, out, rows=None):
         w, b = self.input_proj.weight, self.input_proj.bias
         if self.input_dim <= 8:
-            _lib.check(_lib.lib().mignn_input_proj(
-                _lib.ptr(x), x.shape[0], self.input_dim, _lib.ptr(w), _lib.ptr(b),
+            _lib.check(_lib.lib().mignn_input_proj_rows(
+                _lib.ptr(x), x.shape[0], self.input_dim, _lib.ptr(rows), _lib.ptr(w), _lib.ptr(b),
                 self.hidden_dim, _lib.ptr(out), out.stride(0), _stream(x)), "mignn_input_proj")
         else:
-            linear(x, w, b, out=out)
+            linear(x if rows is None else x[rows.long()], w, b, out=out)
 
     def _bn(self, i):
         if not self.use_batch_norm:
@@ -511,7 +566,7 @@ class FlowGNN(nn.Module):
         bout = layer.lin_skip.bias.detach().float().contiguous()
         return wqk, bqk, wout, bout
 
-    def _output_mlp(self, x, tmp, out):
+    def _output_mlp(self, x, tmp, out, rows=None, inv=None):
         """output_proj (gnn_model.py:90-100, :195): Lin-ReLU-Lin-ReLU-Lin-ReLU-Lin.
         precision "f16x3" with H in {64, 128} and output_dim <= 8: one fused
         launch (mignn_mlp_head, split-fp16 MFMA); otherwise four fp32 launches."""
@@ -532,12 +587,19 @@ class FlowGNN(nn.Module):
                 return img
             img = self._cached("head", 0, ts, make)
             _lib.check(L.mignn_mlp_head(P(x), x.stride(0), x.shape[0], H, P(img), self.output_dim,
-                                        P(out), out.stride(0), _stream(x)), "mignn_mlp_head")
+                                        P(out), out.stride(0), P(rows), _stream(x)),
+                       "mignn_mlp_head")
             return
         h1 = linear(x, l0.weight, l0.bias, relu=True, out=tmp)
         h2 = linear(h1, l3.weight, l3.bias, relu=True, out=x)
         h3 = linear(h2, l6.weight, l6.bias, relu=True)
-        linear(h3, l8.weight, l8.bias, out=out)
+        if inv is None:
+            linear(h3, l8.weight, l8.bias, out=out)
+            return
+        y = linear(h3, l8.weight, l8.bias)          # internal order -> caller order
+        _lib.check(_lib.lib().mignn_rows_gather(
+            _lib.ptr(y), y.stride(0), _lib.ptr(inv), y.shape[0], y.shape[1], _lib.ptr(out),
+            out.stride(0), _stream(y)), "mignn_rows_gather")
 
 
 class FlowGNNSurrogate(nn.Module):

@@ -58,6 +58,27 @@ const char* mignn_last_error(void);
 enum { MIGNN_CSR_VERBATIM = 0, MIGNN_CSR_ONE_SELF_LOOP = 1 };
 
 size_t mignn_csr_scratch_bytes(int64_t num_edges, int64_t num_nodes);
+/* As mignn_csr_build, with every valid node id x of edge_index mapped to
+ * relabel[x] (a permutation of [0, N), e.g. the inverse locality order
+ * below): the CSR of the relabelled graph.  In-row order is still the edge
+ * order of edge_index.  mignn_csr_build == this with relabel = NULL. */
+int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                              int mode, const int32_t* relabel, int32_t* row_ptr, int32_t* col,
+                              float* dinv, int64_t* info, void* scratch, size_t scratch_bytes,
+                              void* stream);
+
+/* Locality order of the nodes for the internal activation layout (no
+ * reference counterpart: the forward's results are the same up to fp32
+ * summation order).  pos: [n, >=3] cell centres (FlowGNN's node features,
+ * reference graph_constructor.py:259), row stride ldp.  Cells of the mesh
+ * spacing (per axis, from the edges) are grouped into 4x4 pencils swept along
+ * the third axis, so a 64-row tile of the fused layer is a 4x4x4 block.
+ * Outputs perm[new] = old node id and inv[old] = new (int32, n each); stable
+ * (ties keep input order).  Scratch: mignn_locality_order_scratch_bytes(n). */
+size_t mignn_locality_order_scratch_bytes(int64_t n);
+int mignn_locality_order(const float* pos, int64_t ldp, int64_t n, const int64_t* edge_index,
+                         int64_t num_edges, int32_t* perm, int32_t* inv, void* scratch,
+                         size_t scratch_bytes, void* stream);
 int mignn_csr_build(const int64_t* edge_index, /* [2, E] int64, contiguous */
                     int64_t num_edges, int64_t num_nodes, int mode,
                     int32_t* row_ptr, int32_t* col, float* dinv, int64_t* info,
@@ -97,6 +118,11 @@ int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
  * input_proj, gnn_model.py:55, :159. */
 int mignn_input_proj(const float* x, int64_t n, int in_dim, const float* w, const float* b,
                      int h, float* out, int64_t ldo, void* stream);
+/* out row r = Linear(x row rows[r]) (rows = NULL: r): the projection gathered
+ * into the locality order. */
+int mignn_input_proj_rows(const float* x, int64_t n, int in_dim, const int32_t* rows,
+                          const float* w, const float* b, int h, float* out, int64_t ldo,
+                          void* stream);
 
 /* BatchNorm1d eval fold: scale = w / sqrt(var + eps), shift = b - mean*scale
  * (the same fold ATen's CPU batch_norm applies).  BatchNorm, gnn_model.py:87. */
@@ -170,13 +196,15 @@ int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const floa
  * (mignn_mlp_head_prep_bytes(h) bytes, 16-B aligned, device memory); call
  * it again whenever a weight or bias changes.  Replaces the four nn.Linear
  * launches of FlowGNN.output_proj (eval mode: Dropout is the identity).
- * Error vs fp64 ~1e-6 relative.  x: n rows of h floats, 16-B aligned rows. */
+ * Error vs fp64 ~1e-6 relative.  x: n rows of h floats, 16-B aligned rows;
+ * result row r goes to out row out_rows[r] (NULL: r), i.e. back from the
+ * locality order to the caller's node order. */
 size_t mignn_mlp_head_prep_bytes(int h);
 int mignn_mlp_head_prep(const float* w1, const float* b1, const float* w2, const float* b2,
                         const float* w3, const float* b3, const float* w4, const float* b4,
                         int h, int out_dim, void* img, size_t img_bytes, void* stream);
 int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, const void* img, int out_dim,
-                   float* out, int64_t ldo, void* stream);
+                   float* out, int64_t ldo, const int32_t* out_rows, void* stream);
 
 /* Fused GIN layer (gnn_model.py:70-75, :166, :184-191), h in {64, 128}:
  *   tmp_i = relu(nn.0( sum_{j in row i} x_j + (1 + eps) x_i ))      (rows rb..re -> tmp[0..])

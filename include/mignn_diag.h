@@ -23,6 +23,10 @@ int mignn_diag_set_trace_f16x3(void* buf);
 
 /* Fused output head (H = 128, out_dim 7) timing ablations: mode bit 1 = no x
  * loads, bit 2 = no MFMAs (results wrong by design). */
+/* Shader clock probe: `blocks` workgroups of 4*iters dependent FMAs each;
+ * out[2b] = s_memtime delta, out[2b+1] = s_memrealtime delta (100 MHz). */
+int mignn_diag_clock(int blocks, int iters, int64_t* out, void* stream);
+
 int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img, float* out,
                         void* stream);
 #ifdef __cplusplus

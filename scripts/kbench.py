@@ -23,10 +23,10 @@ n = x0.shape[0]
 if os.environ.get("KB_PERM"):
     # relabel the mesh into k-pencils of BI x BJ columns (locality experiment)
     bi, bj = (int(v) for v in os.environ["KB_PERM"].split(","))
-    assert nx % bi == 0 and ny % bj == 0
+    # edge pencils may be narrower (ceil division)
     ids = torch.arange(n, device=dev)
     i, j, k = ids % nx, (ids // nx) % ny, ids // (nx * ny)
-    npi = nx // bi
+    npi = (nx + bi - 1) // bi
     key = ((((j // bj) * npi + (i // bi)) * nz + k) * bj + (j % bj)) * bi + (i % bi)
     pos = torch.empty_like(ids)
     pos[torch.argsort(key)] = ids
@@ -101,7 +101,7 @@ HOUT = torch.empty(n, 7, device=dev)
 
 
 def head16(_):
-    _lib.check(L.mignn_mlp_head(P(X), H, n, H, P(HIMG), 7, P(HOUT), 7, st), "head")
+    _lib.check(L.mignn_mlp_head(P(X), H, n, H, P(HIMG), 7, P(HOUT), 7, None, st), "head")
 
 
 def headdiag(mode):
@@ -148,6 +148,15 @@ cases = {
 }
 if os.environ.get("KB_ONLY"):
     cases = {k: v for k, v in cases.items() if any(t in k for t in os.environ["KB_ONLY"].split(","))}
+def clock_mhz(blocks=1024, iters=200000):
+    buf = torch.zeros(2 * blocks, dtype=torch.int64, device=dev)
+    _lib.check(L.mignn_diag_clock(blocks, iters, P(buf), st), "clock")
+    torch.cuda.synchronize()
+    b = buf.view(blocks, 2).double().cpu()
+    return round(float((b[:, 0] / b[:, 1]).median() * 100.0), 1)
+
+
+clock_before = clock_mhz()
 times = {k: [] for k in cases}
 for rnd in range(5):
     for k, (fn, fl) in cases.items():
@@ -161,6 +170,7 @@ for rnd in range(5):
         if rnd > 0:
             times[k].append(e0.elapsed_time(e1) / 3)
 res = {k: round(statistics.median(v), 4) for k, v in times.items()}
+res["clock_mhz_before_after"] = [clock_before, clock_mhz()]
 if os.environ.get("KB_TRACE"):
     buf = torch.zeros(8 * 64 * 8, dtype=torch.int64, device=dev)
     _lib.check(L.mignn_diag_set_trace_f16x3(P(buf)), "trace")

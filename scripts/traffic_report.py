@@ -15,7 +15,7 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 config = sys.argv[2] if len(sys.argv) > 2 else "GCN_L4_H128_250x200x200"
-KERNEL = "fused_tile_kernel<128, 128, 0, true>"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "gcn_f16x3_kernel<128>"
 vals = {}
 for f in glob.glob(f"{root}/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):

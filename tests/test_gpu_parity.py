@@ -224,8 +224,8 @@ def test_mlp_head_f16x3_vs_fp64(H, case):
     _lib.check(L.mignn_mlp_head_prep(*wb, H, od, P(img), img.numel(), _lib.stream()),
                "mlp_head_prep")
     out = torch.full((n, od + pado), float("nan"), device=DEV)
-    _lib.check(L.mignn_mlp_head(P(x), ld, n, H, P(img), od, P(out), od + pado, _lib.stream()),
-               "mlp_head")
+    _lib.check(L.mignn_mlp_head(P(x), ld, n, H, P(img), od, P(out), od + pado, None,
+                                _lib.stream()), "mlp_head")
     ref = _head_ref(x, ws, bs)
     got = out.cpu().double()
     scale = max(1.0, ref.abs().max().item())
@@ -234,25 +234,116 @@ def test_mlp_head_f16x3_vs_fp64(H, case):
     assert torch.isnan(got[:, od:]).all()
 
 
+def test_mlp_head_scatter_rows():
+    """out_rows: result row r lands in out row out_rows[r] (locality order ->
+    caller order); identical values to the unscattered launch."""
+    H, n, od = 128, 777, 7
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, H, generator=g).to(DEV)
+    dims = [(H, H), (H, H), (H // 2, H), (od, H // 2)]
+    ws = [(torch.randn(o, i, generator=g) / math.sqrt(i)).to(DEV) for o, i in dims]
+    bs = [(torch.randn(o, generator=g) * 0.1).to(DEV) for o, _ in dims]
+    L, P = _lib.lib(), _lib.ptr
+    img = torch.empty(L.mignn_mlp_head_prep_bytes(H), dtype=torch.uint8, device=DEV)
+    wb = [P(t) for pair in zip(ws, bs) for t in pair]
+    _lib.check(L.mignn_mlp_head_prep(*wb, H, od, P(img), img.numel(), _lib.stream()), "prep")
+    rows = torch.randperm(n, generator=g).to(torch.int32).to(DEV)
+    a = torch.full((n, od), float("nan"), device=DEV)
+    b = torch.full((n, od), float("nan"), device=DEV)
+    _lib.check(L.mignn_mlp_head(P(x), H, n, H, P(img), od, P(a), od, None, _lib.stream()), "a")
+    _lib.check(L.mignn_mlp_head(P(x), H, n, H, P(img), od, P(b), od, P(rows), _lib.stream()), "b")
+    assert torch.equal(b[rows.long()], a)
+
+
 def test_mlp_head_rejects_bad_shapes():
     L, P = _lib.lib(), _lib.ptr
     x = torch.zeros(4, 96, device=DEV)
     img = torch.zeros(1 << 18, dtype=torch.uint8, device=DEV)
     out = torch.zeros(4, 8, device=DEV)
-    rc = L.mignn_mlp_head(P(x), 96, 4, 96, P(img), 7, P(out), 8, _lib.stream())
+    rc = L.mignn_mlp_head(P(x), 96, 4, 96, P(img), 7, P(out), 8, None, _lib.stream())
     assert rc == 1 and "h must be 64 or 128" in _lib.last_error()
-    rc = L.mignn_mlp_head(P(x), 96, 4, 64, P(img), 9, P(out), 8, _lib.stream())
+    rc = L.mignn_mlp_head(P(x), 96, 4, 64, P(img), 9, P(out), 8, None, _lib.stream())
     assert rc == 1
-    rc = L.mignn_mlp_head(P(x) + 4, 96, 4, 64, P(img), 7, P(out), 8, _lib.stream())
+    rc = L.mignn_mlp_head(P(x) + 4, 96, 4, 64, P(img), 7, P(out), 8, None, _lib.stream())
     assert rc == 1 and "16-B" in _lib.last_error()
 
 
+# ------------------------------------------------------------------ locality order
+def _pencil_order_np(nx, ny, nz):
+    """numpy restatement of the 4x4-pencil key on the natural grid labels."""
+    v = np.arange(nx * ny * nz)
+    i, j, k = v % nx, (v // nx) % ny, v // (nx * ny)
+    nbx = (nx + 3) // 4
+    key = (((j // 4) * nbx + i // 4) * nz + k) * 16 + (j % 4) * 4 + i % 4
+    return np.argsort(key, kind="stable")
+
+
+@pytest.mark.parametrize("dims", [(12, 8, 10), (10, 9, 7), (250, 20, 6)])
+def test_locality_order_grid(dims):
+    from mignn.gnn_model import locality_order
+    x, ei = grid_graph(*dims, device=DEV)
+    perm, inv = locality_order(x, ei)
+    n = x.shape[0]
+    p = perm.cpu().numpy()
+    assert np.array_equal(np.sort(p), np.arange(n))
+    assert np.array_equal(inv.cpu().numpy()[p], np.arange(n))
+    assert np.array_equal(p, _pencil_order_np(*dims))
+
+
+def test_locality_order_shuffled_and_degenerate():
+    """A relabelled grid gets the same cells in the same order (by position);
+    no edges / coincident points / a flat mesh still give a permutation."""
+    from mignn.gnn_model import locality_order
+    x0, ei0 = grid_graph(12, 8, 10, device=DEV)
+    x1, ei1 = grid_graph(12, 8, 10, device=DEV, permute_seed=3)
+    p0, _ = locality_order(x0, ei0)
+    p1, _ = locality_order(x1, ei1)
+    assert torch.equal(x0[p0.long()], x1[p1.long()])
+    for x, ei in ((torch.rand(1000, 3, device=DEV), torch.zeros(2, 0, dtype=torch.int64, device=DEV)),
+                  (torch.zeros(50, 3, device=DEV), torch.randint(0, 50, (2, 200), device=DEV)),
+                  (torch.cat([torch.rand(300, 2), torch.zeros(300, 1)], 1).to(DEV),
+                   torch.randint(0, 300, (2, 900), device=DEV)),
+                  # NaN rows, 1e+-30 magnitudes, invalid edge ids
+                  (torch.where(torch.rand(400, 1) < 0.1, torch.tensor(float("nan")),
+                               torch.randn(400, 3) * 10.0 ** torch.randint(-30, 31, (400, 3)))
+                   .to(DEV), torch.randint(-5, 405, (2, 1200), device=DEV))):
+        perm, inv = locality_order(x, ei)
+        n = x.shape[0]
+        assert torch.equal(perm.sort().values.cpu(), torch.arange(n, dtype=torch.int32))
+        assert torch.equal(inv[perm.long()].cpu(), torch.arange(n, dtype=torch.int32))
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("layer_type", ["GCN", "GAT", "GIN", "Transformer"])
+def test_flowgnn_reorder_matches_natural(layer_type, precision):
+    """The internal locality order changes only the summation order: forward
+    with MIGNN_REORDER=1 equals the unreordered forward to fp32 rounding, on
+    the natural and the shuffled grid."""
+    H = 64
+    cfg = dict(hidden_dim=H, num_layers=2, layer_type=layer_type)
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=1))
+    m = m.to(DEV).eval()
+    m.precision = precision
+    for seed in (None, 4):
+        x, ei = grid_graph(14, 9, 11, device=DEV, permute_seed=seed)
+        with torch.no_grad():
+            m.reorder = "0"
+            y0 = m(x, ei)
+            m.reorder = "1"
+            y1 = m(x, ei)
+        err = (y0 - y1).abs().max().item()
+        assert err < 2e-6, (layer_type, precision, seed, err)
+
+
 # ------------------------------------------------------------------ end-to-end parity
+@pytest.mark.parametrize("reorder", ["0", "1"])
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", model_names())
-def test_flowgnn_bfs_parity(name, precision):
+def test_flowgnn_bfs_parity(name, precision, reorder):
     cfg, sd, outs, err = model_fixture(name)
     m = make_model(cfg, sd, precision)
+    m.reorder = reorder
     for gname, (y32, y64) in outs.items():
         x, ei, ea = bfs_graph(gname)
         ea_in = None if cfg["layer_type"] == "Transformer" else ea.to(DEV)
@@ -260,7 +351,8 @@ def test_flowgnn_bfs_parity(name, precision):
             y = m(x.to(DEV), ei.to(DEV), ea_in).cpu()
         e32 = (y - y32).abs().max().item()
         e64 = (y.double() - y64).abs().max().item()
-        print(f"{name} {gname} {precision}: max|gpu-cpu32| {e32:.2e}  max|gpu-fp64| {e64:.2e}")
+        print(f"{name} {gname} {precision} reorder={reorder}: max|gpu-cpu32| {e32:.2e}  "
+              f"max|gpu-fp64| {e64:.2e}")
         assert e32 <= TOL and e64 <= TOL
     if err is not None:
         x, ei, ea = bfs_graph("train")
@@ -269,11 +361,13 @@ def test_flowgnn_bfs_parity(name, precision):
         assert str(exc.value).split("\n")[0] == err
 
 
+@pytest.mark.parametrize("reorder", ["0", "1"])
 @pytest.mark.parametrize("name", tiny_names())
 @pytest.mark.parametrize("lt", ["GCN", "GAT", "GIN", "Transformer"])
-def test_flowgnn_tiny_edge_cases(name, lt):
+def test_flowgnn_tiny_edge_cases(name, lt, reorder):
     x, ei, sd, y32, y64 = tiny_fixture(name, lt)
     m = make_model(dict(hidden_dim=8, num_layers=2, layer_type=lt), sd)
+    m.reorder = reorder
     with torch.no_grad():
         y = m(x.to(DEV), ei.to(DEV)).cpu()
     assert (y.double() - y64).abs().max().item() <= TOL
