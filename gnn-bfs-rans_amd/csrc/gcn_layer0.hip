@@ -1,0 +1,121 @@
+// input_proj + first GCN layer in one pass over the coordinates.
+//
+// FlowGNN's first two steps (gnn_model.py:159, :162-192 with GCNConv) are
+//   x0_i = W_in c_i + b_in                                   (c_i: D <= 8 features)
+//   y_i  = relu( sc * (x0_i + b + W sum_j w_ij x0_j) + sh )  (eval BN folded in sc, sh)
+// and both maps are linear up to the ReLU, so with C_i = sum_j w_ij c_j and
+// s_i = sum_j w_ij (the CSR row incl. the self-loop, PyG gcn_norm weights):
+//   y_i = relu( A c_i + B C_i + d s_i + e ),
+//   A = diag(sc) W_in, B = diag(sc) W W_in, d = sc * (W b_in), e = sc * (b_in + b) + sh
+// (coefficients composed in fp64 by the host, mignn.h).  The [N, H] x0 is
+// never materialised: the kernel reads 12-32 B per neighbour instead of a
+// 512-B row and writes y once -- an HBM-write-bound pass (N*H*4 bytes).
+//
+// Layout: a wave takes 64 consecutive rows; pass 1, lane = row: gather and
+// aggregate (c_i, C_i, s_i) in CSR order into LDS; pass 2, 32 lanes x 16 B
+// per row: each lane owns 4 output columns (their 4 x (2D+2) coefficients in
+// registers) and writes two rows per store instruction (non-temporal).
+#include "common.hpp"
+
+namespace mignn {
+namespace {
+
+constexpr int kWaves = 4;
+
+template <int D>
+__global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
+    int64_t row_end, const float* __restrict__ coef, int h, float* __restrict__ out,
+    int64_t ldo) {
+    constexpr int K = 2 * D + 2;                  // coefficients per column
+    __shared__ float agg[kWaves][64][2 * D + 2];   // c_i | C_i | s_i | pad
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    float (*ag)[2 * D + 2] = agg[wave];
+    const int cpl = h / 4;                         // lanes per row (<= 64)
+    const int rps = 64 / cpl;                      // rows per store instruction
+    const int sub = lane / cpl, cq = (lane % cpl) * 4;
+    const bool active = sub < rps;
+    float cf[4][K];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < K; ++k) cf[q][k] = active ? coef[(int64_t)(cq + q) * K + k] : 0.f;
+
+    const int64_t nrows = row_end - row_begin;
+    const int64_t stride = (int64_t)gridDim.x * kWaves * 64;
+    for (int64_t base = ((int64_t)blockIdx.x * kWaves + wave) * 64; base < nrows; base += stride) {
+        // pass 1: lane = row
+        const int64_t r = base + lane;
+        if (r < nrows) {
+            const int64_t i = row_begin + r;
+            float c[D], C[D], s = 0.f;
+#pragma unroll
+            for (int a = 0; a < D; ++a) { c[a] = pos[i * ldp + a]; C[a] = 0.f; }
+            const int32_t e0 = row_ptr[i], e1 = row_ptr[i + 1];
+            for (int32_t e = e0; e < e1; ++e) {
+                const int64_t j = col[e];
+                const float w = ew[e];
+                s += w;
+#pragma unroll
+                for (int a = 0; a < D; ++a) C[a] = fmaf(w, pos[j * ldp + a], C[a]);
+            }
+#pragma unroll
+            for (int a = 0; a < D; ++a) { ag[lane][a] = c[a]; ag[lane][D + a] = C[a]; }
+            ag[lane][2 * D] = s;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+        // pass 2: rps rows per instruction, lane owns columns cq .. cq + 3
+        const int64_t nblk = nrows - base < 64 ? nrows - base : 64;
+        for (int rr = 0; rr < nblk; rr += rps) {
+            const int rl = rr + sub;
+            if (active && rl < nblk) {
+                float v[K - 1];
+#pragma unroll
+                for (int k = 0; k < K - 1; ++k) v[k] = ag[rl][k];
+                float o[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float t = cf[q][K - 1];
+#pragma unroll
+                    for (int k = 0; k < K - 1; ++k) t = fmaf(cf[q][k], v[k], t);
+                    o[q] = t < 0.f ? 0.f : t;
+                }
+                f32x4* const dst = reinterpret_cast<f32x4*>(out + (row_begin + base + rl) * ldo + cq);
+                __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, dst);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();   // pass 1 of the next block overwrites ag
+    }
+}
+
+}  // namespace
+}  // namespace mignn
+
+using namespace mignn;
+
+extern "C" int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                                       const float* pos, int64_t ldp, int in_dim,
+                                       int64_t row_begin, int64_t row_end, const float* coef,
+                                       int h, float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(row_ptr && col && ew && pos && coef && out, "gcn_layer0: null pointer");
+    MIGNN_REQUIRE(in_dim >= 1 && in_dim <= 4, "gcn_layer0: in_dim must be 1..4 (got %d)", in_dim);
+    MIGNN_REQUIRE(ldp >= in_dim, "gcn_layer0: ldp < in_dim");
+    MIGNN_REQUIRE(h % 4 == 0 && h >= 4 && h <= 256 && (64 % (h / 4)) == 0,
+                  "gcn_layer0: h must be 4*2^k <= 256 (got %d)", h);
+    MIGNN_REQUIRE(ldo % 4 == 0 && aligned16(out), "gcn_layer0: out rows must be 16-B aligned");
+    MIGNN_REQUIRE(row_begin >= 0 && row_end >= row_begin, "gcn_layer0: bad row range");
+    if (row_end == row_begin) return MIGNN_OK;
+    hipStream_t st = as_stream(stream);
+    const int64_t blocks = (row_end - row_begin + kWaves * 64 - 1) / (kWaves * 64);
+    const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);
+    switch (in_dim) {
+    case 1: hipLaunchKernelGGL(gcn_layer0_kernel<1>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    case 2: hipLaunchKernelGGL(gcn_layer0_kernel<2>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    case 3: hipLaunchKernelGGL(gcn_layer0_kernel<3>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    default: hipLaunchKernelGGL(gcn_layer0_kernel<4>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    }
+    return launch_status("gcn_layer0_kernel");
+}

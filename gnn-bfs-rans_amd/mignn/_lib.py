@@ -53,6 +53,8 @@ SIGNATURES = {
     "mignn_locality_order_scratch_bytes": (c_size_t, [c_int64]),
     "mignn_locality_order": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P, _P, c_size_t,
                                      _P]),
+    "mignn_gcn_layer0_coords": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,
+                                        c_int, _P, c_int64, _P]),
     "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),

@@ -372,10 +372,21 @@ class FlowGNN(nn.Module):
         mode = CSR_ONE_SELF_LOOP if self.layer_type in ("GCN", "GAT") else CSR_VERBATIM
         pos = xin if self._use_reorder(xin) else None
         csr = self._csr.get(edge_index, num_nodes, mode, pos)
-        # input_proj (gnn_model.py:159), gathered into the CSR's node order
-        self._input_proj(xin, buf_a, rows=csr.perm)
         cur, nxt = buf_a, buf_b
+        first = 0
+        if self._fuse_layer0():
+            # input_proj + GCN layer 0 from the coordinates (mignn_gcn_layer0_coords)
+            try:
+                self._gcn_layer0(xin, csr, cur)
+            except RuntimeError as e:
+                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
+            first = 1
+        else:
+            # input_proj (gnn_model.py:159), gathered into the CSR's node order
+            self._input_proj(xin, cur, rows=csr.perm)
         for i, layer in enumerate(self.gnn_layers):
+            if i < first:
+                continue
             try:
                 if self.layer_type == "Transformer" and edge_attr is not None:
                     # PyG TransformerConv.message adds a non-None edge_attr to value_j
@@ -421,6 +432,50 @@ class FlowGNN(nn.Module):
             f"  edge_index range: {rng}\n"
             f"  x shape: {x.shape}, edge_attr shape: "
             f"{edge_attr.shape if edge_attr is not None else 'None'}")
+
+    def _fuse_layer0(self) -> bool:
+        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GCN"
+                and self.num_layers > 0 and 1 <= self.input_dim <= 4
+                and self.hidden_dim in (4, 8, 16, 32, 64, 128, 256))
+
+    def _layer0_coef(self):
+        """A = diag(sc) W_in, B = diag(sc) W W_in, d = sc*(W b_in), e = sc*(b_in + b) + sh
+        per output column, fp64-composed (gcn_layer0.hip)."""
+        layer = self.gnn_layers[0]
+        ts = [self.input_proj.weight, self.input_proj.bias, layer.lin.weight, layer.bias]
+        if self.use_batch_norm:
+            bn = self.batch_norms[0].module
+            ts += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
+
+        def make():
+            Win, bin_ = (t.detach().double() for t in ts[:2])
+            W, b = (t.detach().double() for t in ts[2:4])
+            if self.use_batch_norm:
+                bn = self.batch_norms[0].module
+                sc = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+                sh = bn.bias.double() - bn.running_mean.double() * sc
+            else:
+                sc = torch.ones_like(b)
+                sh = torch.zeros_like(b)
+            A = sc[:, None] * Win
+            B = sc[:, None] * (W @ Win)
+            d = sc * (W @ bin_)
+            e = sc * (bin_ + b) + sh
+            return torch.cat([A, B, d[:, None], e[:, None]], 1).float().contiguous()
+        return self._cached("layer0", 0, ts, make)
+
+    def _gcn_layer0(self, x, csr: Csr, out):
+        D = self.input_dim
+        pos = x
+        if csr.perm is not None:       # coordinates in the CSR's node order
+            pos = torch.empty((x.shape[0], D), dtype=torch.float32, device=x.device)
+            _lib.check(_lib.lib().mignn_rows_gather(
+                _lib.ptr(x), x.stride(0), _lib.ptr(csr.perm), x.shape[0], D, _lib.ptr(pos), D,
+                _stream(x)), "mignn_rows_gather")
+        _lib.check(_lib.lib().mignn_gcn_layer0_coords(
+            _lib.ptr(csr.row_ptr), _lib.ptr(csr.col), _lib.ptr(csr.ew), _lib.ptr(pos),
+            pos.stride(0), D, 0, x.shape[0], _lib.ptr(self._layer0_coef()), self.hidden_dim,
+            _lib.ptr(out), out.stride(0), _stream(x)), "mignn_gcn_layer0_coords")
 
     def _use_reorder(self, x) -> bool:
         if self.reorder not in ("auto", "0", "1"):

@@ -206,6 +206,19 @@ int mignn_mlp_head_prep(const float* w1, const float* b1, const float* w2, const
 int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, const void* img, int out_dim,
                    float* out, int64_t ldo, const int32_t* out_rows, void* stream);
 
+/* input_proj + GCN layer 0 in one pass (gnn_model.py:159, :162-192): both are
+ * linear up to the ReLU, so with C_i = sum_{j in row i} ew_j pos_j and
+ * s_i = sum ew_j (CSR row incl. the self-loop):
+ *   out_i = relu( A pos_i + B C_i + d s_i + e )
+ * coef: [h][2*in_dim + 2] floats per output column n = {A[n][:], B[n][:], d[n],
+ * e[n]} with A = diag(sc) W_in, B = diag(sc) W W_in, d = sc*(W b_in),
+ * e = sc*(b_in + b) + sh (composed by the caller, fp64).  pos: rows of
+ * in_dim (1..4) features, stride ldp, in the CSR's node order.  h = 4*2^k. */
+int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                            const float* pos, int64_t ldp, int in_dim, int64_t row_begin,
+                            int64_t row_end, const float* coef, int h, float* out, int64_t ldo,
+                            void* stream);
+
 /* Fused GIN layer (gnn_model.py:70-75, :166, :184-191), h in {64, 128}:
  *   tmp_i = relu(nn.0( sum_{j in row i} x_j + (1 + eps) x_i ))      (rows rb..re -> tmp[0..])
  *   out_i = epi( nn.2(tmp_i) ) with residual x_i, BN affine, ReLU   (flags as above)

@@ -336,6 +336,25 @@ def test_flowgnn_reorder_matches_natural(layer_type, precision):
         assert err < 2e-6, (layer_type, precision, seed, err)
 
 
+@pytest.mark.parametrize("H,bn,reorder", [(64, True, "0"), (128, True, "1"), (128, False, "0"),
+                                         (32, True, "1")])
+def test_gcn_layer0_fusion_matches(H, bn, reorder, monkeypatch):
+    """input_proj + GCN layer 0 composed into one pass over the coordinates
+    (mignn_gcn_layer0_coords) equals the two-step path to fp32 rounding."""
+    cfg = dict(hidden_dim=H, num_layers=2, layer_type="GCN", use_batch_norm=bn)
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=2))
+    m = m.to(DEV).eval()
+    m.reorder = reorder
+    x, ei = grid_graph(13, 10, 9, device=DEV, permute_seed=2)
+    with torch.no_grad():
+        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "0")
+        y0 = m(x, ei)
+        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "1")
+        y1 = m(x, ei)
+    assert (y0 - y1).abs().max().item() < 2e-6
+
+
 # ------------------------------------------------------------------ end-to-end parity
 @pytest.mark.parametrize("reorder", ["0", "1"])
 @pytest.mark.parametrize("precision", PRECISIONS)
