@@ -22,7 +22,7 @@ namespace {
 
 constexpr int kWaves = 4;
 
-template <int D>
+template <int D, int DIAG = 0>   // DIAG (timing ablations): 1 = no gathers, 2 = no stores
 __global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
@@ -48,13 +48,39 @@ __global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
     for (int64_t base = ((int64_t)blockIdx.x * kWaves + wave) * 64; base < nrows; base += stride) {
         // pass 1: lane = row
         const int64_t r = base + lane;
-        if (r < nrows) {
+        if constexpr ((DIAG & 1) != 0) {
+            ag[lane][0] = static_cast<float>(r);
+        } else if (r < nrows) {
             const int64_t i = row_begin + r;
             float c[D], C[D], s = 0.f;
 #pragma unroll
             for (int a = 0; a < D; ++a) { c[a] = pos[i * ldp + a]; C[a] = 0.f; }
             const int32_t e0 = row_ptr[i], e1 = row_ptr[i + 1];
-            for (int32_t e = e0; e < e1; ++e) {
+            // first kU entries: all index loads, then all coordinate loads (two
+            // memory round trips instead of one per entry); CSR order kept
+            constexpr int kU = 8;
+            int32_t jj[kU];
+            float ww[kU];
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                jj[k] = e0 + k < e1 ? col[e0 + k] : 0;
+                ww[k] = e0 + k < e1 ? ew[e0 + k] : 0.f;
+            }
+            float pv[kU][D];
+#pragma unroll
+            for (int k = 0; k < kU; ++k)
+#pragma unroll
+                for (int a = 0; a < D; ++a)
+                    pv[k][a] = e0 + k < e1 ? pos[(int64_t)jj[k] * ldp + a] : 0.f;
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                if (e0 + k < e1) {
+                    s += ww[k];
+#pragma unroll
+                    for (int a = 0; a < D; ++a) C[a] = fmaf(ww[k], pv[k][a], C[a]);
+                }
+            }
+            for (int32_t e = e0 + kU; e < e1; ++e) {   // rows of > kU entries
                 const int64_t j = col[e];
                 const float w = ew[e];
                 s += w;
@@ -84,7 +110,9 @@ __global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
                     o[q] = t < 0.f ? 0.f : t;
                 }
                 f32x4* const dst = reinterpret_cast<f32x4*>(out + (row_begin + base + rl) * ldo + cq);
-                __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, dst);
+                if constexpr ((DIAG & 2) == 0)
+                    __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, dst);
+                else if (o[0] == 1234.5f) *dst = f32x4{o[0], o[1], o[2], o[3]};
             }
         }
         __builtin_amdgcn_wave_barrier();   // pass 1 of the next block overwrites ag
@@ -118,4 +146,20 @@ extern "C" int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* co
     default: hipLaunchKernelGGL(gcn_layer0_kernel<4>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
     }
     return launch_status("gcn_layer0_kernel");
+}
+
+extern "C" int mignn_diag_gcn_layer0(int mode, const int32_t* row_ptr, const int32_t* col,
+                                     const float* ew, const float* pos, int64_t n,
+                                     const float* coef, float* out, void* stream) {
+    MIGNN_REQUIRE(mode >= 0 && mode <= 3 && n > 0, "diag_gcn_layer0: bad args");
+    hipStream_t st = as_stream(stream);
+    const int64_t blocks = (n + kWaves * 64 - 1) / (kWaves * 64);
+    const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL((gcn_layer0_kernel<3, 0>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
+    case 1: hipLaunchKernelGGL((gcn_layer0_kernel<3, 1>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
+    case 2: hipLaunchKernelGGL((gcn_layer0_kernel<3, 2>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
+    default: hipLaunchKernelGGL((gcn_layer0_kernel<3, 3>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
+    }
+    return launch_status("gcn_layer0_kernel(diag)");
 }

@@ -55,6 +55,13 @@ SIGNATURES = {
                                      _P]),
     "mignn_gcn_layer0_coords": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,
                                         c_int, _P, c_int64, _P]),
+    "mignn_mesh_graph_scratch_bytes": (c_size_t, [c_int64, c_int64]),
+    "mignn_mesh_graph_count": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, _P, c_int64, c_int,
+                                       _P, _P, c_size_t, _P]),
+    "mignn_mesh_graph_emit": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, _P, _P, c_int,
+                                      c_int64, _P, _P, _P, c_int64, _P, c_size_t, _P]),
+    "mignn_edge_attributes": (c_int, [_P, c_int64, c_int64, _P, _P, _P]),
+    "mignn_boundary_mask": (c_int, [_P, c_int64, c_int64, c_int64, c_int64, _P, _P]),
     "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),
@@ -69,6 +76,7 @@ DIAG_SIGNATURES = {
                                   _P]),
     "mignn_diag_set_trace": (c_int, [_P]),
     "mignn_diag_set_trace_f16x3": (c_int, [_P]),
+    "mignn_diag_gcn_layer0": (c_int, [c_int, _P, _P, _P, _P, c_int64, _P, _P, _P]),
     "mignn_diag_clock": (c_int, [c_int, c_int, _P, _P]),
     "mignn_diag_mlp_head": (c_int, [c_int, _P, c_int64, _P, _P, _P]),
 }

@@ -230,6 +230,41 @@ int mignn_gin_layer(const int32_t* row_ptr, const int32_t* col, const float* x, 
                     float* tmp, int64_t ldt, float* out, int64_t ldo, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Mesh -> graph (reference graph_constructor.py).
+ * owner [n_faces] / neighbour [n_internal_faces] int64 cell ids as read from
+ * the OpenFOAM polyMesh, cell_centers float64 [n_cells, 3].
+ *   mode ALL:     build_edge_index (:28-56) + build_graph's validation (:166-172)
+ *   mode FIRST_N: build_graph(filter_internal=True, n_internal_cells=n_first)
+ *   mode MASK:    build_graph(filter_internal=True) with the mesh internal_mask
+ * isolated = 1: nodes in no edge get an appended self-loop (:174-187, :221-226);
+ * 0: not (build_edge_index alone).  Same edge order, rules and float64 edge
+ * attributes (rounded to float32) as the reference.
+ * mignn_mesh_graph_count writes device counts[4] = {n_nodes, face edges,
+ * isolated self-loops, total edges E}; the caller reads E, allocates
+ * edge_index [2, E] int64, edge_attr [E, 4] and x [n_nodes, ldx] and calls
+ * mignn_mesh_graph_emit with the SAME scratch.  x row i = features row of the
+ * i-th kept cell (feat_dim float64 values, rounded to float32); x may be NULL.
+ * ------------------------------------------------------------------------ */
+enum { MIGNN_MESH_ALL = 0, MIGNN_MESH_FIRST_N = 1, MIGNN_MESH_MASK = 2 };
+size_t mignn_mesh_graph_scratch_bytes(int64_t n_faces, int64_t n_cells);
+int mignn_mesh_graph_count(const int64_t* owner, int64_t n_faces, const int64_t* neighbour,
+                           int64_t n_internal_faces, int64_t n_cells, int mode,
+                           const uint8_t* mask, int64_t n_first, int isolated, int64_t* counts,
+                           void* scratch, size_t scratch_bytes, void* stream);
+int mignn_mesh_graph_emit(const int64_t* owner, int64_t n_faces, const int64_t* neighbour,
+                          int64_t n_internal_faces, int64_t n_cells, int mode,
+                          const double* cell_centers, const double* features, int feat_dim,
+                          int64_t num_edges, int64_t* edge_index, float* edge_attr, float* x,
+                          int64_t ldx, void* scratch, size_t scratch_bytes, void* stream);
+/* compute_edge_attributes (:58-90) of any [2, E] edge list over n cells;
+ * an out-of-range index gives zeros (build_graph's check, :196-200) */
+int mignn_edge_attributes(const int64_t* edge_index, int64_t num_edges, int64_t n,
+                          const double* cell_centers, float* edge_attr, void* stream);
+/* get_boundary_mask (:276-296): mask[c] = 1 for owners of the patch's faces */
+int mignn_boundary_mask(const int64_t* owner, int64_t n_faces, int64_t start_face,
+                        int64_t n_boundary_faces, int64_t n_cells, uint8_t* mask, void* stream);
+
+/* ------------------------------------------------------------------------
  * Multi-GPU halo helpers and synthetic inputs.
  * ------------------------------------------------------------------------ */
 /* dst[r, :] = src[idx[r], :] for r < n (halo pack / unpack by index list) */

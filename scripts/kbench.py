@@ -116,6 +116,31 @@ def head32(_):
     linear(h3, HW[3], HB[3], out=HOUT)
 
 
+L0COEF = torch.randn(H, 8, device=dev, generator=g) * 0.1
+X0 = x0.contiguous()
+
+
+def layer0(_):
+    _lib.check(L.mignn_gcn_layer0_coords(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X0), 3, 3, 0, n,
+                                         P(L0COEF), H, P(Y), H, st), "layer0")
+
+
+def fill(_):
+    Y.fill_(1.0)
+
+
+def readsum(_):
+    torch.sum(X, dim=0, out=SUMOUT)
+
+
+SUMOUT = torch.empty(H, device=dev)
+
+
+def layer0diag(mode):
+    _lib.check(L.mignn_diag_gcn_layer0(mode, P(csr.row_ptr), P(csr.col), P(csr.ew), P(X0), n,
+                                       P(L0COEF), P(Y), st), "layer0diag")
+
+
 def copy(_):
     Y.copy_(X)
 
@@ -135,10 +160,11 @@ cases = {
     "gcn16_no_local": (gcn16, 15 | 8192), "gcn16_no_ext_local": (gcn16, 15 | 4096 | 8192),
     "gcn16_only_dma": (gcn16, 15 | 256 | 512), "gcn_no_mfma": (gcn, 15 | 512), "gcn_no_gather": (gcn, 15 | 256),
     "gcn_xmaj": (gcn, 15 | 1024), "gcn_xmaj_no_mfma": (gcn, 15 | 1024 | 512),
-    "head16": (head16, 0), "head16_no_xload": (headdiag, 1), "head16_no_mfma": (headdiag, 2),
+    "layer0": (layer0, 0), "layer0_no_gather": (layer0diag, 1), "layer0_no_store": (layer0diag, 2),
+    "layer0_neither": (layer0diag, 3), "head16": (head16, 0), "head16_no_xload": (headdiag, 1), "head16_no_mfma": (headdiag, 2),
     "head16_valu_only": (headdiag, 3), "head32(4 launches)": (head32, 0),
     "gcn_aggregate_only(simple)": (agg, 0), "linear_rows": (lin, 9),
-    "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0),
+    "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0), "fill(torch)": (fill, 0), "colsum_read(torch)": (readsum, 0),
     "diag_csr_gather": (diag, (0, 0)), "diag_csr_gather_g2048": (diag, (0, 2048)),
     "diag_stencil_gather": (diag, (1, 0)), "diag_stencil_gather_g2048": (diag, (1, 2048)),
     "diag_copy": (diag, (2, 0)), "diag_copy_nt": (diag, (2 | 8, 0)),
@@ -174,7 +200,7 @@ res["clock_mhz_before_after"] = [clock_before, clock_mhz()]
 if os.environ.get("KB_TRACE"):
     buf = torch.zeros(8 * 64 * 8, dtype=torch.int64, device=dev)
     _lib.check(L.mignn_diag_set_trace_f16x3(P(buf)), "trace")
-    gcn16(15 | 2048)
+    gcn16(15 | 2048 | int(os.environ.get("KB_TRACE_FLAGS", "0")))
     torch.cuda.synchronize()
     _lib.check(L.mignn_diag_set_trace_f16x3(None), "trace")
     t = buf.view(8, 64, 8).cpu().double()
