@@ -67,6 +67,7 @@ def parse():
                    help="GCN transform / output head arithmetic (FlowGNN.precision)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-bfs", action="store_true")
+    p.add_argument("--no-graph", action="store_true", help="skip the mesh->graph builder leg")
     p.add_argument("--cpu-grid", default="100,100,100")
     return p.parse_args()
 
@@ -274,6 +275,8 @@ def main():
 
     if rank == 0 and not args.no_bfs:
         line["bfs_mesh"] = bfs_leg(dev)
+    if rank == 0 and world == 1 and not args.no_graph:
+        line["graph_build"] = graph_build_leg(dev, nx, ny, nz, not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_leg(model, sd, cfg, args, dev)
     if rank == 0:
@@ -320,6 +323,45 @@ def bfs_leg(dev):
             "ms_per_forward": round(t * 1e3, 4),
             "edges_per_s": cfg["num_layers"] * ei.shape[1] / t,
             "max_abs_err_vs_ref_cpu": err.max().item(), "mae_vs_ref_cpu": err.mean().item()}
+
+
+def graph_build_leg(dev, nx, ny, nz, with_cpu):
+    """mesh -> graph (GraphConstructor.build_graph, train
+    path: filter_internal, n_internal_cells = all cells) on a blockMesh-ordered
+    polyMesh of the bench's cell count; the numpy oracle (vectorised CPU
+    restatement of the reference's loops) on a bounded 1M-cell sample."""
+    from mignn.graph import GraphConstructor
+    from mignn.synthetic import hex_polymesh
+
+    mesh = hex_polymesh(nx, ny, nz, device=dev)
+    gc = GraphConstructor(mesh, device=dev)
+    n = mesh["n_cells"]
+    kw = dict(node_features=mesh["cell_centers"], filter_internal=True, n_internal_cells=n)
+    g = gc.build_graph(**kw)                     # warm-up
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        g = gc.build_graph(**kw)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts)
+    E = g.num_edges
+    out = {"cells": n, "faces": int(mesh["owner"].numel()), "edges": E,
+           "ms": round(1e3 * t, 3), "edges_per_s": E / t,
+           "note": "includes the one host read of the edge count and the output allocation"}
+    del g, gc, mesh
+    if with_cpu:
+        from oracle import graph_oracle as go
+        m = hex_polymesh(100, 100, 100, device="cpu")
+        mc = {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in m.items()}
+        t0 = time.perf_counter()
+        _, ei, _, _ = go.build_graph(mc, node_features=mc["cell_centers"], filter_internal=True,
+                                     n_internal_cells=mc["n_cells"])
+        tc = time.perf_counter() - t0
+        out["cpu_oracle"] = {"edges_per_s": ei.shape[1] / tc, "s": round(tc, 3), "cores": 1,
+                             "sample": "100x100x100 cells, vectorised numpy oracle"}
+    return out
 
 
 def cpu_leg(model, sd, cfg, args, dev):

@@ -82,3 +82,32 @@ def grid_graph(nx: int, ny: int, nz: int, device="cuda", permute_seed: Optional[
         x = x[inv]
         ei = perm[ei]
     return x, ei
+
+
+def hex_polymesh(nx: int, ny: int, nz: int, device="cuda"):
+    """OpenFOAM-ordered polyMesh connectivity of a non-periodic nx*ny*nz hex
+    block (blockMesh cell order, i fastest): internal faces sorted by owner,
+    then neighbour (c+1, c+nx, c+nx*ny), followed by the boundary faces
+    (-x, +x, -y, +y, -z, +z patches); cell centres on the unit cube.
+    Returns a dict shaped like OpenFOAMLoader.load_mesh() (input synthesis for
+    the graph-builder benchmark / tests)."""
+    n = nx * ny * nz
+    c = torch.arange(n, device=device, dtype=torch.int64)
+    i, j, k = c % nx, (c // nx) % ny, c // (nx * ny)
+    nb = torch.stack([torch.where(i < nx - 1, c + 1, -1), torch.where(j < ny - 1, c + nx, -1),
+                      torch.where(k < nz - 1, c + nx * ny, -1)], 1).reshape(-1)
+    own = c.repeat_interleave(3)
+    keep = nb >= 0
+    owner_int, neigh = own[keep], nb[keep]
+    bnd = [c[i == 0], c[i == nx - 1], c[j == 0], c[j == ny - 1], c[k == 0], c[k == nz - 1]]
+    names = ["xmin", "xmax", "ymin", "ymax", "zmin", "zmax"]
+    starts, o = [], int(owner_int.numel())
+    for b in bnd:
+        starts.append(o)
+        o += int(b.numel())
+    owner = torch.cat([owner_int] + bnd)
+    cc = torch.stack([(i + 0.5) / nx, (j + 0.5) / ny, (k + 0.5) / nz], 1).double()
+    return {"owner": owner, "neighbour": neigh, "cell_centers": cc, "n_cells": n,
+            "internal_mask": torch.ones(n, dtype=torch.bool, device=device),
+            "boundaries": {nm: {"startFace": st, "nFaces": int(b.numel())}
+                           for nm, st, b in zip(names, starts, bnd)}}
