@@ -268,10 +268,19 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const int slot = blockIdx.x >> 3;
     const int per_xcd = G >> 3;
     const int64_t nsteps = (ntiles + G - 1) / G;
-    // at step s the chip covers tiles [sG, (s+1)G); XCD x a contiguous run
-    auto tile_of = [&](int64_t s) -> int64_t { return s * G + (int64_t)xcd * per_xcd + slot; };
-    // own-row image buffer of a tile: (its step index) mod 3
-    auto xbuf_of = [&](int64_t tile) -> int { return static_cast<int>((tile / G) % C::XBUF); };
+    // default: at step s the chip covers tiles [sG, (s+1)G), XCD x a run of
+    // per_xcd of them.  MIGNN_SCHED_XCD_CHUNKS: XCD x walks its own contiguous
+    // range of nsteps * per_xcd tiles (per_xcd per step), so in a locality
+    // order a tile's neighbours were read by the same XCD a step or two
+    // earlier and are still in its L2.
+    const bool chunks = (flags & MIGNN_SCHED_XCD_CHUNKS) != 0;
+    const int64_t chunk = chunks ? nsteps * per_xcd : per_xcd;
+    const int64_t sstride = chunks ? per_xcd : G;
+    auto tile_of = [&](int64_t s) -> int64_t { return (int64_t)xcd * chunk + s * sstride + slot; };
+    // own-row image buffer of a tile of this workgroup: (its step index) mod 3
+    auto xbuf_of = [&](int64_t tile) -> int {
+        return static_cast<int>(((tile - (int64_t)xcd * chunk) / sstride) % C::XBUF);
+    };
 
     if (tid == 0) {
         cntX[0] = 0;

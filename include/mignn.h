@@ -105,7 +105,10 @@ enum {
     MIGNN_DIAG_NO_EXT = 4096,   /* f16x3 GCN layer: skip the out-of-tile gathers */
     MIGNN_DIAG_NO_LOCAL = 8192,  /* f16x3 GCN layer: skip the in-tile (LDS) pass */
     MIGNN_DIAG_NO_TABLES = 16384, /* f16x3 GCN layer: skip the lookup-table build */
-    MIGNN_DIAG_PLAIN_STORE = 32768 /* f16x3 GCN layer: plain (not non-temporal) row stores */
+    MIGNN_DIAG_PLAIN_STORE = 32768, /* f16x3 GCN layer: plain (not non-temporal) row stores */
+    /* f16x3 GCN layer tile schedule: each XCD walks a contiguous range of tiles
+     * (for CSRs in a locality order, mignn_locality_order) */
+    MIGNN_SCHED_XCD_CHUNKS = 65536
 };
 int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
                  const float* a2, int64_t lda2, int k2,

@@ -31,6 +31,20 @@ if os.environ.get("KB_PERM"):
     pos = torch.empty_like(ids)
     pos[torch.argsort(key)] = ids
     ei = pos[ei]
+if os.environ.get("KB_PANEL"):
+    # 4x4x4-cell tiles; panels of PxP tile columns swept along k, tiles of a
+    # panel's k-level consecutive (locality experiment)
+    pp = int(os.environ["KB_PANEL"])
+    ids = torch.arange(n, device=dev)
+    i, j, k = ids % nx, (ids // nx) % ny, ids // (nx * ny)
+    ti, tj, tk = i // 4, j // 4, k // 4
+    ntk = (nz + 3) // 4
+    npi = ((nx + 3) // 4 + pp - 1) // pp
+    key = (((((tj // pp) * npi + ti // pp) * ntk + tk) * pp + tj % pp) * pp + ti % pp) * 64 \
+        + (k % 4) * 16 + (j % 4) * 4 + i % 4
+    pos = torch.empty_like(ids)
+    pos[torch.argsort(key, stable=True)] = ids
+    ei = pos[ei]
 if os.environ.get("KB_MORTON"):
     # relabel nodes in Morton (Z-curve) order of their grid cell (locality experiment)
     ids = torch.arange(n, device=dev)
@@ -152,7 +166,7 @@ def diag(mode_blocks):
 
 
 cases = {
-    "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_no_produce": (gcn16, 15 | 256),
+    "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_chunks": (gcn16, 15 | 65536), "gcn16_no_produce": (gcn16, 15 | 256),
     "gcn16_no_mfma": (gcn16, 15 | 512), "gcn16_no_ext": (gcn16, 15 | 4096),
     "gcn16_no_tables_ext": (gcn16, 15 | 4096 | 16384),
     "gcn16_plain": (gcn16, 15 | 32768), "gcn16_no_produce_plain": (gcn16, 15 | 256 | 32768),
