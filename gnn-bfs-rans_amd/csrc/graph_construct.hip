@@ -20,6 +20,9 @@
 
 #include "common.hpp"
 
+// numpy rounds every multiply and add separately: no FMA contraction here
+#pragma clang fp contract(off)
+
 namespace mignn {
 namespace {
 
@@ -146,15 +149,15 @@ __device__ __forceinline__ void edge_attr(const double* cc, int32_t s, int32_t d
     }
     const double* ps = cc + 3 * (int64_t)inv[s];
     const double* pd = cc + 3 * (int64_t)inv[d];
-    const double dx = __dsub_rn(pd[0], ps[0]), dy = __dsub_rn(pd[1], ps[1]),
-                 dz = __dsub_rn(pd[2], ps[2]);
-    const double sq = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
-    const double dist = __dsqrt_rn(sq);
+    const double dx = (pd[0] - ps[0]), dy = (pd[1] - ps[1]),
+                 dz = (pd[2] - ps[2]);
+    const double sq = (((dx * dx) + (dy * dy)) + (dz * dz));
+    const double dist = sqrt(sq);
     double ux = dx, uy = dy, uz = dz;
     if (dist > 0.0) {
-        ux = __ddiv_rn(dx, dist);
-        uy = __ddiv_rn(dy, dist);
-        uz = __ddiv_rn(dz, dist);
+        ux = (dx / dist);
+        uy = (dy / dist);
+        uz = (dz / dist);
     }
     out[0] = static_cast<float>(ux);
     out[1] = static_cast<float>(uy);
@@ -224,14 +227,14 @@ __global__ void edge_attr_kernel(const int64_t* __restrict__ ei, int64_t E, int6
         }
         const double* ps = cc + 3 * s;
         const double* pd = cc + 3 * d;
-        const double dx = __dsub_rn(pd[0], ps[0]), dy = __dsub_rn(pd[1], ps[1]),
-                     dz = __dsub_rn(pd[2], ps[2]);
-        const double dist = __dsqrt_rn(
-            __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)));
+        const double dx = (pd[0] - ps[0]), dy = (pd[1] - ps[1]),
+                     dz = (pd[2] - ps[2]);
+        const double dist = sqrt(
+            (((dx * dx) + (dy * dy)) + (dz * dz)));
         const double r = dist > 0.0 ? dist : 1.0;
-        o[0] = static_cast<float>(dist > 0.0 ? __ddiv_rn(dx, r) : dx);
-        o[1] = static_cast<float>(dist > 0.0 ? __ddiv_rn(dy, r) : dy);
-        o[2] = static_cast<float>(dist > 0.0 ? __ddiv_rn(dz, r) : dz);
+        o[0] = static_cast<float>(dist > 0.0 ? (dx / r) : dx);
+        o[1] = static_cast<float>(dist > 0.0 ? (dy / r) : dy);
+        o[2] = static_cast<float>(dist > 0.0 ? (dz / r) : dz);
         o[3] = static_cast<float>(dist);
     }
 }

@@ -62,6 +62,12 @@ SIGNATURES = {
                                       c_int64, _P, _P, _P, c_int64, _P, c_size_t, _P]),
     "mignn_edge_attributes": (c_int, [_P, c_int64, c_int64, _P, _P, _P]),
     "mignn_boundary_mask": (c_int, [_P, c_int64, c_int64, c_int64, c_int64, _P, _P]),
+    "mignn_field_affine": (c_int, [_P, c_int, c_int64, c_int64, c_int, _P, _P, c_int, c_int, _P, _P,
+                                   c_int64, _P]),
+    "mignn_field_moments": (c_int, [_P, c_int, c_int64, c_int64, c_int, _P, _P, _P]),
+    "mignn_write_openfoam_field": (c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                           ctypes.c_char_p, ctypes.c_char_p, _P, c_int64, c_int,
+                                           c_int64]),
     "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),

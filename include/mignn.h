@@ -268,6 +268,30 @@ int mignn_boundary_mask(const int64_t* owner, int64_t n_faces, int64_t start_fac
                         int64_t n_boundary_faces, int64_t n_cells, uint8_t* mask, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Output side (reference normalization.py, inference.py).
+ * mignn_field_affine: per column c < ncol (<= 30) of x (float32, or float64
+ * when x_is_f64), inverse = 1: y = x * std[c] + mean[c]
+ * (FieldNormalizer.inverse_transform, normalization.py:110-133); inverse = 0:
+ * y = (x - mean[c]) / std[c] (transform, :86-108).  float64 arithmetic
+ * without FMA into y (float64, stride ldy) -- NumPy >= 2 promotion; columns in
+ * legacy_mask use float32 arithmetic into y32 instead (numpy < 2 value-based
+ * casting of float64 scalar scalers on float32 fields).
+ * mignn_field_moments: per column mean and population std (fit, :18-84),
+ * float64, two passes.
+ * mignn_write_openfoam_field: HOST function; writes one field file exactly as
+ * save_fields_openfoam_format (inference.py:90-178) does: "%.6e" values, NaN
+ * as "nan"; values are host float64 [n, ncomp] (ncomp 1 or 3), row stride ld.
+ * ------------------------------------------------------------------------ */
+int mignn_field_affine(const void* x, int x_is_f64, int64_t ldx, int64_t n, int ncol,
+                       const double* mean, const double* std_, int inverse, int legacy_mask,
+                       double* y, float* y32, int64_t ldy, void* stream);
+int mignn_field_moments(const void* x, int x_is_f64, int64_t ldx, int64_t n, int ncol,
+                        double* mean, double* std_, void* stream);
+int mignn_write_openfoam_field(const char* path, const char* field_class, const char* object,
+                               const char* location, const char* dimensions,
+                               const double* values, int64_t n, int ncomp, int64_t ld);
+
+/* ------------------------------------------------------------------------
  * Multi-GPU halo helpers and synthetic inputs.
  * ------------------------------------------------------------------------ */
 /* dst[r, :] = src[idx[r], :] for r < n (halo pack / unpack by index list) */
