@@ -68,6 +68,13 @@ SIGNATURES = {
     "mignn_write_openfoam_field": (c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                            ctypes.c_char_p, ctypes.c_char_p, _P, c_int64, c_int,
                                            c_int64]),
+    "mignn_foam_parse_labels": (c_int, [_P, c_int64, c_int, _P, c_int64, _P]),
+    "mignn_foam_parse_points": (c_int, [_P, c_int64, _P, c_int64, _P]),
+    "mignn_foam_parse_faces": (c_int, [_P, c_int64, _P, c_int64, _P, c_int64, _P, _P]),
+    "mignn_foam_parse_scalar_field": (c_int, [_P, c_int64, _P, c_int64, _P]),
+    "mignn_foam_parse_vector_field": (c_int, [_P, c_int64, _P, c_int64, _P]),
+    "mignn_foam_cell_centers": (c_int, [_P, c_int64, _P, c_int64, _P, c_int64, _P, _P, c_int64,
+                                        c_int64, _P]),
     "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),

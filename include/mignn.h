@@ -292,6 +292,34 @@ int mignn_write_openfoam_field(const char* path, const char* field_class, const 
                                const double* values, int64_t n, int ncomp, int64_t ld);
 
 /* ------------------------------------------------------------------------
+ * OpenFOAM ASCII reader (reference openfoam_loader.py), HOST
+ * functions with the reference's exact parsing rules and quirks (see
+ * csrc/foam_reader.hip).  Each parser takes the file's bytes (buf, len) and
+ * host output arrays of capacity cap (rows for points / vector fields);
+ * counts come back through the n_* pointers.
+ * ------------------------------------------------------------------------ */
+/* labelList (owner / neighbour): compat 0 = the reference's read_array
+ * (openfoam_loader.py:53-65) including the header-digit quirk; compat 1 = the
+ * list as OpenFOAM defines it (count after the FoamFile header). */
+int mignn_foam_parse_labels(const char* buf, int64_t len, int compat, int64_t* out, int64_t cap,
+                            int64_t* n_out);
+int mignn_foam_parse_points(const char* buf, int64_t len, double* out, int64_t cap_rows,
+                            int64_t* n_rows);
+int mignn_foam_parse_faces(const char* buf, int64_t len, int64_t* offsets, int64_t cap_faces,
+                           int64_t* verts, int64_t cap_verts, int64_t* n_faces, int64_t* n_verts);
+int mignn_foam_parse_scalar_field(const char* buf, int64_t len, double* out, int64_t cap,
+                                  int64_t* n_out);
+int mignn_foam_parse_vector_field(const char* buf, int64_t len, double* out, int64_t cap_rows,
+                                  int64_t* n_rows);
+/* get_cell_centers (openfoam_loader.py:191-227): per cell the mean of the
+ * unique vertices of its owner faces then neighbour faces, summed in CPython's
+ * set iteration order (emulated) so the float64 results match bit for bit. */
+int mignn_foam_cell_centers(const double* points, int64_t n_points, const int64_t* owner,
+                            int64_t n_owner, const int64_t* neighbour, int64_t n_neighbour,
+                            const int64_t* face_off, const int64_t* face_verts, int64_t n_faces,
+                            int64_t n_cells, double* centers);
+
+/* ------------------------------------------------------------------------
  * Multi-GPU halo helpers and synthetic inputs.
  * ------------------------------------------------------------------------ */
 /* dst[r, :] = src[idx[r], :] for r < n (halo pack / unpack by index list) */
