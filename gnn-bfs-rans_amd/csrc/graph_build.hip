@@ -38,7 +38,7 @@ namespace {
 constexpr int kBlock = 256;
 
 __global__ void csr_keys_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t N, int mode,
-                                const int32_t* __restrict__ relabel,
+                                int transpose, const int32_t* __restrict__ relabel,
                                 uint32_t* __restrict__ keys, int32_t* __restrict__ vals,
                                 unsigned long long* __restrict__ counters) {
     __shared__ unsigned int s_kept, s_bad;
@@ -47,8 +47,9 @@ __global__ void csr_keys_kernel(const int64_t* __restrict__ ei, int64_t E, int64
     unsigned kept = 0, bad = 0;
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
          e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t s = ei[e];
-        const int64_t d = ei[E + e];
+        // transposed: rows keyed by the source (backward of the aggregation)
+        const int64_t s = ei[transpose ? E + e : e];
+        const int64_t d = ei[transpose ? e : E + e];
         const bool valid = (s >= 0) & (s < N) & (d >= 0) & (d < N);
         bool keep = valid;
         if (mode == MIGNN_CSR_ONE_SELF_LOOP && s == d) keep = false;
@@ -276,6 +277,8 @@ extern "C" int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t E, i
     MIGNN_REQUIRE(N >= 0 && E >= 0, "csr_build: negative sizes (E=%lld N=%lld)", (long long)E,
                   (long long)N);
     MIGNN_REQUIRE(E + N < (int64_t(1) << 31) - 1, "csr_build: E+N exceeds int32 CSR range");
+    const int transpose = (mode & MIGNN_CSR_TRANSPOSE) ? 1 : 0;
+    mode &= ~MIGNN_CSR_TRANSPOSE;
     MIGNN_REQUIRE(mode == MIGNN_CSR_VERBATIM || mode == MIGNN_CSR_ONE_SELF_LOOP,
                   "csr_build: bad mode %d", mode);
     MIGNN_REQUIRE(row_ptr && col && scratch && (E == 0 || edge_index),
@@ -298,7 +301,8 @@ extern "C" int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t E, i
     MIGNN_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), st));
     if (E > 0) {
         hipLaunchKernelGGL(csr_keys_kernel, dim3(grid_for(E, kBlock, 4096)), dim3(kBlock), 0, st,
-                           edge_index, E, N, mode, relabel, keys_in, vals_in, counters);
+                           edge_index, E, N, mode, transpose, relabel, keys_in, vals_in,
+                           counters);
         if ((rc = launch_status("csr_keys_kernel"))) return rc;
         const unsigned bits = key_bits(N);
         size_t temp = L.temp_bytes;

@@ -19,7 +19,7 @@ LIB_NAME = "libmignn.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 EPI_BIAS, EPI_RESIDUAL, EPI_AFFINE, EPI_RELU = 1, 2, 4, 8
-CSR_VERBATIM, CSR_ONE_SELF_LOOP = 0, 1
+CSR_VERBATIM, CSR_ONE_SELF_LOOP, CSR_TRANSPOSE = 0, 1, 4
 
 _P = c_void_p
 # name -> (restype, argtypes); mirrors include/mignn.h
@@ -75,6 +75,22 @@ SIGNATURES = {
     "mignn_foam_parse_vector_field": (c_int, [_P, c_int64, _P, c_int64, _P]),
     "mignn_foam_cell_centers": (c_int, [_P, c_int64, _P, c_int64, _P, c_int64, _P, _P, c_int64,
                                         c_int64, _P]),
+    "mignn_train_scratch_bytes": (c_size_t, [c_int64, c_int]),
+    "mignn_gemm": (c_int, [_P, c_int64, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int64,
+                           _P, c_int64, _P, c_int64, _P, c_size_t, _P]),
+    "mignn_col_sums": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, c_size_t, _P]),
+    "mignn_bn_train_stats": (c_int, [_P, c_int64, c_int64, c_int, c_float, c_float, _P, _P, _P,
+                                     _P, _P, _P, c_size_t, _P]),
+    "mignn_bn_act_forward": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, c_int, c_float,
+                                     ctypes.c_uint64, _P, c_int64, _P]),
+    "mignn_bn_act_backward": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, _P, _P, _P, _P,
+                                      c_int, c_float, ctypes.c_uint64, _P, c_int64, _P, _P, _P,
+                                      c_size_t, _P]),
+    "mignn_wmse_loss": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, _P, c_float, c_int, _P,
+                                _P, _P, c_size_t, _P]),
+    "mignn_wmse_loss_backward": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, _P, c_float,
+                                         c_int, _P, _P, _P, c_int64, _P]),
+    "mignn_dropout_mask": (c_int, [c_int64, c_int, c_float, ctypes.c_uint64, _P, _P]),
     "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),

@@ -46,7 +46,9 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from ._lib import CSR_ONE_SELF_LOOP, CSR_VERBATIM, EPI_AFFINE, EPI_BIAS, EPI_RELU, EPI_RESIDUAL
+from . import train_ops as T
+from ._lib import (CSR_ONE_SELF_LOOP, CSR_TRANSPOSE, CSR_VERBATIM, EPI_AFFINE, EPI_BIAS, EPI_RELU,
+                   EPI_RESIDUAL)
 
 HEADS = 4  # gnn_model.py:67, :79
 
@@ -363,6 +365,8 @@ class FlowGNN(nn.Module):
         if edge_attr is not None and E > 0 and edge_attr.shape[0] != E:
             raise ValueError(f"edge_attr must have {E} entries, got {edge_attr.shape[0]}")
         H = self.hidden_dim
+        if self.training:
+            return self._forward_train(x, edge_index, edge_attr)
         out = torch.empty((num_nodes, self.output_dim), dtype=torch.float32, device=x.device)
         if num_nodes == 0:
             return out
@@ -401,11 +405,11 @@ class FlowGNN(nn.Module):
 
     # ------------------------------------------------------------- internals
     def _check_runtime(self, x, edge_index):
-        if self.training:
+        if self.training and self.layer_type != "GCN":
             raise NotImplementedError(
-                "mignn FlowGNN implements the eval-mode forward (inference.py / visualize.py / "
-                "validate paths); call .eval().  Training-mode BN/dropout and backward are "
-                "SURVEY.md §8f-3 (next).")
+                f"mignn FlowGNN trains the GCN layer type (train.py's default); model.train() "
+                f"with layer_type={self.layer_type!r} is not implemented -- call .eval() for "
+                "the forward.")
         if x.device.type != "cuda" or edge_index.device.type != "cuda":
             raise RuntimeError(
                 "mignn FlowGNN runs on ROCm devices only (no CPU path): move the model and the "
@@ -419,6 +423,40 @@ class FlowGNN(nn.Module):
             raise RuntimeError("mignn FlowGNN requires hidden_dim % 8 == 0")
         if self.precision not in ("f32", "f16x3"):
             raise ValueError(f"precision must be 'f32' or 'f16x3', got {self.precision!r}")
+
+    def _forward_train(self, x, edge_index, edge_attr):
+        """model.train() forward (gnn_model.py:159-195) as autograd ops over HIP
+        kernels (mignn.train_ops): batch-statistics BN with running-stat updates,
+        dropout, and a backward for every parameter."""
+        num_nodes = x.shape[0]
+        if num_nodes == 0:
+            raise ValueError("training forward on an empty graph")
+        xin = x.contiguous().float() if (x.dtype != torch.float32 or not x.is_contiguous()) else x
+        csr = self._csr.get(edge_index, num_nodes, CSR_ONE_SELF_LOOP)
+        csr_t = self._csr.get(edge_index, num_nodes, CSR_ONE_SELF_LOOP | CSR_TRANSPOSE)
+        h = T.linear(xin, self.input_proj.weight, self.input_proj.bias)
+        p = float(self.dropout.p)
+        for i, layer in enumerate(self.gnn_layers):
+            try:
+                z = T.gcn_residual(h, layer.lin.weight, layer.bias, csr, csr_t)
+            except RuntimeError as e:
+                raise self._layer_error(i, e, num_nodes, edge_index, h, edge_attr) from e
+            bn = self.batch_norms[i].module if self.use_batch_norm else None
+            h = T.bn_relu_dropout(z, bn, p)
+        mods = list(self.output_proj)
+        k = 0
+        while k < len(mods):
+            m = mods[k]
+            if isinstance(m, nn.Linear):
+                relu = k + 1 < len(mods) and isinstance(mods[k + 1], nn.ReLU)
+                h = T.linear(h, m.weight, m.bias, relu=relu)
+                k += 2 if relu else 1
+            elif isinstance(m, nn.Dropout):
+                h = T.dropout(h, float(m.p))
+                k += 1
+            else:
+                raise NotImplementedError(f"output_proj module {type(m).__name__}")
+        return h
 
     def _layer_error(self, i, e, num_nodes, edge_index, x, edge_attr):
         E = edge_index.shape[1]

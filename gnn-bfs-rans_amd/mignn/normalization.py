@@ -11,6 +11,9 @@ on the native kernels / host writer of csrc/fields.hip.
   reference under NumPy >= 2.  `numpy_legacy=True` reproduces numpy < 2
   value-based casting (scalar scalers keep float32 fields float32).
 * The writer produces byte-identical files ("%.6e"), natively.
+* `WeightedMSELoss` (normalization.py:136-250), the training criterion of
+  train.py:352-363, with its forward and backward on the device
+  (mignn_wmse_loss).
 """
 
 from __future__ import annotations
@@ -21,8 +24,10 @@ from typing import Dict
 
 import numpy as np
 import torch
+import torch.nn as nn
 
 from . import _lib
+from . import train_ops as _T
 
 _SCALAR_FIELDS = {
     "p": ("[0 2 -2 0 0 0 0]", "volScalarField"),
@@ -166,3 +171,36 @@ def save_fields_openfoam_format(fields: Dict, output_dir: str, time_dir: str = "
     for name, (dims, cls) in _SCALAR_FIELDS.items():
         if name in fields:
             write(name, cls, dims, fields[name], 1)
+
+
+class WeightedMSELoss(nn.Module):
+    """normalization.py:136-250: per-field MSE, weighted, plus the pressure
+    reference term w_p * prw * (mean(p_pred) - mean(p_target))^2 (fieldwise),
+    or the element-weighted mean (use_fieldwise=False).  Device-only."""
+
+    def __init__(self, field_weights: Dict[str, float] = None, use_fieldwise: bool = True,
+                 pressure_ref_weight: float = 0.1):
+        super().__init__()
+        if field_weights is None:
+            field_weights = {"U": 1.0, "p": 3.0, "k": 0.5, "epsilon": 0.5, "nut": 0.5}
+        self.field_weights = field_weights
+        self.use_fieldwise = use_fieldwise
+        self.pressure_ref_weight = pressure_ref_weight
+        g = field_weights.get
+        self.weights = torch.tensor([g("U", 1.0), g("U", 1.0), g("U", 1.0), g("p", 1.0),
+                                     g("k", 0.5), g("epsilon", 0.5), g("nut", 0.5)],
+                                    dtype=torch.float32)
+
+    def forward(self, pred: torch.Tensor, target: torch.Tensor,
+                pressure_ref_weight: float = 0.1) -> torch.Tensor:
+        if pred.device.type != "cuda" or target.device.type != "cuda":
+            raise RuntimeError("mignn WeightedMSELoss runs on ROCm devices only (no CPU path)")
+        if pred.dim() != 2 or target.shape != pred.shape:
+            raise RuntimeError(f"pred {tuple(pred.shape)} / target {tuple(target.shape)} mismatch")
+        if self.use_fieldwise:   # read at call time, like the reference (:199-231)
+            g = self.field_weights.get
+            w = [g("U", 1.0)] * 3 + [g("p", 1.0), g("k", 0.5), g("epsilon", 0.5), g("nut", 0.5)]
+        else:
+            w = self.weights.tolist()
+        return _T.weighted_mse(pred, target, w, pressure_ref_weight if self.use_fieldwise else 0.0,
+                               self.use_fieldwise)

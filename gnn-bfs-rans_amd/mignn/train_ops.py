@@ -1,0 +1,303 @@
+"""Autograd ops of the training path over libmignn.so.
+
+Each op is a `torch.autograd.Function` whose forward and backward are HIP
+kernels (csrc/train.hip, csrc/aggregate.hip, csrc/linear.hip); PyTorch only
+records the graph and owns the memory.  They compose `FlowGNN`'s
+model.train() forward (gnn_model.py:159-195) so that train.py's
+`loss.backward()` (train.py:177) produces every parameter gradient:
+
+  linear            nn.Linear (input_proj :55, output_proj :90-100), optional
+                    fused ReLU
+  dropout           nn.Dropout / F.dropout (counter-hash mask, regenerated in
+                    the backward)
+  gcn_residual      x + GCNConv(x)  (:166, :184) -- aggregation first, then
+                    the transform, bias and residual in one MFMA epilogue;
+                    backward through the reversed-edge CSR
+  bn_relu_dropout   BatchNorm (batch statistics, running-stat update) + ReLU +
+                    dropout (:188-191) in one elementwise pass
+  WeightedMSELoss   normalization.py:136-250 (forward and backward on device)
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+
+P = _lib.ptr
+
+
+def _st(t: torch.Tensor) -> int:
+    return _lib.stream(t.device)
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    return t if (t.is_contiguous() and t.dtype == torch.float32) else t.float().contiguous()
+
+
+def _red_scratch(n: int, h: int, dev) -> torch.Tensor:
+    nb = _lib.lib().mignn_train_scratch_bytes(n, h)
+    return torch.empty(nb, dtype=torch.uint8, device=dev)
+
+
+def gemm(a, sai, sak, b, sbk, sbj, m, n, k, out, ldc=None, residual=None, split=False):
+    """out[i, j] = sum_k A(i, k) B(k, j) (+ residual) on the f32 MFMA (mignn_gemm)."""
+    ldc = out.stride(0) if ldc is None else ldc
+    scratch, nbytes = None, 0
+    if split:   # room for mignn_gemm's split partials (<= ~1024 tiles in flight)
+        tiles = -(-m // 64) * -(-n // 64)
+        nbytes = (1024 // tiles + 1) * m * n * 4
+        scratch = torch.empty(nbytes, dtype=torch.uint8, device=out.device)
+    _lib.check(_lib.lib().mignn_gemm(
+        P(a), sai, sak, P(b), sbk, sbj, m, n, k, P(residual),
+        0 if residual is None else residual.stride(0), P(out), ldc, P(scratch), nbytes,
+        _st(out)), "mignn_gemm")
+    return out
+
+
+def weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW[o, i] = sum_m dy[m, o] x[m, i]  (nn.Linear weight gradient)."""
+    n, o = dy.shape
+    i = x.shape[1]
+    dw = torch.empty((o, i), dtype=torch.float32, device=dy.device)
+    return gemm(dy, 1, dy.stride(0), x, x.stride(0), 1, o, i, n, dw, split=True)
+
+
+def data_grad(dy: torch.Tensor, w: torch.Tensor, residual=None) -> torch.Tensor:
+    """dx[m, i] = sum_o dy[m, o] w[o, i] (+ residual)  (nn.Linear input gradient)."""
+    n, o = dy.shape
+    i = w.shape[1]
+    dx = torch.empty((n, i), dtype=torch.float32, device=dy.device)
+    return gemm(dy, dy.stride(0), 1, w, w.stride(0), 1, n, i, o, dx, residual=residual)
+
+
+def col_sums(x: torch.Tensor) -> torch.Tensor:
+    n, h = x.shape
+    out = torch.empty(h, dtype=torch.float32, device=x.device)
+    s = _red_scratch(n, h, x.device)
+    _lib.check(_lib.lib().mignn_col_sums(P(x), x.stride(0), n, h, P(out), P(s), s.numel(),
+                                         _st(x)), "mignn_col_sums")
+    return out
+
+
+def draw_seed() -> int:
+    """A dropout seed from torch's (CPU) default generator, so torch.manual_seed
+    makes training runs repeatable."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+# ---------------------------------------------------------------------------
+
+class _Linear(Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu: bool):
+        from .gnn_model import linear as _mfma_linear
+        x = _c(x)
+        n, k = x.shape
+        if k % 4 == 0 and x.stride(0) % 4 == 0:
+            y = _mfma_linear(x, w, b, relu=relu)
+        else:   # thin inputs (input_proj, 3 coordinates): the VALU projection
+            if relu:
+                raise NotImplementedError("fused ReLU on a thin Linear")
+            y = torch.empty((n, w.shape[0]), dtype=torch.float32, device=x.device)
+            _lib.check(_lib.lib().mignn_input_proj(
+                P(x), n, k, P(w), P(b), w.shape[0], P(y), y.stride(0), _st(x)),
+                "mignn_input_proj")
+        ctx.relu = relu
+        ctx.has_bias = b is not None
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        g = _c(gy)
+        if ctx.relu:   # through the fused ReLU: g * (y > 0)
+            g = _act_backward(g, y, relu=True, p=0.0, seed=0)
+        dx = data_grad(g, w) if ctx.needs_input_grad[0] else None
+        dw = weight_grad(g, x) if ctx.needs_input_grad[1] else None
+        db = col_sums(g) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        return dx, dw, db, None
+
+
+def _act_backward(dout, y, relu: bool, p: float, seed: int) -> torch.Tensor:
+    """d/dy of drop_p(relu?(y)) given the forward's y (no BN)."""
+    n, h = dout.shape
+    dz = torch.empty_like(dout)
+    _lib.check(_lib.lib().mignn_bn_act_backward(
+        P(dout), dout.stride(0), P(y), y.stride(0), n, h, None, None, None, None, int(relu),
+        float(p), seed, P(dz), dz.stride(0), None, None, None, 0, _st(dout)),
+        "mignn_bn_act_backward")
+    return dz
+
+
+class _Dropout(Function):
+    @staticmethod
+    def forward(ctx, x, p: float, seed: int):
+        x = _c(x)
+        n, h = x.shape
+        y = torch.empty_like(x)
+        _lib.check(_lib.lib().mignn_bn_act_forward(
+            P(x), x.stride(0), n, h, None, None, None, None, 0, float(p), seed, P(y),
+            y.stride(0), _st(x)), "mignn_bn_act_forward")
+        ctx.p, ctx.seed = p, seed
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        return _act_backward(_c(gy), x, relu=False, p=ctx.p, seed=ctx.seed), None, None
+
+
+class _GCNResidual(Function):
+    """z = x + GCNConv(x) = x + (A x) W^T + b, A = PyG gcn_norm adjacency."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, csr, csr_t):
+        from .gnn_model import linear as _mfma_linear
+        x = _c(x)
+        n, h = x.shape
+        agg = torch.empty_like(x)
+        _lib.check(_lib.lib().mignn_gcn_aggregate(
+            P(csr.row_ptr), P(csr.col), P(csr.dinv), P(x), x.stride(0), 0, n, h, P(agg),
+            agg.stride(0), _st(x)), "mignn_gcn_aggregate")
+        z = _mfma_linear(agg, w, b, residual=x)
+        ctx.csr, ctx.csr_t = csr, csr_t
+        ctx.save_for_backward(agg, w)
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        agg, w = ctx.saved_tensors
+        g = _c(gz)
+        n, h = g.shape
+        db = col_sums(g)
+        dw = weight_grad(g, agg)
+        # dx = g + (A^T g) W: A^T = the aggregation over the reversed edges
+        # with the same symmetric weights dinv_i * dinv_j
+        t = torch.empty_like(g)
+        csr, csr_t = ctx.csr, ctx.csr_t
+        _lib.check(_lib.lib().mignn_gcn_aggregate(
+            P(csr_t.row_ptr), P(csr_t.col), P(csr.dinv), P(g), g.stride(0), 0, n, h, P(t),
+            t.stride(0), _st(g)), "mignn_gcn_aggregate(transpose)")
+        dx = data_grad(t, w, residual=g)
+        return dx, dw, db, None, None
+
+
+class _BNReluDropout(Function):
+    """dropout(relu(BatchNorm_train(z))); bn_mod = the BatchNorm1d (running
+    stats updated in place, as torch does in train mode); bn_mod None: no BN."""
+
+    @staticmethod
+    def forward(ctx, z, gamma, beta, bn_mod, p: float, seed: int):
+        z = _c(z)
+        n, h = z.shape
+        dev = z.device
+        mean = invstd = None
+        if bn_mod is not None:
+            mean = torch.empty(h, dtype=torch.float32, device=dev)
+            invstd = torch.empty_like(mean)
+            s = _red_scratch(n, h, dev)
+            track = bn_mod.track_running_stats and bn_mod.running_mean is not None
+            mom = bn_mod.momentum if bn_mod.momentum is not None else 0.0
+            _lib.check(_lib.lib().mignn_bn_train_stats(
+                P(z), z.stride(0), n, h, float(bn_mod.eps), float(mom), P(mean), P(invstd),
+                P(bn_mod.running_mean) if track else None,
+                P(bn_mod.running_var) if track else None,
+                P(bn_mod.num_batches_tracked) if track else None, P(s), s.numel(), _st(z)),
+                "mignn_bn_train_stats")
+        y = torch.empty_like(z)
+        _lib.check(_lib.lib().mignn_bn_act_forward(
+            P(z), z.stride(0), n, h, P(mean), P(invstd), P(gamma), P(beta), 1, float(p), seed,
+            P(y), y.stride(0), _st(z)), "mignn_bn_act_forward")
+        ctx.p, ctx.seed, ctx.bn = p, seed, bn_mod is not None
+        ctx.save_for_backward(z, mean, invstd, gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        z, mean, invstd, gamma, beta = ctx.saved_tensors
+        g = _c(gy)
+        n, h = g.shape
+        dz = torch.empty_like(g)
+        dgamma = dbeta = s = None
+        nbytes = 0
+        if ctx.bn:
+            dgamma = torch.empty(h, dtype=torch.float32, device=g.device)
+            dbeta = torch.empty_like(dgamma)
+            s = _red_scratch(n, h, g.device)
+            nbytes = s.numel()
+        _lib.check(_lib.lib().mignn_bn_act_backward(
+            P(g), g.stride(0), P(z), z.stride(0), n, h, P(mean), P(invstd), P(gamma), P(beta),
+            1, float(ctx.p), ctx.seed, P(dz), dz.stride(0), P(dgamma), P(dbeta), P(s), nbytes,
+            _st(g)), "mignn_bn_act_backward")
+        return dz, dgamma, dbeta, None, None, None
+
+
+class _WMSE(Function):
+    @staticmethod
+    def forward(ctx, pred, target, weights, prw: float, fieldwise: bool):
+        pred, target = _c(pred), _c(target)
+        n, ncol = pred.shape
+        dev = pred.device
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        stats = torch.empty(1, dtype=torch.float64, device=dev)
+        s = _red_scratch(n, ncol, dev)
+        w = _host_floats(weights)
+        _lib.check(_lib.lib().mignn_wmse_loss(
+            P(pred), pred.stride(0), P(target), target.stride(0), n, ncol, w, float(prw),
+            int(fieldwise), P(loss), P(stats), P(s), s.numel(), _st(pred)), "mignn_wmse_loss")
+        ctx.weights, ctx.prw, ctx.fieldwise = weights, prw, fieldwise
+        ctx.save_for_backward(pred, target, stats)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        pred, target, stats = ctx.saved_tensors
+        n, ncol = pred.shape
+        gl = _c(gl.reshape(()))
+        dpred = torch.empty_like(pred)
+        _lib.check(_lib.lib().mignn_wmse_loss_backward(
+            P(pred), pred.stride(0), P(target), target.stride(0), n, ncol,
+            _host_floats(ctx.weights), float(ctx.prw), int(ctx.fieldwise), P(stats), P(gl),
+            P(dpred), dpred.stride(0), _st(pred)), "mignn_wmse_loss_backward")
+        return dpred, None, None, None, None
+
+
+def _host_floats(vals):
+    """A host float[7] (ctypes arrays pass as pointers; alive for the call)."""
+    return (ctypes.c_float * 7)(*[float(v) for v in vals])
+
+
+# ---------------------------------------------------------------------------
+# public functional surface
+
+def linear(x, w, b=None, relu: bool = False):
+    return _Linear.apply(x, w, b, relu)
+
+
+def dropout(x, p: float, training: bool = True, seed: Optional[int] = None):
+    if not training or p <= 0.0:
+        return x
+    return _Dropout.apply(x, float(p), draw_seed() if seed is None else seed)
+
+
+def gcn_residual(x, w, b, csr, csr_t):
+    return _GCNResidual.apply(x, w, b, csr, csr_t)
+
+
+def bn_relu_dropout(z, bn_mod, p: float, seed: Optional[int] = None):
+    seed = draw_seed() if (seed is None and p > 0.0) else (seed or 0)
+    if bn_mod is None:
+        return _BNReluDropout.apply(z, None, None, None, float(p), seed)
+    return _BNReluDropout.apply(z, bn_mod.weight, bn_mod.bias, bn_mod, float(p), seed)
+
+
+def weighted_mse(pred, target, weights, pressure_ref_weight: float, fieldwise: bool):
+    return _WMSE.apply(pred, target, tuple(float(w) for w in weights),
+                       float(pressure_ref_weight), bool(fieldwise))

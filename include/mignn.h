@@ -55,7 +55,11 @@ const char* mignn_last_error(void);
  * NULL).  info (device int64[4], may be NULL) = {kept edges, invalid edges,
  * nnz, all-invalid fallback taken}.
  * ------------------------------------------------------------------------ */
-enum { MIGNN_CSR_VERBATIM = 0, MIGNN_CSR_ONE_SELF_LOOP = 1 };
+/* | MIGNN_CSR_TRANSPOSE: the CSR of the reversed edges (rows keyed by the
+ * source; same filtering and self-loop rules), i.e. the transpose of the
+ * aggregation -- the backward of a sum aggregation (training).
+ * dinv is then the source-side degree and unused by the backward. */
+enum { MIGNN_CSR_VERBATIM = 0, MIGNN_CSR_ONE_SELF_LOOP = 1, MIGNN_CSR_TRANSPOSE = 4 };
 
 size_t mignn_csr_scratch_bytes(int64_t num_edges, int64_t num_nodes);
 /* As mignn_csr_build, with every valid node id x of edge_index mapped to
@@ -318,6 +322,57 @@ int mignn_foam_cell_centers(const double* points, int64_t n_points, const int64_
                             int64_t n_owner, const int64_t* neighbour, int64_t n_neighbour,
                             const int64_t* face_off, const int64_t* face_verts, int64_t n_faces,
                             int64_t n_cells, double* centers);
+
+/* ------------------------------------------------------------------------
+ * Training (csrc/train.hip): model.train() forward pieces
+ * and the backward of FlowGNN(GCN) + WeightedMSELoss (train.py:158-196).
+ * Scratch: mignn_train_scratch_bytes(n, h) bytes for the column reductions;
+ * mignn_gemm takes optional scratch for its split reduction partials.
+ * ------------------------------------------------------------------------ */
+size_t mignn_train_scratch_bytes(int64_t n, int h);
+/* C[i, j] = sum_k A(i, k) B(k, j) (+ R[i, j]), A(i, k) = a[i*sai + k*sak],
+ * B(k, j) = b[k*sbk + j*sbj] -- f32 MFMA, exact products.  dX = dY.W of a
+ * Linear (nn.Linear backward, gnn_model.py:55, 90-100; GCNConv lin :63) and
+ * dW = dY^T.X (the reduction over the nodes split over scratch partials and
+ * summed in a fixed order when scratch is given and R is NULL). */
+int mignn_gemm(const float* a, int64_t sai, int64_t sak, const float* b, int64_t sbk, int64_t sbj,
+               int64_t m, int64_t n, int64_t k, const float* r, int64_t ldr, float* c,
+               int64_t ldc, void* scratch, size_t scratch_bytes, void* stream);
+/* sums[c] = sum_m x[m, c] (bias gradients), double accumulation, deterministic */
+int mignn_col_sums(const float* x, int64_t ldx, int64_t n, int h, float* sums, void* scratch,
+                   size_t scratch_bytes, void* stream);
+/* BatchNorm1d training statistics (gnn_model.py:87, 188 in model.train()):
+ * batch mean / 1/sqrt(biased var + eps); running_mean/var (may be NULL)
+ * updated with momentum and the unbiased variance; num_batches_tracked += 1. */
+int mignn_bn_train_stats(const float* z, int64_t ldz, int64_t n, int h, float eps, float momentum,
+                         float* mean, float* invstd, float* running_mean, float* running_var,
+                         int64_t* num_batches_tracked, void* scratch, size_t scratch_bytes,
+                         void* stream);
+/* y = dropout_p(relu(BN(z))) (gnn_model.py:188-191); gamma NULL: no BN.
+ * Dropout mask = counter hash of (seed, m*h + c), regenerated by the backward. */
+int mignn_bn_act_forward(const float* z, int64_t ldz, int64_t n, int h, const float* mean,
+                         const float* invstd, const float* gamma, const float* beta, int relu,
+                         float p, uint64_t seed, float* y, int64_t ldy, void* stream);
+/* dz (and dgamma, dbeta) from dy of mignn_bn_act_forward's output */
+int mignn_bn_act_backward(const float* dout, int64_t ldd, const float* z, int64_t ldz, int64_t n,
+                          int h, const float* mean, const float* invstd, const float* gamma,
+                          const float* beta, int relu, float p, uint64_t seed, float* dz,
+                          int64_t lddz, float* dgamma, float* dbeta, void* scratch,
+                          size_t scratch_bytes, void* stream);
+/* WeightedMSELoss.forward (normalization.py:176-250): weights[7] = per-column
+ * field weights (U, U, U, p, k, epsilon, nut); fieldwise = use_fieldwise;
+ * prw = pressure_ref_weight; weights is a HOST array.  loss: device float scalar; stats: device
+ * double[1] kept for the backward. */
+int mignn_wmse_loss(const float* pred, int64_t ldp, const float* tgt, int64_t ldt, int64_t n,
+                    int ncol, const float* weights, float prw, int fieldwise, float* loss,
+                    double* stats, void* scratch, size_t scratch_bytes, void* stream);
+/* dpred = grad_loss (device scalar) * d loss / d pred */
+int mignn_wmse_loss_backward(const float* pred, int64_t ldp, const float* tgt, int64_t ldt,
+                             int64_t n, int ncol, const float* weights, float prw, int fieldwise,
+                             const double* stats, const float* grad_loss, float* dpred,
+                             int64_t ldd, void* stream);
+/* the dropout keep-scale mask of (p, seed) as an [n, h] array (tests) */
+int mignn_dropout_mask(int64_t n, int h, float p, uint64_t seed, float* mask, void* stream);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU halo helpers and synthetic inputs.

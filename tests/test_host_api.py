@@ -72,8 +72,22 @@ def test_errors_mirror_reference():
     # no CPU path: the product refuses CPU tensors loudly
     with pytest.raises(RuntimeError, match="ROCm devices only"):
         m(torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
-    with pytest.raises(NotImplementedError):
+    # model.train(): GCN trains on the device (CPU tensors refused the same
+    # way); the other layer types are eval-only
+    with pytest.raises(RuntimeError, match="ROCm devices only"):
         m.train()(torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
+    with pytest.raises(NotImplementedError):
+        FlowGNN(hidden_dim=16, num_layers=1, layer_type="GIN").train()(
+            torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
+
+
+def test_weighted_mse_loss_host_side():
+    from mignn.normalization import WeightedMSELoss
+    crit = WeightedMSELoss()
+    assert crit.field_weights["p"] == 3.0 and crit.use_fieldwise and crit.pressure_ref_weight == 0.1
+    assert crit.weights.tolist() == [1.0, 1.0, 1.0, 3.0, 0.5, 0.5, 0.5]
+    with pytest.raises(RuntimeError, match="ROCm devices only"):
+        crit(torch.zeros(4, 7), torch.zeros(4, 7))
 
 
 def test_predict_fields_slices():
