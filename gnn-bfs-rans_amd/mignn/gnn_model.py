@@ -405,9 +405,10 @@ class FlowGNN(nn.Module):
 
     # ------------------------------------------------------------- internals
     def _check_runtime(self, x, edge_index):
-        if self.training and self.layer_type != "GCN":
+        if self.training and self.layer_type not in ("GCN", "GIN"):
             raise NotImplementedError(
-                f"mignn FlowGNN trains the GCN layer type (train.py's default); model.train() "
+                f"mignn FlowGNN trains the GCN and GIN layer types (GCN is train.py's default); "
+                f"model.train() "
                 f"with layer_type={self.layer_type!r} is not implemented -- call .eval() for "
                 "the forward.")
         if x.device.type != "cuda" or edge_index.device.type != "cuda":
@@ -432,13 +433,21 @@ class FlowGNN(nn.Module):
         if num_nodes == 0:
             raise ValueError("training forward on an empty graph")
         xin = x.contiguous().float() if (x.dtype != torch.float32 or not x.is_contiguous()) else x
-        csr = self._csr.get(edge_index, num_nodes, CSR_ONE_SELF_LOOP)
-        csr_t = self._csr.get(edge_index, num_nodes, CSR_ONE_SELF_LOOP | CSR_TRANSPOSE)
+        mode = CSR_ONE_SELF_LOOP if self.layer_type == "GCN" else CSR_VERBATIM
+        csr = self._csr.get(edge_index, num_nodes, mode)
+        csr_t = self._csr.get(edge_index, num_nodes, mode | CSR_TRANSPOSE)
         h = T.linear(xin, self.input_proj.weight, self.input_proj.bias)
         p = float(self.dropout.p)
         for i, layer in enumerate(self.gnn_layers):
             try:
-                z = T.gcn_residual(h, layer.lin.weight, layer.bias, csr, csr_t)
+                if self.layer_type == "GCN":
+                    z = T.gcn_residual(h, layer.lin.weight, layer.bias, csr, csr_t)
+                else:   # GIN: nn = Seq(Linear, ReLU, Linear), eps buffer
+                    l1, l2 = layer.nn[0], layer.nn[2]
+                    eps = self._cached("eps", i, (layer.eps,),
+                                       lambda: float(layer.eps.reshape(-1)[0]))
+                    z = T.gin_residual(h, l1.weight, l1.bias, l2.weight, l2.bias, eps, csr,
+                                       csr_t)
             except RuntimeError as e:
                 raise self._layer_error(i, e, num_nodes, edge_index, h, edge_attr) from e
             bn = self.batch_norms[i].module if self.use_batch_norm else None

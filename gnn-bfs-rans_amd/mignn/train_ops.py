@@ -13,6 +13,10 @@ model.train() forward (gnn_model.py:159-195) so that train.py's
   gcn_residual      x + GCNConv(x)  (:166, :184) -- aggregation first, then
                     the transform, bias and residual in one MFMA epilogue;
                     backward through the reversed-edge CSR
+  gin_residual      x + GINConv(x) = x + nn((1+eps) x + sum_j x_j)  (:70-75,
+                    :166, :184) -- verbatim sum aggregation, two MFMA Linears
+                    (ReLU fused into the first, residual into the second);
+                    backward through the reversed verbatim CSR
   bn_relu_dropout   BatchNorm (batch statistics, running-stat update) + ReLU +
                     dropout (:188-191) in one elementwise pass
   WeightedMSELoss   normalization.py:136-250 (forward and backward on device)
@@ -189,6 +193,47 @@ class _GCNResidual(Function):
         return dx, dw, db, None, None
 
 
+class _GINResidual(Function):
+    """z = x + GINConv(x) = x + W2 relu(W1 agg + b1) + b2,
+    agg = (1 + eps) x + sum_{j -> i} x_j over edge_index as given (PyG GINConv,
+    gnn_model.py:70-75; every self-loop entry adds another x_i)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, self_scale: float, csr, csr_t):
+        from .gnn_model import linear as _mfma_linear
+        x = _c(x)
+        n, h = x.shape
+        agg = torch.empty_like(x)
+        _lib.check(_lib.lib().mignn_sum_aggregate(
+            P(csr.row_ptr), P(csr.col), P(x), x.stride(0), float(self_scale), 0, n, h, P(agg),
+            agg.stride(0), _st(x)), "mignn_sum_aggregate")
+        h1 = _mfma_linear(agg, w1, b1, relu=True)
+        z = _mfma_linear(h1, w2, b2, residual=x)
+        ctx.self_scale, ctx.csr_t = self_scale, csr_t
+        ctx.save_for_backward(agg, h1, w1, w2)
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        agg, h1, w1, w2 = ctx.saved_tensors
+        g = _c(gz)
+        n, h = g.shape
+        db2 = col_sums(g)
+        dw2 = weight_grad(g, h1)
+        dh1 = _act_backward(data_grad(g, w2), h1, relu=True, p=0.0, seed=0)
+        db1 = col_sums(dh1)
+        dw1 = weight_grad(dh1, agg)
+        # dx = g + ((1 + eps) dh1 + A^T dh1) W1   (A^T: the reversed verbatim edges;
+        # the aggregation commutes with the right-multiplication by W1)
+        u = torch.empty_like(dh1)
+        csr_t = ctx.csr_t
+        _lib.check(_lib.lib().mignn_sum_aggregate(
+            P(csr_t.row_ptr), P(csr_t.col), P(dh1), dh1.stride(0), float(ctx.self_scale), 0, n,
+            dh1.shape[1], P(u), u.stride(0), _st(g)), "mignn_sum_aggregate(transpose)")
+        dx = data_grad(u, w1, residual=g)
+        return dx, dw1, db1, dw2, db2, None, None, None
+
+
 class _BNReluDropout(Function):
     """dropout(relu(BatchNorm_train(z))); bn_mod = the BatchNorm1d (running
     stats updated in place, as torch does in train mode); bn_mod None: no BN."""
@@ -289,6 +334,10 @@ def dropout(x, p: float, training: bool = True, seed: Optional[int] = None):
 
 def gcn_residual(x, w, b, csr, csr_t):
     return _GCNResidual.apply(x, w, b, csr, csr_t)
+
+
+def gin_residual(x, w1, b1, w2, b2, eps: float, csr, csr_t):
+    return _GINResidual.apply(x, w1, b1, w2, b2, 1.0 + float(eps), csr, csr_t)
 
 
 def bn_relu_dropout(z, bn_mod, p: float, seed: Optional[int] = None):

@@ -1,5 +1,5 @@
 """Generate tests/golden/train.npz: one training step of the reference's own
-FlowGNN + WeightedMSELoss (SURVEY.md §8f-3 parity fixtures).
+FlowGNN + WeightedMSELoss (SURVEY.md §8f-3 parity fixtures), GCN and GIN.
 
 Runs ONLY in the build container (/root/reference): like make_golden.py it
 injects the CPU oracle's PyG-named classes as `torch_geometric.nn` and runs
@@ -49,6 +49,8 @@ CONFIGS = {
     "c1_gcn_h64_l2": dict(hidden_dim=64, num_layers=2),
     "c2_gcn_h128_l4": dict(hidden_dim=128, num_layers=4),
     "gcn_h256_l2": dict(hidden_dim=256, num_layers=2),
+    "gin_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GIN"),
+    "gin_h128_l3": dict(hidden_dim=128, num_layers=3, layer_type="GIN"),
 }
 
 
@@ -66,8 +68,10 @@ def main():
     for ci, (name, cfg) in enumerate(CONFIGS.items()):
         gen = torch.Generator().manual_seed(500 + ci)
         target = torch.randn((x.shape[0], 7), generator=gen)
-        model = FlowGNN(input_dim=3, output_dim=7, layer_type="GCN", use_edge_attr=True,
-                        dropout=0.0, use_batch_norm=True, **cfg)
+        kw = dict(cfg)
+        kw.setdefault("layer_type", "GCN")
+        model = FlowGNN(input_dim=3, output_dim=7, use_edge_attr=True,
+                        dropout=0.0, use_batch_norm=True, **kw)
         sd = seeded_state_dict(model.state_dict(), seed=300 + ci)
         for k, v in sd.items():
             out[f"{name}/sd/{k}"] = v.numpy().copy()

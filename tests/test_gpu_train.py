@@ -1,5 +1,5 @@
 """GPU parity of the training path: one model.train()
-step of FlowGNN(GCN) + WeightedMSELoss through the HIP kernels
+step of FlowGNN(GCN / GIN) + WeightedMSELoss through the HIP kernels
 (mignn.train_ops -> csrc/train.hip) against the reference's own FlowGNN +
 WeightedMSELoss run on the CPU (tests/golden/train.npz, made by
 tests/golden/make_train_fixture.py, dropout 0).
@@ -32,7 +32,7 @@ from mignn.normalization import WeightedMSELoss
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 WEIGHTS = {"U": 1.0, "p": 3.0, "k": 0.5, "epsilon": 0.5, "nut": 0.5}
-CONFIGS = ["c1_gcn_h64_l2", "c2_gcn_h128_l4", "gcn_h256_l2"]
+CONFIGS = ["c1_gcn_h64_l2", "c2_gcn_h128_l4", "gcn_h256_l2", "gin_h64_l2", "gin_h128_l3"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -53,7 +53,8 @@ def _fixture(name):
 def _step(name, fieldwise=True):
     f, cfg, sd = _fixture(name)
     x, ei, ea = bfs_graph("train")
-    model = FlowGNN(input_dim=3, output_dim=7, layer_type="GCN", dropout=0.0, **cfg)
+    cfg.setdefault("layer_type", "GCN")
+    model = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
     model.load_state_dict(sd)
     model = model.to(DEV).train()
     crit = WeightedMSELoss(field_weights=WEIGHTS, use_fieldwise=fieldwise,
@@ -131,7 +132,7 @@ def test_eval_after_train_uses_running_stats():
     from oracle import flowgnn_oracle as orc
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     cfg = json.loads(str(f[f"{name}/cfg"]))
-    cfg["layer_type"] = "GCN"
+    cfg.setdefault("layer_type", "GCN")
     y64 = orc.flowgnn_forward(sd, cfg, x, ei, None, dtype=torch.float64)
     assert (y.double() - y64).abs().max().item() <= 1e-5
 
@@ -259,8 +260,34 @@ def test_bn_relu_dropout_grad_matches_torch():
     assert (bn.bias.grad.cpu().double() - b.grad).abs().max().item() <= 1e-3
 
 
+def test_gin_adam_steps_reduce_loss():
+    """GIN (verbatim sum aggregation, two-Linear nn) through a few Adam steps."""
+    torch.manual_seed(1)
+    x, ei, ea = bfs_graph("train")
+    x, ei = x.to(DEV), ei.to(DEV)
+    c = (x - x.mean(0)) / x.std(0).clamp_min(1e-6)
+    target = torch.stack([torch.sin(c[:, 0]), torch.cos(c[:, 1]), c[:, 0] * c[:, 1],
+                          c[:, 0] ** 2 - 1, torch.tanh(c[:, 1]), 0.5 * c[:, 0],
+                          torch.sin(c[:, 0] + c[:, 1])], 1).contiguous()
+    model = FlowGNN(input_dim=3, hidden_dim=64, output_dim=7, num_layers=2, layer_type="GIN",
+                    dropout=0.1).to(DEV)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-5)
+    crit = WeightedMSELoss(field_weights=WEIGHTS)
+    losses = []
+    for _ in range(25):
+        model.train()
+        opt.zero_grad()
+        loss = crit(model(x, ei), target, pressure_ref_weight=0.1)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+        opt.step()
+        losses.append(loss.item())
+    assert all(np.isfinite(losses))
+    assert losses[-1] < 0.5 * losses[0], losses
+
+
 def test_train_mode_other_layer_types_raise():
-    for lt in ("GAT", "GIN", "Transformer"):
+    for lt in ("GAT", "Transformer"):
         m = FlowGNN(hidden_dim=16, num_layers=1, layer_type=lt).to(DEV).train()
         x, ei, _ = bfs_graph("train")
         with pytest.raises(NotImplementedError):
