@@ -405,9 +405,10 @@ class FlowGNN(nn.Module):
 
     # ------------------------------------------------------------- internals
     def _check_runtime(self, x, edge_index):
-        if self.training and self.layer_type not in ("GCN", "GIN"):
+        if self.training and self.layer_type not in ("GCN", "GIN", "GAT"):
             raise NotImplementedError(
-                f"mignn FlowGNN trains the GCN and GIN layer types (GCN is train.py's default); "
+                f"mignn FlowGNN trains the GCN, GIN and GAT layer types (GCN is train.py's "
+                f"default); "
                 f"model.train() "
                 f"with layer_type={self.layer_type!r} is not implemented -- call .eval() for "
                 "the forward.")
@@ -433,7 +434,7 @@ class FlowGNN(nn.Module):
         if num_nodes == 0:
             raise ValueError("training forward on an empty graph")
         xin = x.contiguous().float() if (x.dtype != torch.float32 or not x.is_contiguous()) else x
-        mode = CSR_ONE_SELF_LOOP if self.layer_type == "GCN" else CSR_VERBATIM
+        mode = CSR_ONE_SELF_LOOP if self.layer_type in ("GCN", "GAT") else CSR_VERBATIM
         csr = self._csr.get(edge_index, num_nodes, mode)
         csr_t = self._csr.get(edge_index, num_nodes, mode | CSR_TRANSPOSE)
         h = T.linear(xin, self.input_proj.weight, self.input_proj.bias)
@@ -442,6 +443,16 @@ class FlowGNN(nn.Module):
             try:
                 if self.layer_type == "GCN":
                     z = T.gcn_residual(h, layer.lin.weight, layer.bias, csr, csr_t)
+                elif self.layer_type == "GAT":
+                    # per-step weight images (O(heads H^2), differentiable):
+                    # wlog = [W_k^T att_src_k | W_k^T att_dst_k], wcat = head-mean blocks
+                    heads, C = layer.heads, layer.out_channels
+                    W = layer.lin.weight.view(heads, C, -1)
+                    wlog = torch.cat([torch.einsum("hck,hc->hk", W, layer.att_src.view(heads, C)),
+                                      torch.einsum("hck,hc->hk", W, layer.att_dst.view(heads, C))])
+                    wcat = W.permute(1, 0, 2).reshape(C, heads * W.shape[2]) / heads
+                    z = T.gat_residual(h, wlog, wcat, layer.bias, csr, csr_t, heads,
+                                       layer.negative_slope, float(layer.dropout))
                 else:   # GIN: nn = Seq(Linear, ReLU, Linear), eps buffer
                     l1, l2 = layer.nn[0], layer.nn[2]
                     eps = self._cached("eps", i, (layer.eps,),

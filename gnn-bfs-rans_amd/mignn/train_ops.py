@@ -17,6 +17,10 @@ model.train() forward (gnn_model.py:159-195) so that train.py's
                     :166, :184) -- verbatim sum aggregation, two MFMA Linears
                     (ReLU fused into the first, residual into the second);
                     backward through the reversed verbatim CSR
+  gat_residual      x + GATConv(x) (:65-68, :168) -- logits GEMM, softmax
+                    aggregation with attention dropout, head-mean GEMM with
+                    bias + residual; backward: rows kernel (softmax state,
+                    dst-logit grads) + reversed-CSR kernel (dx, src-logit grads)
   bn_relu_dropout   BatchNorm (batch statistics, running-stat update) + ReLU +
                     dropout (:188-191) in one elementwise pass
   WeightedMSELoss   normalization.py:136-250 (forward and backward on device)
@@ -234,6 +238,52 @@ class _GINResidual(Function):
         return dx, dw1, db1, dw2, db2, None, None, None
 
 
+class _GATResidual(Function):
+    """z = x + GATConv(x), re-associated: logits = x wlog^T ([N, 2*heads]),
+    Y = softmax-aggregate(x) ([N, heads*H]), z = Y wcat^T + b + x.  wlog / wcat
+    are the per-step weight images (autograd tensors built from lin.weight,
+    att_src, att_dst by FlowGNN); their gradients flow back through them."""
+
+    @staticmethod
+    def forward(ctx, x, wlog, wcat, b, csr, csr_t, heads: int, slope: float, p: float,
+                seed: int):
+        from .gnn_model import linear as _mfma_linear
+        x = _c(x)
+        wlog, wcat = _c(wlog), _c(wcat)
+        n, h = x.shape
+        logits = _mfma_linear(x, wlog)
+        y = torch.empty((n, heads * h), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.lib().mignn_gat_train_forward(
+            P(csr.row_ptr), P(csr.col), P(logits), P(x), x.stride(0), n, h, heads, float(slope),
+            float(p), seed, P(y), y.stride(0), _st(x)), "mignn_gat_train_forward")
+        z = _mfma_linear(y, wcat, b, residual=x)
+        ctx.csr, ctx.csr_t, ctx.meta = csr, csr_t, (heads, slope, p, seed)
+        ctx.save_for_backward(x, logits, y, wlog, wcat)
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, logits, y, wlog, wcat = ctx.saved_tensors
+        heads, slope, p, seed = ctx.meta
+        g = _c(gz)
+        n, h = g.shape
+        db = col_sums(g)
+        dwcat = weight_grad(g, y)                 # [H, heads*H]
+        dy = data_grad(g, wcat)                   # [N, heads*H]
+        stats = torch.empty((n, 3 * heads), dtype=torch.float32, device=g.device)
+        dlog = torch.empty((n, 2 * heads), dtype=torch.float32, device=g.device)
+        dxa = torch.empty_like(g)
+        csr, csr_t = ctx.csr, ctx.csr_t
+        _lib.check(_lib.lib().mignn_gat_train_backward(
+            P(csr.row_ptr), P(csr.col), P(csr_t.row_ptr), P(csr_t.col), P(logits), P(x),
+            x.stride(0), P(dy), dy.stride(0), P(g), g.stride(0), n, h, heads, float(slope),
+            float(p), seed, P(stats), P(dlog), P(dxa), dxa.stride(0), _st(g)),
+            "mignn_gat_train_backward")
+        dwlog = weight_grad(dlog, x)              # [2*heads, H]
+        dx = data_grad(dlog, wlog, residual=dxa)  # + dlogits . wlog
+        return dx, dwlog, dwcat, db, None, None, None, None, None, None
+
+
 class _BNReluDropout(Function):
     """dropout(relu(BatchNorm_train(z))); bn_mod = the BatchNorm1d (running
     stats updated in place, as torch does in train mode); bn_mod None: no BN."""
@@ -338,6 +388,13 @@ def gcn_residual(x, w, b, csr, csr_t):
 
 def gin_residual(x, w1, b1, w2, b2, eps: float, csr, csr_t):
     return _GINResidual.apply(x, w1, b1, w2, b2, 1.0 + float(eps), csr, csr_t)
+
+
+def gat_residual(x, wlog, wcat, b, csr, csr_t, heads: int, slope: float, p: float,
+                 seed: Optional[int] = None):
+    seed = draw_seed() if (seed is None and p > 0.0) else (seed or 0)
+    return _GATResidual.apply(x, wlog, wcat, b, csr, csr_t, int(heads), float(slope), float(p),
+                              seed)
 
 
 def bn_relu_dropout(z, bn_mod, p: float, seed: Optional[int] = None):

@@ -374,6 +374,25 @@ int mignn_wmse_loss_backward(const float* pred, int64_t ldp, const float* tgt, i
 /* the dropout keep-scale mask of (p, seed) as an [n, h] array (tests) */
 int mignn_dropout_mask(int64_t n, int h, float p, uint64_t seed, float* mask, void* stream);
 
+/* GATConv(H, H, heads, concat=False, dropout=p) training (gnn_model.py:65-68, :168;
+ * csrc/gat_train.hip).  logits [n, 2*heads] = x . [v_src | v_dst]^T (ld 2*heads).
+ * Forward: y[i, k*h + c] = sum_{j in row i} drop(alpha_jik) x[j, c], alpha = PyG
+ * softmax of LeakyReLU(a_src[j,k] + a_dst[i,k]); attention dropout keyed on
+ * (seed, i, j, k).  Backward, given dy [n, heads*h]: dlogits [n, 2*heads] and
+ * dx = dz + sum_{i,k} drop alpha_jik dy[i, k] (dz may be NULL);
+ * stats = caller scratch of n*3*heads floats.  Row/col CSRs: mode
+ * MIGNN_CSR_ONE_SELF_LOOP and its MIGNN_CSR_TRANSPOSE. */
+int mignn_gat_train_forward(const int32_t* row_ptr, const int32_t* col, const float* logits,
+                            const float* x, int64_t ldx, int64_t n, int h, int heads,
+                            float negative_slope, float p, uint64_t seed, float* y, int64_t ldy,
+                            void* stream);
+int mignn_gat_train_backward(const int32_t* row_ptr, const int32_t* col, const int32_t* rowt_ptr,
+                             const int32_t* colt, const float* logits, const float* x,
+                             int64_t ldx, const float* dy, int64_t lddy, const float* dz,
+                             int64_t lddz, int64_t n, int h, int heads, float negative_slope,
+                             float p, uint64_t seed, float* stats, float* dlogits, float* dx,
+                             int64_t lddx, void* stream);
+
 /* ------------------------------------------------------------------------
  * Multi-GPU halo helpers and synthetic inputs.
  * ------------------------------------------------------------------------ */

@@ -1,5 +1,5 @@
 """Generate tests/golden/train.npz: one training step of the reference's own
-FlowGNN + WeightedMSELoss (SURVEY.md §8f-3 parity fixtures), GCN and GIN.
+FlowGNN + WeightedMSELoss (SURVEY.md §8f-3 parity fixtures), GCN, GIN and GAT.
 
 Runs ONLY in the build container (/root/reference): like make_golden.py it
 injects the CPU oracle's PyG-named classes as `torch_geometric.nn` and runs
@@ -51,6 +51,8 @@ CONFIGS = {
     "gcn_h256_l2": dict(hidden_dim=256, num_layers=2),
     "gin_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GIN"),
     "gin_h128_l3": dict(hidden_dim=128, num_layers=3, layer_type="GIN"),
+    "gat_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GAT"),
+    "gat_h128_l3": dict(hidden_dim=128, num_layers=3, layer_type="GAT"),
 }
 
 

@@ -73,11 +73,11 @@ def test_errors_mirror_reference():
     with pytest.raises(RuntimeError, match="ROCm devices only"):
         m(torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
     # model.train(): GCN trains on the device (CPU tensors refused the same
-    # GCN and GIN; the attention layer types are eval-only
+    # GCN, GIN and GAT; TransformerConv is eval-only
     with pytest.raises(RuntimeError, match="ROCm devices only"):
         m.train()(torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
     with pytest.raises(NotImplementedError):
-        FlowGNN(hidden_dim=16, num_layers=1, layer_type="GAT").train()(
+        FlowGNN(hidden_dim=16, num_layers=1, layer_type="Transformer").train()(
             torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
 
 
