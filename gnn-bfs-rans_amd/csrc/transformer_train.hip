@@ -1,0 +1,305 @@
+// TransformerConv training path (PyG TransformerConv(H, H,
+// heads, concat=False, dropout=p, edge_dim=None, beta=False) as constructed at
+// gnn_model.py:77-80, called at :170 with edge_attr=None).
+//
+// Training keeps Q, K, V explicit (one MFMA launch for [Wq;Wk;Wv]):
+//   s_ji   = <Q_i[k], K_j[k]> / sqrt(H)           over edge_index as given
+//   alpha  = per-destination softmax (exp(s - max) / (sum + 1e-16)), then
+//            attention dropout (counter hash of (seed, dst, src, head))
+//   O_i    = (1/heads) sum_k sum_j drop(alpha_jik) V_j[k]   (+ x_i, residual)
+//   z      = O + x + lin_skip(x)                              (MFMA epilogue)
+// A row with no incoming edge aggregates to 0 (PyG's empty scatter).
+//
+// Backward, dY_i[k] = dz_i / heads:
+//   dalpha_jik = drop * <dY_i[k], V_j[k]>,  c_ik = sum_j alpha dalpha
+//   ds_jik     = alpha (dalpha - c_ik) / sqrt(H)
+//   dQ_i[k] = sum_j ds K_j[k]                       (rows kernel, forward CSR)
+//   dK_j[k] = sum_i ds Q_i[k],  dV_j[k] = sum_i drop alpha dY_i[k]
+//                                                   (cols kernel, reversed CSR)
+// The rows kernel leaves (max, 1/(sum+1e-16), c) per (row, head); the cols
+// kernel recomputes alpha from Q_i . K_j and those: no edge map, no atomics.
+// One 64-lane wave per row, channels c = lane + 64 v.
+#include "common.hpp"
+
+namespace mignn {
+namespace {
+
+constexpr int kWaves = 4;
+
+__device__ __forceinline__ uint32_t edge_hash(uint64_t seed, uint64_t idx) {
+    uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;   // splitmix64
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return static_cast<uint32_t>(z >> 32);
+}
+
+struct EdgeDrop {
+    uint64_t seed;
+    uint32_t thresh;
+    float scale;
+    int64_t n;
+    int heads;
+    __device__ __forceinline__ float keep(int64_t i, int64_t j, int k) const {
+        if (thresh == 0u) return scale;
+        const uint64_t idx = (static_cast<uint64_t>(i) * n + j) * heads + k;
+        return edge_hash(seed, idx) >= thresh ? scale : 0.f;
+    }
+};
+
+EdgeDrop make_edge_drop(float p, uint64_t seed, int64_t n, int heads) {
+    EdgeDrop d{seed, 0u, 1.f, n, heads};
+    if (p >= 1.f) {
+        d.thresh = 0xFFFFFFFFu;
+        d.scale = 0.f;
+    } else if (p > 0.f) {
+        d.thresh = static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
+        d.scale = 1.f / (1.f - p);
+    }
+    return d;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int VPL>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, int lane, int h, float (&v)[VPL]) {
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        const int c = lane + 64 * u;
+        v[u] = c < h ? p[c] : 0.f;
+    }
+}
+
+template <int VPL>
+__device__ __forceinline__ float dot_row(const float (&a)[VPL], const float* __restrict__ p, int lane,
+                                         int h) {
+    float d = 0.f;
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        const int c = lane + 64 * u;
+        if (c < h) d += a[u] * p[c];
+    }
+    return wave_sum(d);
+}
+
+struct QKV {
+    const float* base;
+    int64_t ld;
+    int h, heads;
+    __device__ __forceinline__ const float* q(int64_t r, int k) const { return base + r * ld + int64_t(k) * h; }
+    __device__ __forceinline__ const float* kk(int64_t r, int k) const { return base + r * ld + int64_t(heads + k) * h; }
+    __device__ __forceinline__ const float* v(int64_t r, int k) const { return base + r * ld + int64_t(2 * heads + k) * h; }
+};
+
+template <int VPL>
+__global__ __launch_bounds__(256) void tf_fwd_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, QKV t, float scale,
+    EdgeDrop drop, const float* __restrict__ x, int64_t ldx, int64_t n, float* __restrict__ o,
+    int64_t ldo) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int h = t.h, beg = row_ptr[i], end = row_ptr[i + 1];
+    const float hinv = 1.f / t.heads;
+    float out[VPL];
+    load_row<VPL>(x + i * ldx, lane, h, out);   // residual x_i
+    for (int k = 0; k < t.heads; ++k) {
+        float q[VPL], acc[VPL];
+        load_row<VPL>(t.q(i, k), lane, h, q);
+        float m = -INFINITY, s = 0.f;
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) acc[u] = 0.f;
+        for (int e = beg; e < end; ++e) {   // online softmax
+            const int64_t j = col[e];
+            const float sc = dot_row<VPL>(q, t.kk(j, k), lane, h) * scale;
+            if (sc > m) {
+                const float r = expf(m - sc);
+                s *= r;
+#pragma unroll
+                for (int u = 0; u < VPL; ++u) acc[u] *= r;
+                m = sc;
+            }
+            const float w = expf(sc - m);
+            s += w;
+            const float wk = w * drop.keep(i, j, k);
+            const float* vj = t.v(j, k);
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+                const int c = lane + 64 * u;
+                if (c < h) acc[u] += wk * vj[c];
+            }
+        }
+        const float f = hinv / (s + 1e-16f);
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) out[u] += acc[u] * f;
+    }
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) {
+        const int c = lane + 64 * u;
+        if (c < h) o[i * ldo + c] = out[u];
+    }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void tf_bwd_rows_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, QKV t, float scale,
+    EdgeDrop drop, const float* __restrict__ dz, int64_t lddz, int64_t n,
+    float* __restrict__ stats, float* __restrict__ dqkv, int64_t ldd) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int h = t.h, heads = t.heads, beg = row_ptr[i], end = row_ptr[i + 1];
+    float dy[VPL];
+    load_row<VPL>(dz + i * lddz, lane, h, dy);
+#pragma unroll
+    for (int u = 0; u < VPL; ++u) dy[u] *= 1.f / heads;
+    for (int k = 0; k < heads; ++k) {
+        float q[VPL], dq[VPL];
+        load_row<VPL>(t.q(i, k), lane, h, q);
+        float m = -INFINITY;
+        for (int e = beg; e < end; ++e) m = fmaxf(m, dot_row<VPL>(q, t.kk(col[e], k), lane, h) * scale);
+        float s = 0.f;
+        for (int e = beg; e < end; ++e) s += expf(dot_row<VPL>(q, t.kk(col[e], k), lane, h) * scale - m);
+        const float inv = 1.f / (s + 1e-16f);
+        float cs = 0.f;
+        for (int e = beg; e < end; ++e) {
+            const int64_t j = col[e];
+            const float alpha = expf(dot_row<VPL>(q, t.kk(j, k), lane, h) * scale - m) * inv;
+            cs += alpha * dot_row<VPL>(dy, t.v(j, k), lane, h) * drop.keep(i, j, k);
+        }
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) dq[u] = 0.f;
+        for (int e = beg; e < end; ++e) {
+            const int64_t j = col[e];
+            const float* kj = t.kk(j, k);
+            const float alpha = expf(dot_row<VPL>(q, kj, lane, h) * scale - m) * inv;
+            const float da = dot_row<VPL>(dy, t.v(j, k), lane, h) * drop.keep(i, j, k);
+            const float ds = alpha * (da - cs) * scale;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+                const int c = lane + 64 * u;
+                if (c < h) dq[u] += ds * kj[c];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+            const int c = lane + 64 * u;
+            if (c < h) dqkv[i * ldd + int64_t(k) * h + c] = dq[u];
+        }
+        if (lane == 0) {
+            stats[i * 3 * heads + k] = m;
+            stats[i * 3 * heads + heads + k] = inv;
+            stats[i * 3 * heads + 2 * heads + k] = cs;
+        }
+    }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(256) void tf_bwd_cols_kernel(
+    const int32_t* __restrict__ rowt_ptr, const int32_t* __restrict__ colt, QKV t, float scale,
+    EdgeDrop drop, const float* __restrict__ dz, int64_t lddz, int64_t n,
+    const float* __restrict__ stats, float* __restrict__ dqkv, int64_t ldd) {
+    const int lane = threadIdx.x & 63;
+    const int64_t j = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+    if (j >= n) return;
+    const int h = t.h, heads = t.heads, beg = rowt_ptr[j], end = rowt_ptr[j + 1];
+    const float hinv = 1.f / heads;
+    for (int k = 0; k < heads; ++k) {
+        float kj[VPL], vj[VPL], dk[VPL], dv[VPL];
+        load_row<VPL>(t.kk(j, k), lane, h, kj);
+        load_row<VPL>(t.v(j, k), lane, h, vj);
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) dk[u] = dv[u] = 0.f;
+        for (int e = beg; e < end; ++e) {
+            const int64_t i = colt[e];
+            const float* qi = t.q(i, k);
+            const float* gi = dz + i * lddz;
+            const float m = stats[i * 3 * heads + k];
+            const float inv = stats[i * 3 * heads + heads + k];
+            const float cs = stats[i * 3 * heads + 2 * heads + k];
+            const float alpha = expf(dot_row<VPL>(kj, qi, lane, h) * scale - m) * inv;
+            const float kp = drop.keep(i, j, k);
+            const float da = dot_row<VPL>(vj, gi, lane, h) * hinv * kp;
+            const float ds = alpha * (da - cs) * scale;
+            const float wv = alpha * kp * hinv;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+                const int c = lane + 64 * u;
+                if (c < h) {
+                    dv[u] += wv * gi[c];
+                    dk[u] += ds * qi[c];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < VPL; ++u) {
+            const int c = lane + 64 * u;
+            if (c < h) {
+                dqkv[j * ldd + int64_t(heads + k) * h + c] = dk[u];
+                dqkv[j * ldd + int64_t(2 * heads + k) * h + c] = dv[u];
+            }
+        }
+    }
+}
+
+int vpl_for(int h) { return h <= 64 ? 1 : h <= 128 ? 2 : h <= 256 ? 4 : 0; }
+
+}  // namespace
+}  // namespace mignn
+
+using namespace mignn;
+
+#define MIGNN_TF_DISPATCH(KERNEL, ...)                                                        \
+    switch (vpl_for(h)) {                                                                    \
+        case 1: KERNEL<1><<<grid, block, 0, st>>>(__VA_ARGS__); break;                       \
+        case 2: KERNEL<2><<<grid, block, 0, st>>>(__VA_ARGS__); break;                       \
+        default: KERNEL<4><<<grid, block, 0, st>>>(__VA_ARGS__); break;                      \
+    }
+
+extern "C" int mignn_transformer_train_forward(const int32_t* row_ptr, const int32_t* col,
+                                               const float* qkv, int64_t ldq, const float* x,
+                                               int64_t ldx, int64_t n, int h, int heads,
+                                               float score_scale, float p, uint64_t seed,
+                                               float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(n >= 0 && h > 0 && heads > 0 && heads <= 8, "transformer_train_forward: bad shape");
+    MIGNN_REQUIRE(vpl_for(h) > 0, "transformer_train_forward: hidden %d > 256", h);
+    MIGNN_REQUIRE(ldq >= int64_t(3) * heads * h && ldx >= h && ldo >= h,
+                  "transformer_train_forward: bad leading dims");
+    if (n == 0) return 0;
+    MIGNN_REQUIRE(row_ptr && col && qkv && x && out, "transformer_train_forward: null pointer");
+    const QKV t{qkv, ldq, h, heads};
+    const EdgeDrop d = make_edge_drop(p, seed, n, heads);
+    const dim3 grid(static_cast<unsigned>((n + kWaves - 1) / kWaves)), block(64 * kWaves);
+    hipStream_t st = as_stream(stream);
+    MIGNN_TF_DISPATCH(tf_fwd_kernel, row_ptr, col, t, score_scale, d, x, ldx, n, out, ldo)
+    return launch_status("tf_fwd_kernel");
+}
+
+extern "C" int mignn_transformer_train_backward(const int32_t* row_ptr, const int32_t* col,
+                                                const int32_t* rowt_ptr, const int32_t* colt,
+                                                const float* qkv, int64_t ldq, const float* dz,
+                                                int64_t lddz, int64_t n, int h, int heads,
+                                                float score_scale, float p, uint64_t seed,
+                                                float* stats, float* dqkv, int64_t ldd,
+                                                void* stream) {
+    MIGNN_REQUIRE(n >= 0 && h > 0 && heads > 0 && heads <= 8, "transformer_train_backward: bad shape");
+    MIGNN_REQUIRE(vpl_for(h) > 0, "transformer_train_backward: hidden %d > 256", h);
+    MIGNN_REQUIRE(ldq >= int64_t(3) * heads * h && ldd >= int64_t(3) * heads * h && lddz >= h,
+                  "transformer_train_backward: bad leading dims");
+    if (n == 0) return 0;
+    MIGNN_REQUIRE(row_ptr && col && rowt_ptr && colt && qkv && dz && stats && dqkv,
+                  "transformer_train_backward: null pointer");
+    const QKV t{qkv, ldq, h, heads};
+    const EdgeDrop d = make_edge_drop(p, seed, n, heads);
+    const dim3 grid(static_cast<unsigned>((n + kWaves - 1) / kWaves)), block(64 * kWaves);
+    hipStream_t st = as_stream(stream);
+    int rc;
+    MIGNN_TF_DISPATCH(tf_bwd_rows_kernel, row_ptr, col, t, score_scale, d, dz, lddz, n, stats, dqkv, ldd)
+    if ((rc = launch_status("tf_bwd_rows_kernel"))) return rc;
+    MIGNN_TF_DISPATCH(tf_bwd_cols_kernel, rowt_ptr, colt, t, score_scale, d, dz, lddz, n, stats, dqkv, ldd)
+    return launch_status("tf_bwd_cols_kernel");
+}

@@ -93,6 +93,12 @@ SIGNATURES = {
     "mignn_dropout_mask": (c_int, [c_int64, c_int, c_float, ctypes.c_uint64, _P, _P]),
     "mignn_gat_train_forward": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, c_int, c_float,
                                         c_float, ctypes.c_uint64, _P, c_int64, _P]),
+    "mignn_transformer_train_forward": (c_int, [_P, _P, _P, c_int64, _P, c_int64, c_int64, c_int,
+                                                c_int, c_float, c_float, ctypes.c_uint64, _P,
+                                                c_int64, _P]),
+    "mignn_transformer_train_backward": (c_int, [_P, _P, _P, _P, _P, c_int64, _P, c_int64,
+                                                 c_int64, c_int, c_int, c_float, c_float,
+                                                 ctypes.c_uint64, _P, _P, c_int64, _P]),
     "mignn_gat_train_backward": (c_int, [_P, _P, _P, _P, _P, _P, c_int64, _P, c_int64, _P,
                                          c_int64, c_int64, c_int, c_int, c_float, c_float,
                                          ctypes.c_uint64, _P, _P, _P, c_int64, _P]),

@@ -405,7 +405,7 @@ class FlowGNN(nn.Module):
 
     # ------------------------------------------------------------- internals
     def _check_runtime(self, x, edge_index):
-        if self.training and self.layer_type not in ("GCN", "GIN", "GAT"):
+        if self.training and self.layer_type not in ("GCN", "GIN", "GAT", "Transformer"):
             raise NotImplementedError(
                 f"mignn FlowGNN trains the GCN, GIN and GAT layer types (GCN is train.py's "
                 f"default); "
@@ -453,6 +453,17 @@ class FlowGNN(nn.Module):
                     wcat = W.permute(1, 0, 2).reshape(C, heads * W.shape[2]) / heads
                     z = T.gat_residual(h, wlog, wcat, layer.bias, csr, csr_t, heads,
                                        layer.negative_slope, float(layer.dropout))
+                elif self.layer_type == "Transformer":
+                    if edge_attr is not None:   # PyG adds edge_attr to value_j (see eval)
+                        _value_plus_edge_attr_check((edge_index.shape[1], HEADS, self.hidden_dim),
+                                                    tuple(edge_attr.shape))
+                    wqkv = torch.cat([layer.lin_query.weight, layer.lin_key.weight,
+                                      layer.lin_value.weight])
+                    bqkv = torch.cat([layer.lin_query.bias, layer.lin_key.bias,
+                                      layer.lin_value.bias])
+                    z = T.transformer_residual(h, wqkv, bqkv, layer.lin_skip.weight,
+                                               layer.lin_skip.bias, csr, csr_t, layer.heads,
+                                               float(layer.dropout))
                 else:   # GIN: nn = Seq(Linear, ReLU, Linear), eps buffer
                     l1, l2 = layer.nn[0], layer.nn[2]
                     eps = self._cached("eps", i, (layer.eps,),

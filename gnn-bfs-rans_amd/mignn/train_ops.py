@@ -21,6 +21,10 @@ model.train() forward (gnn_model.py:159-195) so that train.py's
                     aggregation with attention dropout, head-mean GEMM with
                     bias + residual; backward: rows kernel (softmax state,
                     dst-logit grads) + reversed-CSR kernel (dx, src-logit grads)
+  transformer_residual  x + TransformerConv(x) (:77-80, :170; edge_attr None) --
+                    one [Wq;Wk;Wv] MFMA, softmax aggregation of V with
+                    attention dropout (+ residual), lin_skip MFMA epilogue;
+                    backward: rows kernel (dQ) + reversed-CSR kernel (dK, dV)
   bn_relu_dropout   BatchNorm (batch statistics, running-stat update) + ReLU +
                     dropout (:188-191) in one elementwise pass
   WeightedMSELoss   normalization.py:136-250 (forward and backward on device)
@@ -83,12 +87,17 @@ def data_grad(dy: torch.Tensor, w: torch.Tensor, residual=None) -> torch.Tensor:
     return gemm(dy, dy.stride(0), 1, w, w.stride(0), 1, n, i, o, dx, residual=residual)
 
 
+_COL_CHUNK = 512   # mignn_col_sums' widest reduction (64 lanes x RED_CC columns)
+
+
 def col_sums(x: torch.Tensor) -> torch.Tensor:
     n, h = x.shape
     out = torch.empty(h, dtype=torch.float32, device=x.device)
-    s = _red_scratch(n, h, x.device)
-    _lib.check(_lib.lib().mignn_col_sums(P(x), x.stride(0), n, h, P(out), P(s), s.numel(),
-                                         _st(x)), "mignn_col_sums")
+    s = _red_scratch(n, min(h, _COL_CHUNK), x.device)
+    for c0 in range(0, h, _COL_CHUNK):   # wide inputs ([Q|K|V] grads): column panels
+        xc = x[:, c0:c0 + _COL_CHUNK]
+        _lib.check(_lib.lib().mignn_col_sums(P(xc), x.stride(0), n, xc.shape[1], P(out[c0:]),
+                                             P(s), s.numel(), _st(x)), "mignn_col_sums")
     return out
 
 
@@ -284,6 +293,48 @@ class _GATResidual(Function):
         return dx, dwlog, dwcat, db, None, None, None, None, None, None
 
 
+class _TransformerResidual(Function):
+    """z = x + TransformerConv(x) = x + O + x ws^T + bs,
+    O_i = mean_k sum_j drop(softmax_j(<Q_i,K_j>/sqrt(H))) V_j, [Q|K|V] = x wqkv^T + bqkv."""
+
+    @staticmethod
+    def forward(ctx, x, wqkv, bqkv, ws, bs, csr, csr_t, heads: int, p: float, seed: int):
+        from .gnn_model import linear as _mfma_linear
+        x = _c(x)
+        wqkv, bqkv = _c(wqkv), _c(bqkv)
+        n, h = x.shape
+        qkv = _mfma_linear(x, wqkv, bqkv)                # [N, 3*heads*H]
+        o = torch.empty_like(x)
+        scale = 1.0 / float(h) ** 0.5
+        _lib.check(_lib.lib().mignn_transformer_train_forward(
+            P(csr.row_ptr), P(csr.col), P(qkv), qkv.stride(0), P(x), x.stride(0), n, h, heads,
+            scale, float(p), seed, P(o), o.stride(0), _st(x)), "mignn_transformer_train_forward")
+        z = _mfma_linear(x, ws, bs, residual=o)
+        ctx.csr, ctx.csr_t, ctx.meta = csr, csr_t, (heads, scale, p, seed)
+        ctx.save_for_backward(x, qkv, wqkv, ws)
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, qkv, wqkv, ws = ctx.saved_tensors
+        heads, scale, p, seed = ctx.meta
+        g = _c(gz)
+        n, h = g.shape
+        dbs = col_sums(g)
+        dws = weight_grad(g, x)
+        dqkv = torch.empty_like(qkv)
+        stats = torch.empty((n, 3 * heads), dtype=torch.float32, device=g.device)
+        csr, csr_t = ctx.csr, ctx.csr_t
+        _lib.check(_lib.lib().mignn_transformer_train_backward(
+            P(csr.row_ptr), P(csr.col), P(csr_t.row_ptr), P(csr_t.col), P(qkv), qkv.stride(0),
+            P(g), g.stride(0), n, h, heads, float(scale), float(p), seed, P(stats), P(dqkv),
+            dqkv.stride(0), _st(g)), "mignn_transformer_train_backward")
+        dbqkv = col_sums(dqkv)
+        dwqkv = weight_grad(dqkv, x)
+        dx = data_grad(dqkv, wqkv, residual=data_grad(g, ws, residual=g))
+        return dx, dwqkv, dbqkv, dws, dbs, None, None, None, None, None
+
+
 class _BNReluDropout(Function):
     """dropout(relu(BatchNorm_train(z))); bn_mod = the BatchNorm1d (running
     stats updated in place, as torch does in train mode); bn_mod None: no BN."""
@@ -395,6 +446,13 @@ def gat_residual(x, wlog, wcat, b, csr, csr_t, heads: int, slope: float, p: floa
     seed = draw_seed() if (seed is None and p > 0.0) else (seed or 0)
     return _GATResidual.apply(x, wlog, wcat, b, csr, csr_t, int(heads), float(slope), float(p),
                               seed)
+
+
+def transformer_residual(x, wqkv, bqkv, ws, bs, csr, csr_t, heads: int, p: float,
+                         seed: Optional[int] = None):
+    seed = draw_seed() if (seed is None and p > 0.0) else (seed or 0)
+    return _TransformerResidual.apply(x, wqkv, bqkv, ws, bs, csr, csr_t, int(heads), float(p),
+                                      seed)
 
 
 def bn_relu_dropout(z, bn_mod, p: float, seed: Optional[int] = None):

@@ -405,6 +405,24 @@ int mignn_rows_gather(const float* src, int64_t lds, const int32_t* idx, int64_t
 int mignn_grid_graph(int nx, int ny, int nz, int z_begin, int z_count, int64_t* edge_index,
                      float* x, void* stream);
 
+/* TransformerConv(H, H, heads, concat=False, dropout=p) training, edge_attr=None
+ * (gnn_model.py:77-80, :170; csrc/transformer_train.hip).  qkv [n, 3*heads*h] =
+ * [Q | K | V] (head k at column k*h of each block), verbatim CSR.
+ * Forward: out_i = x_i + (1/heads) sum_k sum_j drop(alpha_jik) V_j[k],
+ * alpha = softmax_j(score_scale <Q_i[k], K_j[k]>) (+1e-16), attention dropout
+ * keyed on (seed, i, j, k).  Backward, given dz [n, h] (dout = dz): writes the
+ * dQ | dK | dV blocks of dqkv; stats = caller scratch of n*3*heads floats. */
+int mignn_transformer_train_forward(const int32_t* row_ptr, const int32_t* col, const float* qkv,
+                                    int64_t ldq, const float* x, int64_t ldx, int64_t n, int h,
+                                    int heads, float score_scale, float p, uint64_t seed,
+                                    float* out, int64_t ldo, void* stream);
+int mignn_transformer_train_backward(const int32_t* row_ptr, const int32_t* col,
+                                     const int32_t* rowt_ptr, const int32_t* colt,
+                                     const float* qkv, int64_t ldq, const float* dz, int64_t lddz,
+                                     int64_t n, int h, int heads, float score_scale, float p,
+                                     uint64_t seed, float* stats, float* dqkv, int64_t ldd,
+                                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,5 +1,5 @@
 """Generate tests/golden/train.npz: one training step of the reference's own
-FlowGNN + WeightedMSELoss (SURVEY.md §8f-3 parity fixtures), GCN, GIN and GAT.
+FlowGNN + WeightedMSELoss (SURVEY.md §8f-3 parity fixtures), GCN, GIN, GAT and Transformer (edge_attr=None).
 
 Runs ONLY in the build container (/root/reference): like make_golden.py it
 injects the CPU oracle's PyG-named classes as `torch_geometric.nn` and runs
@@ -53,6 +53,9 @@ CONFIGS = {
     "gin_h128_l3": dict(hidden_dim=128, num_layers=3, layer_type="GIN"),
     "gat_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GAT"),
     "gat_h128_l3": dict(hidden_dim=128, num_layers=3, layer_type="GAT"),
+    # TransformerConv: edge_attr=None (with edge_attr the reference raises, §8 a-8)
+    "tf_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="Transformer"),
+    "tf_h128_l2": dict(hidden_dim=128, num_layers=2, layer_type="Transformer"),
 }
 
 
@@ -85,7 +88,7 @@ def main():
             crit = WeightedMSELoss(field_weights=WEIGHTS, use_fieldwise=True,
                                    pressure_ref_weight=0.1)
             model.zero_grad()
-            y = model(x.to(dt), ei, ea.to(dt))
+            y = model(x.to(dt), ei, None if kw["layer_type"] == "Transformer" else ea.to(dt))
             loss = crit(y, target.to(dt), pressure_ref_weight=0.1)
             loss.backward()
             # fp64 results stored rounded to float32 (fixture size)

@@ -1,5 +1,5 @@
 """GPU parity of the training path: one model.train()
-step of FlowGNN(GCN / GIN / GAT) + WeightedMSELoss through the HIP kernels
+step of FlowGNN(GCN / GIN / GAT / Transformer) + WeightedMSELoss through the HIP kernels
 (mignn.train_ops -> csrc/train.hip) against the reference's own FlowGNN +
 WeightedMSELoss run on the CPU (tests/golden/train.npz, made by
 tests/golden/make_train_fixture.py, dropout 0).
@@ -12,7 +12,7 @@ tensor) x max|grad| of that tensor.  The gradients are fp32 sums over
 12k nodes with heavy cancellation (BN weights, input_proj.weight): there the
 reference's own fp32 run is off by up to ~1e-2 of max|grad|, and ours by
 0.1-3x that -- both are rounding of the same ill-conditioned sums.  BN
-running stats relative 1e-5.  Dropout (not comparable across RNGs) is tested
+running stats relative 1e-5 / absolute 5e-6.  Dropout (not comparable across RNGs) is tested
 on its own: keep rate, scale, forward/backward mask agreement, determinism
 per seed.
 """
@@ -33,7 +33,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 WEIGHTS = {"U": 1.0, "p": 3.0, "k": 0.5, "epsilon": 0.5, "nut": 0.5}
 CONFIGS = ["c1_gcn_h64_l2", "c2_gcn_h128_l4", "gcn_h256_l2", "gin_h64_l2", "gin_h128_l3",
-           "gat_h64_l2", "gat_h128_l3"]
+           "gat_h64_l2", "gat_h128_l3", "tf_h64_l2", "tf_h128_l2"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -62,7 +62,8 @@ def _step(name, fieldwise=True):
                            pressure_ref_weight=0.1)
     target = torch.from_numpy(f[f"{name}/target"]).to(DEV)
     model.zero_grad()
-    y = model(x.to(DEV), ei.to(DEV), ea.to(DEV))
+    y = model(x.to(DEV), ei.to(DEV),
+              None if cfg["layer_type"] == "Transformer" else ea.to(DEV))
     loss = crit(y, target, pressure_ref_weight=0.1) if fieldwise else crit(y, target)
     loss.backward()
     torch.cuda.synchronize()
@@ -98,12 +99,14 @@ def test_train_step_matches_reference(name):
     bad = [(pn, o, r) for pn, o, r in errs if o > max(2e-4, 4 * r, ref_worst)]
     print(f"{name}: forward {err:.2e}, worst grad rel err {worst:.2e} (ref fp32 {ref_worst:.2e})")
     assert not bad, bad
+    # running stats vs the reference's fp32 run: 0.1 x a batch mean of O(1)
+    # pre-BN values, so both fp32 runs carry ~1e-6 absolute noise
     for i, bn in enumerate(model.batch_norms):
         m = bn.module
         np.testing.assert_allclose(m.running_mean.cpu().numpy(), f[f"{name}/bn/{i}/running_mean"],
-                                   rtol=1e-5, atol=1e-6)
+                                   rtol=1e-5, atol=5e-6)
         np.testing.assert_allclose(m.running_var.cpu().numpy(), f[f"{name}/bn/{i}/running_var"],
-                                   rtol=1e-5, atol=1e-6)
+                                   rtol=1e-5, atol=5e-6)
         assert int(m.num_batches_tracked) == int(f[f"{name}/bn/{i}/num_batches_tracked"])
 
 
@@ -261,7 +264,7 @@ def test_bn_relu_dropout_grad_matches_torch():
     assert (bn.bias.grad.cpu().double() - b.grad).abs().max().item() <= 1e-3
 
 
-@pytest.mark.parametrize("lt", ["GIN", "GAT"])
+@pytest.mark.parametrize("lt", ["GIN", "GAT", "Transformer"])
 def test_other_types_adam_steps_reduce_loss(lt):
     """GIN (verbatim sum aggregation) and GAT (attention dropout 0.1) through a
     few Adam steps."""
@@ -289,12 +292,51 @@ def test_other_types_adam_steps_reduce_loss(lt):
     assert losses[-1] < 0.5 * losses[0], losses
 
 
-def test_train_mode_other_layer_types_raise():
-    for lt in ("Transformer",):
-        m = FlowGNN(hidden_dim=16, num_layers=1, layer_type=lt).to(DEV).train()
-        x, ei, _ = bfs_graph("train")
-        with pytest.raises(NotImplementedError):
-            m(x[:100].to(DEV), ei[:, :10].to(DEV))
+def test_train_transformer_with_edge_attr_raises():
+    """The reference's TransformerConv path fails when edge_attr is passed
+    (value_j + edge_attr broadcast): train mode too."""
+    m = FlowGNN(hidden_dim=16, num_layers=1, layer_type="Transformer").to(DEV).train()
+    x, ei, ea = bfs_graph("train")
+    with pytest.raises(RuntimeError, match="Message passing failed in layer 0 \\(Transformer\\)"):
+        m(x.to(DEV), ei.to(DEV), ea.to(DEV))
+
+
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_transformer_attention_dropout_gradient(p):
+    """Transformer backward (rows + reversed-CSR kernels, attention dropout)
+    vs central differences of its own forward along random directions."""
+    from mignn.gnn_model import build_csr
+    from mignn._lib import CSR_VERBATIM, CSR_TRANSPOSE
+    torch.manual_seed(4)
+    x, ei, _ = bfs_graph("train")
+    n, h, heads = 600, 64, 4
+    keep = (ei[0] < n) & (ei[1] < n)
+    ei = ei[:, keep].to(DEV)
+    csr = build_csr(ei, n, CSR_VERBATIM)
+    csr_t = build_csr(ei, n, CSR_VERBATIM | CSR_TRANSPOSE)
+    xv = (torch.randn(n, h) * 0.5).to(DEV).requires_grad_(True)
+    wqkv = (torch.randn(3 * heads * h, h) * 0.1).to(DEV).requires_grad_(True)
+    bqkv = (torch.randn(3 * heads * h) * 0.1).to(DEV).requires_grad_(True)
+    ws = (torch.randn(h, h) * 0.1).to(DEV).requires_grad_(True)
+    bs = torch.zeros(h, device=DEV, requires_grad=True)
+    f = lambda a, w, bb, s: T.transformer_residual(a, w, bb, s, bs, csr, csr_t, heads, p, seed=7)
+    ts = [xv, wqkv, bqkv, ws]
+    z = f(*ts)
+    gz = torch.randn_like(z)
+    (z * gz).sum().backward()
+    args = [t.detach() for t in ts]
+    res = []
+    for k, t in enumerate(ts):
+        d = torch.randn_like(t)
+        eps = 1e-2
+        with torch.no_grad():
+            ap = list(args); ap[k] = args[k] + eps * d
+            am = list(args); am[k] = args[k] - eps * d
+            num = ((f(*ap) - f(*am)) * gz).sum().item() / (2 * eps)
+        res.append((k, num, (t.grad * d).sum().item()))
+    print(res)
+    for k, num, ana in res:
+        assert abs(num - ana) <= 1e-2 * max(1.0, abs(ana)), (k, num, ana)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.3])

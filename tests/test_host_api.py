@@ -73,10 +73,10 @@ def test_errors_mirror_reference():
     with pytest.raises(RuntimeError, match="ROCm devices only"):
         m(torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
     # model.train(): GCN trains on the device (CPU tensors refused the same
-    # GCN, GIN and GAT; TransformerConv is eval-only
+    # every layer type trains on the device
     with pytest.raises(RuntimeError, match="ROCm devices only"):
         m.train()(torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="ROCm devices only"):
         FlowGNN(hidden_dim=16, num_layers=1, layer_type="Transformer").train()(
             torch.zeros(4, 3), torch.zeros(2, 5, dtype=torch.long))
 
