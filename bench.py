@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--no-bfs", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="skip the mesh->graph builder leg")
     p.add_argument("--cpu-grid", default="100,100,100")
+    p.add_argument("--no-train", action="store_true", help="skip the training-step leg")
+    p.add_argument("--train-grid", default="100,100,100")
     return p.parse_args()
 
 
@@ -277,6 +279,8 @@ def main():
         line["bfs_mesh"] = bfs_leg(dev)
     if rank == 0 and world == 1 and not args.no_graph:
         line["graph_build"] = graph_build_leg(dev, nx, ny, nz, not args.no_cpu)
+    if rank == 0 and world == 1 and not args.no_train:
+        line["train_step"] = train_leg(dev, args)
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_leg(model, sd, cfg, args, dev)
     if rank == 0:
@@ -323,6 +327,58 @@ def bfs_leg(dev):
             "ms_per_forward": round(t * 1e3, 4),
             "edges_per_s": cfg["num_layers"] * ei.shape[1] / t,
             "max_abs_err_vs_ref_cpu": err.max().item(), "mae_vs_ref_cpu": err.mean().item()}
+
+
+def train_leg(dev, args):
+    """one train.py step (train.py:158-196: model.train()
+    forward with batch-stat BN + dropout 0.1, WeightedMSELoss, backward,
+    clip_grad_norm_, Adam) per layer type, L4 H128, on a periodic hex grid
+    (default 1M nodes / 6M edges).  edges/s = L * E / t_step (forward +
+    backward counted once, as the reference's train loop sees it)."""
+    from mignn import FlowGNN
+    from mignn.normalization import WeightedMSELoss
+    from mignn.synthetic import grid_graph
+
+    nx, ny, nz = (int(v) for v in args.train_grid.split(","))
+    x, ei = grid_graph(nx, ny, nz, device=dev)
+    n, e = x.shape[0], ei.shape[1]
+    g = torch.Generator(device="cpu").manual_seed(11)
+    target = torch.randn((n, 7), generator=g).to(dev)
+    weights = {"U": 1.0, "p": 3.0, "k": 0.5, "epsilon": 0.5, "nut": 0.5}   # train.py:352-360
+    out = {"workload": f"periodic_hex_{nx}x{ny}x{nz}", "nodes": n, "edges": e,
+           "step": "train fwd + WeightedMSELoss + backward + clip_grad_norm_ + Adam"}
+    for lt in ("GCN", "GIN", "GAT", "Transformer"):
+        torch.manual_seed(0)
+        model = FlowGNN(input_dim=3, hidden_dim=args.hidden, output_dim=7,
+                        num_layers=args.layers, layer_type=lt, dropout=0.1).to(dev).train()
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
+        crit = WeightedMSELoss(field_weights=weights, use_fieldwise=True, pressure_ref_weight=0.1)
+        ea = None if lt == "Transformer" else torch.zeros((e, 4), device=dev)
+
+        def step():
+            opt.zero_grad()
+            loss = crit(model(x, ei, ea), target, pressure_ref_weight=0.1)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            opt.step()
+            return loss
+
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        k = 5
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(k):
+            loss = step()
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1) / 1e3 / k
+        out[lt] = {"ms_per_step": round(t * 1e3, 3),
+                   "edges_per_s": args.layers * e / t,
+                   "loss_finite": bool(torch.isfinite(loss).item())}
+        del model, opt
+    return out
 
 
 def graph_build_leg(dev, nx, ny, nz, with_cpu):

@@ -43,8 +43,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(
     const int lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
     const int wm = wave >> 1, wn = wave & 1;
-    const int64_t i0 = static_cast<int64_t>(blockIdx.x) * GB;
-    const int64_t j0 = static_cast<int64_t>(blockIdx.y) * GB;
+    // column tiles fastest: the blocks sharing one A row panel (data
+    // gradients, N = 2-4 tiles) run back to back, so the panel is read from
+    // HBM once and hit in L2 by its neighbours
+    const int64_t ntn = (N + GB - 1) / GB;
+    const int64_t i0 = static_cast<int64_t>(blockIdx.x / ntn) * GB;
+    const int64_t j0 = static_cast<int64_t>(blockIdx.x % ntn) * GB;
     const int64_t kb = static_cast<int64_t>(blockIdx.z) * kchunk;
     const int64_t ke = min(K, kb + kchunk);
     f32x4 acc[2][2];
@@ -403,10 +407,8 @@ extern "C" int mignn_gemm(const float* a, int64_t sai, int64_t sak, const float*
     if (kchunk < GK) kchunk = GK;
     nsplit = (k + kchunk - 1) / kchunk;
     if (nsplit < 1) nsplit = 1;
-    MIGNN_REQUIRE((m + GB - 1) / GB < (int64_t(1) << 31) && (n + GB - 1) / GB < 65536,
-                  "gemm: grid too large");
-    dim3 grid(static_cast<unsigned>((m + GB - 1) / GB), static_cast<unsigned>((n + GB - 1) / GB),
-              static_cast<unsigned>(nsplit));
+    MIGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm: grid too large");
+    dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(nsplit));
     if (nsplit == 1) {
         hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, st, a, sai, sak, b, sbk, sbj, m, n,
                            k, k > 0 ? kchunk : GK, r, ldr, c, ldc, (int64_t)0);
