@@ -18,7 +18,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 if [ -n "${PROFILE:-}" ]; then
   export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench \
-      --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --no-bfs \
+      --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu --no-bfs --no-train \
       > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
 fi
