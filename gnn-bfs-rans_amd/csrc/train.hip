@@ -32,12 +32,16 @@ constexpr int GB = 64;   // GEMM block tile (rows and columns of C)
 constexpr int GK = 16;   // reduction chunk staged through LDS
 constexpr int GPAD = 16; // LDS row padding: lanes (g, r) hit banks 16g + r
 
+// A_KROW: A's k index is unit-stride (data gradients dY.W) -- staged in its
+// native [i][k] order (row pad 1: conflict-free-ish stores and MFMA reads);
+// otherwise staged [k][i] (row pad 16).
+template <bool A_KROW>
 __global__ __launch_bounds__(256) void gemm_kernel(
     const float* __restrict__ A, int64_t sai, int64_t sak, const float* __restrict__ B,
     int64_t sbk, int64_t sbj, int64_t M, int64_t N, int64_t K, int64_t kchunk,
     const float* __restrict__ R, int64_t ldr, float* __restrict__ C, int64_t ldc,
     int64_t split_stride) {
-    __shared__ float As[GK][GB + GPAD];   // As[k][i]
+    __shared__ float As[A_KROW ? GB * (GK + 1) : GK * (GB + GPAD)];
     __shared__ float Bs[GK][GB + GPAD];   // Bs[k][j]
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -64,10 +68,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(
         for (int t = 0; t < 4; ++t) {
             const int e = tid + t * 256;
             int ii, kk;
-            if (sak == 1) { kk = e & 15; ii = e >> 4; }
+            if (A_KROW) { kk = e & 15; ii = e >> 4; }
             else { ii = e & 63; kk = e >> 6; }
             const int64_t gi = i0 + ii, gk = k0 + kk;
-            As[kk][ii] = (gi < M && gk < ke) ? A[gi * sai + gk * sak] : 0.f;
+            const float v = (gi < M && gk < ke) ? A[gi * sai + gk * sak] : 0.f;
+            if (A_KROW) As[ii * (GK + 1) + kk] = v;
+            else As[kk * (GB + GPAD) + ii] = v;
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -83,7 +89,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(
         for (int u = 0; u < 4; ++u) {
             float a[2], b[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a[i] = As[u * 4 + g][wm * 32 + i * 16 + r];
+            for (int i = 0; i < 2; ++i) {
+                const int ai = wm * 32 + i * 16 + r, ak = u * 4 + g;
+                a[i] = A_KROW ? As[ai * (GK + 1) + ak] : As[ak * (GB + GPAD) + ai];
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j) b[j] = Bs[u * 4 + g][wn * 32 + j * 16 + r];
 #pragma unroll
@@ -409,13 +418,14 @@ extern "C" int mignn_gemm(const float* a, int64_t sai, int64_t sak, const float*
     if (nsplit < 1) nsplit = 1;
     MIGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm: grid too large");
     dim3 grid(static_cast<unsigned>(tiles), 1, static_cast<unsigned>(nsplit));
+    auto kern = (sak == 1) ? gemm_kernel<true> : gemm_kernel<false>;
     if (nsplit == 1) {
-        hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, st, a, sai, sak, b, sbk, sbj, m, n,
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, a, sai, sak, b, sbk, sbj, m, n,
                            k, k > 0 ? kchunk : GK, r, ldr, c, ldc, (int64_t)0);
         return launch_status("gemm_kernel");
     }
     float* P = static_cast<float*>(scratch);
-    hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, st, a, sai, sak, b, sbk, sbj, m, n, k,
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, a, sai, sak, b, sbk, sbj, m, n, k,
                        kchunk, (const float*)nullptr, (int64_t)0, P, n, m * n);
     int rc = launch_status("gemm_kernel(split)");
     if (rc) return rc;
