@@ -41,8 +41,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(
     int64_t sbk, int64_t sbj, int64_t M, int64_t N, int64_t K, int64_t kchunk,
     const float* __restrict__ R, int64_t ldr, float* __restrict__ C, int64_t ldc,
     int64_t split_stride) {
-    __shared__ float As[A_KROW ? GB * (GK + 1) : GK * (GB + GPAD)];
-    __shared__ float Bs[GK][GB + GPAD];   // Bs[k][j]
+    constexpr int AS = A_KROW ? GB * (GK + 1) : GK * (GB + GPAD);
+    constexpr int BS = GK * (GB + GPAD);
+    // two LDS stages: chunk c+1 is fetched into registers while chunk c
+    // feeds the MFMAs, then stored to the other stage -- one barrier per chunk
+    __shared__ float As[2][AS];
+    __shared__ float Bs[2][BS];   // Bs[k][j]
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
@@ -61,19 +65,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int64_t k0 = kb; k0 < ke; k0 += GK) {
-        // stage A(i0.., k0..) and B(k0.., j0..), consecutive threads along the
-        // unit-stride dimension of each operand
+    // staging map (consecutive threads along each operand's unit-stride dim)
+    int a_off[4], b_off[4];
+    float ra[4], rb[4];
+    auto fetch = [&](int64_t k0) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int e = tid + t * 256;
             int ii, kk;
             if (A_KROW) { kk = e & 15; ii = e >> 4; }
             else { ii = e & 63; kk = e >> 6; }
+            a_off[t] = A_KROW ? ii * (GK + 1) + kk : kk * (GB + GPAD) + ii;
             const int64_t gi = i0 + ii, gk = k0 + kk;
-            const float v = (gi < M && gk < ke) ? A[gi * sai + gk * sak] : 0.f;
-            if (A_KROW) As[ii * (GK + 1) + kk] = v;
-            else As[kk * (GB + GPAD) + ii] = v;
+            ra[t] = (gi < M && gk < ke) ? A[gi * sai + gk * sak] : 0.f;
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -81,26 +85,46 @@ __global__ __launch_bounds__(256) void gemm_kernel(
             int jj, kk;
             if (sbj == 1) { jj = e & 63; kk = e >> 6; }
             else { kk = e & 15; jj = e >> 4; }
+            b_off[t] = kk * (GB + GPAD) + jj;
             const int64_t gj = j0 + jj, gk = k0 + kk;
-            Bs[kk][jj] = (gj < N && gk < ke) ? B[gk * sbk + gj * sbj] : 0.f;
+            rb[t] = (gj < N && gk < ke) ? B[gk * sbk + gj * sbj] : 0.f;
         }
-        __syncthreads();
+    };
+    auto stash = [&](int stage) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            As[stage][a_off[t]] = ra[t];
+            Bs[stage][b_off[t]] = rb[t];
+        }
+    };
+
+    if (kb < ke) {
+        fetch(kb);
+        stash(0);
+    }
+    __syncthreads();
+    int stage = 0;
+    for (int64_t k0 = kb; k0 < ke; k0 += GK) {
+        const bool more = k0 + GK < ke;
+        if (more) fetch(k0 + GK);   // in flight during the MFMAs below
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             float a[2], b[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int ai = wm * 32 + i * 16 + r, ak = u * 4 + g;
-                a[i] = A_KROW ? As[ai * (GK + 1) + ak] : As[ak * (GB + GPAD) + ai];
+                a[i] = A_KROW ? As[stage][ai * (GK + 1) + ak] : As[stage][ak * (GB + GPAD) + ai];
             }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = Bs[u * 4 + g][wn * 32 + j * 16 + r];
+            for (int j = 0; j < 2; ++j) b[j] = Bs[stage][(u * 4 + g) * (GB + GPAD) + wn * 32 + j * 16 + r];
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[i][j] = mfma16x16x4(a[i], b[j], acc[i][j]);
         }
+        if (more) stash(stage ^ 1);
         __syncthreads();
+        stage ^= 1;
     }
     float* Cz = C + static_cast<int64_t>(blockIdx.z) * split_stride;
 #pragma unroll
