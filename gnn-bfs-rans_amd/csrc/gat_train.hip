@@ -17,9 +17,11 @@
 //   dlogits[i, heads + k] = sum_j ds_jik          (rows kernel, forward CSR)
 //   dlogits[j, k]         = sum_i ds_jik          (cols kernel, reversed CSR)
 //   dx_j = dz_j + sum_{i,k} drop alpha_jik dY_i[k] (+ dlogits . [v_src|v_dst] by GEMM)
-// The rows kernel leaves (max, 1/(sum+1e-16), c) per (row, head) so the
-// cols kernel recomputes alpha for any edge from the two logits alone: no
-// edge-id map between the two CSR orders, no atomics, deterministic.
+// The forward leaves (max, 1/(sum+1e-16)) per (row, head); the rows kernel
+// adds c = <dY_i[k], Y_i[k]> (Y = the forward's aggregate, so no extra pass)
+// and needs one pass over the row; the cols kernel recomputes alpha for any
+// edge from the two logits and those values: no edge-id map between the two
+// CSR orders, no atomics, deterministic.
 //
 // One 64-lane wave per row, channels c = lane + 64 v (coalesced row reads),
 // scalar softmax state replicated across the wave.
@@ -75,7 +77,8 @@ template <int VPL>
 __global__ __launch_bounds__(256) void gat_fwd_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ logits, const float* __restrict__ x, int64_t ldx, int64_t n, int h,
-    int heads, float slope, EdgeDrop drop, float* __restrict__ y, int64_t ldy) {
+    int heads, float slope, EdgeDrop drop, float* __restrict__ y, int64_t ldy,
+    float* __restrict__ stats) {
     const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
     if (i >= n) return;
@@ -89,6 +92,10 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(
         for (int e = beg; e < end; ++e)
             s += expf(leaky(logits[int64_t(col[e]) * ldl + k] + ad, slope) - m);
         const float inv = 1.f / (s + 1e-16f);
+        if (stats && lane == 0) {   // softmax state for the backward
+            stats[i * 3 * heads + k] = m;
+            stats[i * 3 * heads + heads + k] = inv;
+        }
         float acc[VPL];
 #pragma unroll
         for (int v = 0; v < VPL; ++v) acc[v] = 0.f;
@@ -114,8 +121,9 @@ template <int VPL>
 __global__ __launch_bounds__(256) void gat_bwd_rows_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ logits, const float* __restrict__ x, int64_t ldx,
-    const float* __restrict__ dy, int64_t lddy, int64_t n, int h, int heads, float slope,
-    EdgeDrop drop, float* __restrict__ stats, float* __restrict__ dlog) {
+    const float* __restrict__ dy, int64_t lddy, const float* __restrict__ yf, int64_t ldyf,
+    int64_t n, int h, int heads, float slope, EdgeDrop drop, float* __restrict__ stats,
+    float* __restrict__ dlog) {
     const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
     if (i >= n) return;
@@ -123,19 +131,19 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_kernel(
     const int ldl = 2 * heads;
     for (int k = 0; k < heads; ++k) {
         const float ad = logits[i * ldl + heads + k];
-        float m = -INFINITY;
-        for (int e = beg; e < end; ++e) m = fmaxf(m, leaky(logits[int64_t(col[e]) * ldl + k] + ad, slope));
-        float s = 0.f;
-        for (int e = beg; e < end; ++e)
-            s += expf(leaky(logits[int64_t(col[e]) * ldl + k] + ad, slope) - m);
-        const float inv = 1.f / (s + 1e-16f);
+        const float m = stats[i * 3 * heads + k];          // from the forward
+        const float inv = stats[i * 3 * heads + heads + k];
         float g[VPL];
+        float d0 = 0.f;
 #pragma unroll
         for (int v = 0; v < VPL; ++v) {
             const int c = lane + 64 * v;
             g[v] = c < h ? dy[i * lddy + int64_t(k) * h + c] : 0.f;
+            if (c < h) d0 += g[v] * yf[i * ldyf + int64_t(k) * h + c];
         }
-        float cs = 0.f, a1 = 0.f, a2 = 0.f;
+        // c = sum_j alpha dalpha = <dY_i[k], Y_i[k]> (Y = the forward's aggregate)
+        const float cs = wave_sum(d0);
+        float a1 = 0.f, a2 = 0.f;
         for (int e = beg; e < end; ++e) {
             const int64_t j = col[e];
             const float pre = logits[j * ldl + k] + ad;
@@ -148,13 +156,10 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_kernel(
                 if (c < h) d += g[v] * x[j * ldx + c];
             }
             const float da = wave_sum(d) * drop.keep(i, j, k);
-            cs += alpha * da;
             a1 += alpha * da * lp;
             a2 += alpha * lp;
         }
         if (lane == 0) {
-            stats[i * 3 * heads + k] = m;
-            stats[i * 3 * heads + heads + k] = inv;
             stats[i * 3 * heads + 2 * heads + k] = cs;
             dlog[i * ldl + heads + k] = a1 - cs * a2;
         }
@@ -226,7 +231,8 @@ using namespace mignn;
 extern "C" int mignn_gat_train_forward(const int32_t* row_ptr, const int32_t* col,
                                        const float* logits, const float* x, int64_t ldx,
                                        int64_t n, int h, int heads, float negative_slope, float p,
-                                       uint64_t seed, float* y, int64_t ldy, void* stream) {
+                                       uint64_t seed, float* y, int64_t ldy, float* stats,
+                                       void* stream) {
     MIGNN_REQUIRE(n >= 0 && h > 0 && heads > 0 && heads <= 8, "gat_train_forward: bad shape");
     MIGNN_REQUIRE(vpl_for(h) > 0, "gat_train_forward: hidden %d > 256", h);
     MIGNN_REQUIRE(ldx >= h && ldy >= int64_t(heads) * h, "gat_train_forward: bad leading dims");
@@ -236,9 +242,9 @@ extern "C" int mignn_gat_train_forward(const int32_t* row_ptr, const int32_t* co
     const dim3 grid(static_cast<unsigned>((n + kWaves - 1) / kWaves)), block(64 * kWaves);
     hipStream_t st = as_stream(stream);
     switch (vpl_for(h)) {
-        case 1: gat_fwd_kernel<1><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, n, h, heads, negative_slope, d, y, ldy); break;
-        case 2: gat_fwd_kernel<2><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, n, h, heads, negative_slope, d, y, ldy); break;
-        default: gat_fwd_kernel<4><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, n, h, heads, negative_slope, d, y, ldy); break;
+        case 1: gat_fwd_kernel<1><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, n, h, heads, negative_slope, d, y, ldy, stats); break;
+        case 2: gat_fwd_kernel<2><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, n, h, heads, negative_slope, d, y, ldy, stats); break;
+        default: gat_fwd_kernel<4><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, n, h, heads, negative_slope, d, y, ldy, stats); break;
     }
     return launch_status("gat_fwd_kernel");
 }
@@ -246,7 +252,8 @@ extern "C" int mignn_gat_train_forward(const int32_t* row_ptr, const int32_t* co
 extern "C" int mignn_gat_train_backward(const int32_t* row_ptr, const int32_t* col,
                                         const int32_t* rowt_ptr, const int32_t* colt,
                                         const float* logits, const float* x, int64_t ldx,
-                                        const float* dy, int64_t lddy, const float* dz,
+                                        const float* dy, int64_t lddy, const float* y,
+                                        int64_t ldy, const float* dz,
                                         int64_t lddz, int64_t n, int h, int heads,
                                         float negative_slope, float p, uint64_t seed,
                                         float* stats, float* dlogits, float* dx, int64_t lddx,
@@ -256,16 +263,17 @@ extern "C" int mignn_gat_train_backward(const int32_t* row_ptr, const int32_t* c
     MIGNN_REQUIRE(ldx >= h && lddx >= h && lddy >= int64_t(heads) * h && (!dz || lddz >= h),
                   "gat_train_backward: bad leading dims");
     if (n == 0) return 0;
-    MIGNN_REQUIRE(row_ptr && col && rowt_ptr && colt && logits && x && dy && stats && dlogits && dx,
+    MIGNN_REQUIRE(ldy >= int64_t(heads) * h, "gat_train_backward: bad ldy");
+    MIGNN_REQUIRE(row_ptr && col && rowt_ptr && colt && logits && x && dy && y && stats && dlogits && dx,
                   "gat_train_backward: null pointer");
     const EdgeDrop d = make_edge_drop(p, seed, n, heads);
     const dim3 grid(static_cast<unsigned>((n + kWaves - 1) / kWaves)), block(64 * kWaves);
     hipStream_t st = as_stream(stream);
     int rc;
     switch (vpl_for(h)) {
-        case 1: gat_bwd_rows_kernel<1><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, dy, lddy, n, h, heads, negative_slope, d, stats, dlogits); break;
-        case 2: gat_bwd_rows_kernel<2><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, dy, lddy, n, h, heads, negative_slope, d, stats, dlogits); break;
-        default: gat_bwd_rows_kernel<4><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, dy, lddy, n, h, heads, negative_slope, d, stats, dlogits); break;
+        case 1: gat_bwd_rows_kernel<1><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, dy, lddy, y, ldy, n, h, heads, negative_slope, d, stats, dlogits); break;
+        case 2: gat_bwd_rows_kernel<2><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, dy, lddy, y, ldy, n, h, heads, negative_slope, d, stats, dlogits); break;
+        default: gat_bwd_rows_kernel<4><<<grid, block, 0, st>>>(row_ptr, col, logits, x, ldx, dy, lddy, y, ldy, n, h, heads, negative_slope, d, stats, dlogits); break;
     }
     if ((rc = launch_status("gat_bwd_rows_kernel"))) return rc;
     switch (vpl_for(h)) {

@@ -16,8 +16,10 @@
 //   dQ_i[k] = sum_j ds K_j[k]                       (rows kernel, forward CSR)
 //   dK_j[k] = sum_i ds Q_i[k],  dV_j[k] = sum_i drop alpha dY_i[k]
 //                                                   (cols kernel, reversed CSR)
-// The rows kernel leaves (max, 1/(sum+1e-16), c) per (row, head); the cols
-// kernel recomputes alpha from Q_i . K_j and those: no edge map, no atomics.
+// The forward leaves (max, 1/(sum+1e-16)) per (row, head) and the per-head
+// aggregates Y_i[k]; the rows kernel takes c = <dY_i[k], Y_i[k]> from them and
+// makes one pass over the row; the cols kernel recomputes alpha from
+// Q_i . K_j and those values: no edge map, no atomics.
 // One 64-lane wave per row, channels c = lane + 64 v.
 #include "common.hpp"
 
@@ -99,7 +101,7 @@ template <int VPL>
 __global__ __launch_bounds__(256) void tf_fwd_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, QKV t, float scale,
     EdgeDrop drop, const float* __restrict__ x, int64_t ldx, int64_t n, float* __restrict__ o,
-    int64_t ldo) {
+    int64_t ldo, float* __restrict__ yh, int64_t ldyh, float* __restrict__ stats) {
     const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
     if (i >= n) return;
@@ -133,9 +135,18 @@ __global__ __launch_bounds__(256) void tf_fwd_kernel(
                 if (c < h) acc[u] += wk * vj[c];
             }
         }
-        const float f = hinv / (s + 1e-16f);
+        const float inv = 1.f / (s + 1e-16f);
 #pragma unroll
-        for (int u = 0; u < VPL; ++u) out[u] += acc[u] * f;
+        for (int u = 0; u < VPL; ++u) {
+            const int c = lane + 64 * u;
+            const float yv = acc[u] * inv;   // per-head aggregate Y_i[k]
+            out[u] += yv * hinv;
+            if (yh && c < h) yh[i * ldyh + int64_t(k) * h + c] = yv;
+        }
+        if (stats && lane == 0) {   // softmax state for the backward
+            stats[i * 3 * t.heads + k] = m;
+            stats[i * 3 * t.heads + t.heads + k] = inv;
+        }
     }
 #pragma unroll
     for (int u = 0; u < VPL; ++u) {
@@ -147,8 +158,8 @@ __global__ __launch_bounds__(256) void tf_fwd_kernel(
 template <int VPL>
 __global__ __launch_bounds__(256) void tf_bwd_rows_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col, QKV t, float scale,
-    EdgeDrop drop, const float* __restrict__ dz, int64_t lddz, int64_t n,
-    float* __restrict__ stats, float* __restrict__ dqkv, int64_t ldd) {
+    EdgeDrop drop, const float* __restrict__ dz, int64_t lddz, const float* __restrict__ yh,
+    int64_t ldyh, int64_t n, float* __restrict__ stats, float* __restrict__ dqkv, int64_t ldd) {
     const int lane = threadIdx.x & 63;
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
     if (i >= n) return;
@@ -160,17 +171,10 @@ __global__ __launch_bounds__(256) void tf_bwd_rows_kernel(
     for (int k = 0; k < heads; ++k) {
         float q[VPL], dq[VPL];
         load_row<VPL>(t.q(i, k), lane, h, q);
-        float m = -INFINITY;
-        for (int e = beg; e < end; ++e) m = fmaxf(m, dot_row<VPL>(q, t.kk(col[e], k), lane, h) * scale);
-        float s = 0.f;
-        for (int e = beg; e < end; ++e) s += expf(dot_row<VPL>(q, t.kk(col[e], k), lane, h) * scale - m);
-        const float inv = 1.f / (s + 1e-16f);
-        float cs = 0.f;
-        for (int e = beg; e < end; ++e) {
-            const int64_t j = col[e];
-            const float alpha = expf(dot_row<VPL>(q, t.kk(j, k), lane, h) * scale - m) * inv;
-            cs += alpha * dot_row<VPL>(dy, t.v(j, k), lane, h) * drop.keep(i, j, k);
-        }
+        const float m = stats[i * 3 * heads + k];          // from the forward
+        const float inv = stats[i * 3 * heads + heads + k];
+        // c = sum_j alpha dalpha = <dY_i[k], Y_i[k]> (Y = the forward's per-head aggregate)
+        const float cs = dot_row<VPL>(dy, yh + i * ldyh + int64_t(k) * h, lane, h);
 #pragma unroll
         for (int u = 0; u < VPL; ++u) dq[u] = 0.f;
         for (int e = beg; e < end; ++e) {
@@ -190,11 +194,7 @@ __global__ __launch_bounds__(256) void tf_bwd_rows_kernel(
             const int c = lane + 64 * u;
             if (c < h) dqkv[i * ldd + int64_t(k) * h + c] = dq[u];
         }
-        if (lane == 0) {
-            stats[i * 3 * heads + k] = m;
-            stats[i * 3 * heads + heads + k] = inv;
-            stats[i * 3 * heads + 2 * heads + k] = cs;
-        }
+        if (lane == 0) stats[i * 3 * heads + 2 * heads + k] = cs;
     }
 }
 
@@ -264,7 +264,8 @@ extern "C" int mignn_transformer_train_forward(const int32_t* row_ptr, const int
                                                const float* qkv, int64_t ldq, const float* x,
                                                int64_t ldx, int64_t n, int h, int heads,
                                                float score_scale, float p, uint64_t seed,
-                                               float* out, int64_t ldo, void* stream) {
+                                               float* out, int64_t ldo, float* yh, int64_t ldyh,
+                                               float* stats, void* stream) {
     MIGNN_REQUIRE(n >= 0 && h > 0 && heads > 0 && heads <= 8, "transformer_train_forward: bad shape");
     MIGNN_REQUIRE(vpl_for(h) > 0, "transformer_train_forward: hidden %d > 256", h);
     MIGNN_REQUIRE(ldq >= int64_t(3) * heads * h && ldx >= h && ldo >= h,
@@ -275,14 +276,17 @@ extern "C" int mignn_transformer_train_forward(const int32_t* row_ptr, const int
     const EdgeDrop d = make_edge_drop(p, seed, n, heads);
     const dim3 grid(static_cast<unsigned>((n + kWaves - 1) / kWaves)), block(64 * kWaves);
     hipStream_t st = as_stream(stream);
-    MIGNN_TF_DISPATCH(tf_fwd_kernel, row_ptr, col, t, score_scale, d, x, ldx, n, out, ldo)
+    MIGNN_REQUIRE(!yh || ldyh >= int64_t(heads) * h, "transformer_train_forward: bad ldyh");
+    MIGNN_TF_DISPATCH(tf_fwd_kernel, row_ptr, col, t, score_scale, d, x, ldx, n, out, ldo, yh, ldyh,
+                      stats)
     return launch_status("tf_fwd_kernel");
 }
 
 extern "C" int mignn_transformer_train_backward(const int32_t* row_ptr, const int32_t* col,
                                                 const int32_t* rowt_ptr, const int32_t* colt,
                                                 const float* qkv, int64_t ldq, const float* dz,
-                                                int64_t lddz, int64_t n, int h, int heads,
+                                                int64_t lddz, const float* yh, int64_t ldyh,
+                                                int64_t n, int h, int heads,
                                                 float score_scale, float p, uint64_t seed,
                                                 float* stats, float* dqkv, int64_t ldd,
                                                 void* stream) {
@@ -291,14 +295,16 @@ extern "C" int mignn_transformer_train_backward(const int32_t* row_ptr, const in
     MIGNN_REQUIRE(ldq >= int64_t(3) * heads * h && ldd >= int64_t(3) * heads * h && lddz >= h,
                   "transformer_train_backward: bad leading dims");
     if (n == 0) return 0;
-    MIGNN_REQUIRE(row_ptr && col && rowt_ptr && colt && qkv && dz && stats && dqkv,
+    MIGNN_REQUIRE(ldyh >= int64_t(heads) * h, "transformer_train_backward: bad ldyh");
+    MIGNN_REQUIRE(row_ptr && col && rowt_ptr && colt && qkv && dz && yh && stats && dqkv,
                   "transformer_train_backward: null pointer");
     const QKV t{qkv, ldq, h, heads};
     const EdgeDrop d = make_edge_drop(p, seed, n, heads);
     const dim3 grid(static_cast<unsigned>((n + kWaves - 1) / kWaves)), block(64 * kWaves);
     hipStream_t st = as_stream(stream);
     int rc;
-    MIGNN_TF_DISPATCH(tf_bwd_rows_kernel, row_ptr, col, t, score_scale, d, dz, lddz, n, stats, dqkv, ldd)
+    MIGNN_TF_DISPATCH(tf_bwd_rows_kernel, row_ptr, col, t, score_scale, d, dz, lddz, yh, ldyh, n,
+                      stats, dqkv, ldd)
     if ((rc = launch_status("tf_bwd_rows_kernel"))) return rc;
     MIGNN_TF_DISPATCH(tf_bwd_cols_kernel, rowt_ptr, colt, t, score_scale, d, dz, lddz, n, stats, dqkv, ldd)
     return launch_status("tf_bwd_cols_kernel");

@@ -92,15 +92,15 @@ SIGNATURES = {
                                          c_int, _P, _P, _P, c_int64, _P]),
     "mignn_dropout_mask": (c_int, [c_int64, c_int, c_float, ctypes.c_uint64, _P, _P]),
     "mignn_gat_train_forward": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, c_int, c_float,
-                                        c_float, ctypes.c_uint64, _P, c_int64, _P]),
+                                        c_float, ctypes.c_uint64, _P, c_int64, _P, _P]),
     "mignn_transformer_train_forward": (c_int, [_P, _P, _P, c_int64, _P, c_int64, c_int64, c_int,
                                                 c_int, c_float, c_float, ctypes.c_uint64, _P,
-                                                c_int64, _P]),
+                                                c_int64, _P, c_int64, _P, _P]),
     "mignn_transformer_train_backward": (c_int, [_P, _P, _P, _P, _P, c_int64, _P, c_int64,
-                                                 c_int64, c_int, c_int, c_float, c_float,
+                                                 _P, c_int64, c_int64, c_int, c_int, c_float, c_float,
                                                  ctypes.c_uint64, _P, _P, c_int64, _P]),
     "mignn_gat_train_backward": (c_int, [_P, _P, _P, _P, _P, _P, c_int64, _P, c_int64, _P,
-                                         c_int64, c_int64, c_int, c_int, c_float, c_float,
+                                         c_int64, _P, c_int64, c_int64, c_int, c_int, c_float, c_float,
                                          ctypes.c_uint64, _P, _P, _P, c_int64, _P]),
     "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,

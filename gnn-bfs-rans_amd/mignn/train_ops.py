@@ -262,30 +262,31 @@ class _GATResidual(Function):
         n, h = x.shape
         logits = _mfma_linear(x, wlog)
         y = torch.empty((n, heads * h), dtype=torch.float32, device=x.device)
+        stats = torch.empty((n, 3 * heads), dtype=torch.float32, device=x.device)
         _lib.check(_lib.lib().mignn_gat_train_forward(
             P(csr.row_ptr), P(csr.col), P(logits), P(x), x.stride(0), n, h, heads, float(slope),
-            float(p), seed, P(y), y.stride(0), _st(x)), "mignn_gat_train_forward")
+            float(p), seed, P(y), y.stride(0), P(stats), _st(x)), "mignn_gat_train_forward")
         z = _mfma_linear(y, wcat, b, residual=x)
         ctx.csr, ctx.csr_t, ctx.meta = csr, csr_t, (heads, slope, p, seed)
-        ctx.save_for_backward(x, logits, y, wlog, wcat)
+        ctx.save_for_backward(x, logits, y, wlog, wcat, stats)
         return z
 
     @staticmethod
     def backward(ctx, gz):
-        x, logits, y, wlog, wcat = ctx.saved_tensors
+        x, logits, y, wlog, wcat, stats = ctx.saved_tensors
         heads, slope, p, seed = ctx.meta
         g = _c(gz)
         n, h = g.shape
         db = col_sums(g)
         dwcat = weight_grad(g, y)                 # [H, heads*H]
         dy = data_grad(g, wcat)                   # [N, heads*H]
-        stats = torch.empty((n, 3 * heads), dtype=torch.float32, device=g.device)
         dlog = torch.empty((n, 2 * heads), dtype=torch.float32, device=g.device)
         dxa = torch.empty_like(g)
         csr, csr_t = ctx.csr, ctx.csr_t
         _lib.check(_lib.lib().mignn_gat_train_backward(
             P(csr.row_ptr), P(csr.col), P(csr_t.row_ptr), P(csr_t.col), P(logits), P(x),
-            x.stride(0), P(dy), dy.stride(0), P(g), g.stride(0), n, h, heads, float(slope),
+            x.stride(0), P(dy), dy.stride(0), P(y), y.stride(0), P(g), g.stride(0), n, h, heads,
+            float(slope),
             float(p), seed, P(stats), P(dlog), P(dxa), dxa.stride(0), _st(g)),
             "mignn_gat_train_backward")
         dwlog = weight_grad(dlog, x)              # [2*heads, H]
@@ -305,29 +306,32 @@ class _TransformerResidual(Function):
         n, h = x.shape
         qkv = _mfma_linear(x, wqkv, bqkv)                # [N, 3*heads*H]
         o = torch.empty_like(x)
+        yh = torch.empty((n, heads * h), dtype=torch.float32, device=x.device)
+        stats = torch.empty((n, 3 * heads), dtype=torch.float32, device=x.device)
         scale = 1.0 / float(h) ** 0.5
         _lib.check(_lib.lib().mignn_transformer_train_forward(
             P(csr.row_ptr), P(csr.col), P(qkv), qkv.stride(0), P(x), x.stride(0), n, h, heads,
-            scale, float(p), seed, P(o), o.stride(0), _st(x)), "mignn_transformer_train_forward")
+            scale, float(p), seed, P(o), o.stride(0), P(yh), yh.stride(0), P(stats), _st(x)),
+            "mignn_transformer_train_forward")
         z = _mfma_linear(x, ws, bs, residual=o)
         ctx.csr, ctx.csr_t, ctx.meta = csr, csr_t, (heads, scale, p, seed)
-        ctx.save_for_backward(x, qkv, wqkv, ws)
+        ctx.save_for_backward(x, qkv, wqkv, ws, yh, stats)
         return z
 
     @staticmethod
     def backward(ctx, gz):
-        x, qkv, wqkv, ws = ctx.saved_tensors
+        x, qkv, wqkv, ws, yh, stats = ctx.saved_tensors
         heads, scale, p, seed = ctx.meta
         g = _c(gz)
         n, h = g.shape
         dbs = col_sums(g)
         dws = weight_grad(g, x)
         dqkv = torch.empty_like(qkv)
-        stats = torch.empty((n, 3 * heads), dtype=torch.float32, device=g.device)
         csr, csr_t = ctx.csr, ctx.csr_t
         _lib.check(_lib.lib().mignn_transformer_train_backward(
             P(csr.row_ptr), P(csr.col), P(csr_t.row_ptr), P(csr_t.col), P(qkv), qkv.stride(0),
-            P(g), g.stride(0), n, h, heads, float(scale), float(p), seed, P(stats), P(dqkv),
+            P(g), g.stride(0), P(yh), yh.stride(0), n, h, heads, float(scale), float(p), seed,
+            P(stats), P(dqkv),
             dqkv.stride(0), _st(g)), "mignn_transformer_train_backward")
         dbqkv = col_sums(dqkv)
         dwqkv = weight_grad(dqkv, x)

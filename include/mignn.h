@@ -379,17 +379,19 @@ int mignn_dropout_mask(int64_t n, int h, float p, uint64_t seed, float* mask, vo
  * Forward: y[i, k*h + c] = sum_{j in row i} drop(alpha_jik) x[j, c], alpha = PyG
  * softmax of LeakyReLU(a_src[j,k] + a_dst[i,k]); attention dropout keyed on
  * (seed, i, j, k).  Backward, given dy [n, heads*h]: dlogits [n, 2*heads] and
- * dx = dz + sum_{i,k} drop alpha_jik dy[i, k] (dz may be NULL);
- * stats = caller scratch of n*3*heads floats.  Row/col CSRs: mode
+ * dx = dz + sum_{i,k} drop alpha_jik dy[i, k] (dz may be NULL).  stats = caller
+ * buffer of n*3*heads floats: the forward writes the softmax state into it
+ * (nullable there), the backward reads it (y = the forward's output).   Row/col CSRs: mode
  * MIGNN_CSR_ONE_SELF_LOOP and its MIGNN_CSR_TRANSPOSE. */
 int mignn_gat_train_forward(const int32_t* row_ptr, const int32_t* col, const float* logits,
                             const float* x, int64_t ldx, int64_t n, int h, int heads,
                             float negative_slope, float p, uint64_t seed, float* y, int64_t ldy,
-                            void* stream);
+                            float* stats, void* stream);
 int mignn_gat_train_backward(const int32_t* row_ptr, const int32_t* col, const int32_t* rowt_ptr,
                              const int32_t* colt, const float* logits, const float* x,
-                             int64_t ldx, const float* dy, int64_t lddy, const float* dz,
-                             int64_t lddz, int64_t n, int h, int heads, float negative_slope,
+                             int64_t ldx, const float* dy, int64_t lddy, const float* y,
+                             int64_t ldy, const float* dz, int64_t lddz, int64_t n, int h,
+                             int heads, float negative_slope,
                              float p, uint64_t seed, float* stats, float* dlogits, float* dx,
                              int64_t lddx, void* stream);
 
@@ -411,15 +413,18 @@ int mignn_grid_graph(int nx, int ny, int nz, int z_begin, int z_count, int64_t* 
  * Forward: out_i = x_i + (1/heads) sum_k sum_j drop(alpha_jik) V_j[k],
  * alpha = softmax_j(score_scale <Q_i[k], K_j[k]>) (+1e-16), attention dropout
  * keyed on (seed, i, j, k).  Backward, given dz [n, h] (dout = dz): writes the
- * dQ | dK | dV blocks of dqkv; stats = caller scratch of n*3*heads floats. */
+ * dQ | dK | dV blocks of dqkv.  The forward optionally writes the per-head
+ * aggregates yh [n, heads*h] and the softmax state into stats (n*3*heads
+ * floats); the backward needs both. */
 int mignn_transformer_train_forward(const int32_t* row_ptr, const int32_t* col, const float* qkv,
                                     int64_t ldq, const float* x, int64_t ldx, int64_t n, int h,
                                     int heads, float score_scale, float p, uint64_t seed,
-                                    float* out, int64_t ldo, void* stream);
+                                    float* out, int64_t ldo, float* yh, int64_t ldyh,
+                                    float* stats, void* stream);
 int mignn_transformer_train_backward(const int32_t* row_ptr, const int32_t* col,
                                      const int32_t* rowt_ptr, const int32_t* colt,
                                      const float* qkv, int64_t ldq, const float* dz, int64_t lddz,
-                                     int64_t n, int h, int heads, float score_scale, float p,
+                                     const float* yh, int64_t ldyh, int64_t n, int h, int heads, float score_scale, float p,
                                      uint64_t seed, float* stats, float* dqkv, int64_t ldd,
                                      void* stream);
 
