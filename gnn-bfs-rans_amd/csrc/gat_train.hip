@@ -73,6 +73,11 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 __device__ __forceinline__ float leaky(float s, float slope) { return s > 0.f ? s : s * slope; }
 
+constexpr int kMaxHeads = 8;
+
+// All heads in one pass over the row: the scalar softmax state of every head
+// first (logit rows only, [2*heads] floats per node), then each neighbour row
+// x_j is read once and feeds all heads' accumulators.
 template <int VPL>
 __global__ __launch_bounds__(256) void gat_fwd_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -84,39 +89,65 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(
     if (i >= n) return;
     const int beg = row_ptr[i], end = row_ptr[i + 1];
     const int ldl = 2 * heads;
-    for (int k = 0; k < heads; ++k) {
-        const float ad = logits[i * ldl + heads + k];
-        float m = -INFINITY;
-        for (int e = beg; e < end; ++e) m = fmaxf(m, leaky(logits[int64_t(col[e]) * ldl + k] + ad, slope));
-        float s = 0.f;
-        for (int e = beg; e < end; ++e)
-            s += expf(leaky(logits[int64_t(col[e]) * ldl + k] + ad, slope) - m);
-        const float inv = 1.f / (s + 1e-16f);
-        if (stats && lane == 0) {   // softmax state for the backward
-            stats[i * 3 * heads + k] = m;
-            stats[i * 3 * heads + heads + k] = inv;
-        }
-        float acc[VPL];
+    float ad[kMaxHeads], m[kMaxHeads], inv[kMaxHeads], acc[kMaxHeads][VPL];
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) acc[v] = 0.f;
-        for (int e = beg; e < end; ++e) {
-            const int64_t j = col[e];
-            const float a = expf(leaky(logits[j * ldl + k] + ad, slope) - m) * inv * drop.keep(i, j, k);
+    for (int k = 0; k < kMaxHeads; ++k) {
+        ad[k] = k < heads ? logits[i * ldl + heads + k] : 0.f;
+        m[k] = -INFINITY;
+        inv[k] = 0.f;
 #pragma unroll
-            for (int v = 0; v < VPL; ++v) {
-                const int c = lane + 64 * v;
-                if (c < h) acc[v] += a * x[j * ldx + c];
-            }
+        for (int v = 0; v < VPL; ++v) acc[k][v] = 0.f;
+    }
+    for (int e = beg; e < end; ++e) {
+        const int64_t j = col[e];
+#pragma unroll
+        for (int k = 0; k < kMaxHeads; ++k)
+            if (k < heads) m[k] = fmaxf(m[k], leaky(logits[j * ldl + k] + ad[k], slope));
+    }
+    for (int e = beg; e < end; ++e) {
+        const int64_t j = col[e];
+#pragma unroll
+        for (int k = 0; k < kMaxHeads; ++k)
+            if (k < heads) inv[k] += expf(leaky(logits[j * ldl + k] + ad[k], slope) - m[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxHeads; ++k) {
+        inv[k] = 1.f / (inv[k] + 1e-16f);
+        if (k < heads && stats && lane == 0) {   // softmax state for the backward
+            stats[i * 3 * heads + k] = m[k];
+            stats[i * 3 * heads + heads + k] = inv[k];
         }
+    }
+    for (int e = beg; e < end; ++e) {
+        const int64_t j = col[e];
+        float xv[VPL];
 #pragma unroll
         for (int v = 0; v < VPL; ++v) {
             const int c = lane + 64 * v;
-            if (c < h) y[i * ldy + int64_t(k) * h + c] = acc[v];
+            xv[v] = c < h ? x[j * ldx + c] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxHeads; ++k) {
+            if (k >= heads) break;
+            const float a = expf(leaky(logits[j * ldl + k] + ad[k], slope) - m[k]) * inv[k] *
+                            drop.keep(i, j, k);
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) acc[k][v] += a * xv[v];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxHeads; ++k) {
+        if (k >= heads) break;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+            const int c = lane + 64 * v;
+            if (c < h) y[i * ldy + int64_t(k) * h + c] = acc[k][v];
         }
     }
 }
 
-// rows (destinations) of the forward CSR: softmax state + dlogits[:, heads + k]
+// rows (destinations) of the forward CSR: dlogits[:, heads + k], head by head
+// (a head-fused variant held 4 x VPL gradients in VGPRs and ran slower)
 template <int VPL>
 __global__ __launch_bounds__(256) void gat_bwd_rows_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
