@@ -252,30 +252,47 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(RedArgs p, int64_t n, i
     }
 }
 
-__device__ __forceinline__ void sum_partials(const double* partial, int nblk, int h, int c,
-                                             double* s1, double* s2) {
-    double a = 0.0, b = 0.0;
-    for (int k = 0; k < nblk; ++k) {
-        a += partial[(static_cast<int64_t>(k) * 2) * h + c];
-        b += partial[(static_cast<int64_t>(k) * 2 + 1) * h + c];
-    }
-    *s1 = a;
-    *s2 = b;
-}
 
 // BN batch statistics (torch BatchNorm1d training: biased variance for the
 // normalisation, unbiased for running_var, running = (1-m)*running + m*batch)
-__global__ void bn_stats_finalize_kernel(const double* __restrict__ partial, int nblk, int64_t n,
+// one 256-thread block per column: the block's threads take the partials
+// k = tid, tid + 256, ... and a fixed-shape LDS tree sums them (deterministic;
+// the one-thread-per-column loop over up to 512 partials was latency-bound)
+__device__ __forceinline__ void block_sum_partials(const double* partial, int nblk, int h, int c,
+                                                   double* s1, double* s2) {
+    __shared__ double r1[256], r2[256];
+    const int tid = threadIdx.x;
+    double a = 0.0, b = 0.0;
+    for (int k = tid; k < nblk; k += 256) {
+        a += partial[(static_cast<int64_t>(k) * 2) * h + c];
+        b += partial[(static_cast<int64_t>(k) * 2 + 1) * h + c];
+    }
+    r1[tid] = a;
+    r2[tid] = b;
+    __syncthreads();
+#pragma unroll
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) {
+            r1[tid] += r1[tid + w];
+            r2[tid] += r2[tid + w];
+        }
+        __syncthreads();
+    }
+    *s1 = r1[0];
+    *s2 = r2[0];
+}
+
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ partial, int nblk, int64_t n,
                                          int h, float eps, float momentum,
                                          float* __restrict__ mean, float* __restrict__ invstd,
                                          float* __restrict__ running_mean,
                                          float* __restrict__ running_var,
                                          int64_t* __restrict__ num_batches) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c == 0 && num_batches != nullptr) *num_batches += 1;
-    if (c >= h) return;
+    const int c = blockIdx.x;   // one block per column
     double s1, s2;
-    sum_partials(partial, nblk, h, c, &s1, &s2);
+    block_sum_partials(partial, nblk, h, c, &s1, &s2);
+    if (threadIdx.x != 0) return;
+    if (c == 0 && num_batches != nullptr) *num_batches += 1;
     const double mu = s1 / n;
     double var = s2 / n - mu * mu;
     if (var < 0.0) var = 0.0;
@@ -289,12 +306,13 @@ __global__ void bn_stats_finalize_kernel(const double* __restrict__ partial, int
 }
 
 // out1[c] = float(sum1), out2[c] = float(sum2) (either may be NULL)
-__global__ void sums_finalize_kernel(const double* __restrict__ partial, int nblk, int h,
-                                     float* __restrict__ out1, float* __restrict__ out2) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= h) return;
+__global__ __launch_bounds__(256) void sums_finalize_kernel(
+    const double* __restrict__ partial, int nblk, int h, float* __restrict__ out1,
+    float* __restrict__ out2) {
+    const int c = blockIdx.x;   // one block per column
     double s1, s2;
-    sum_partials(partial, nblk, h, c, &s1, &s2);
+    block_sum_partials(partial, nblk, h, c, &s1, &s2);
+    if (threadIdx.x != 0) return;
     if (out1) out1[c] = static_cast<float>(s1);
     if (out2) out2[c] = static_cast<float>(s2);
 }
@@ -346,12 +364,22 @@ struct LossW {
     float w[8];
 };
 
-__global__ void wmse_finalize_kernel(const double* __restrict__ partial, int nblk, int64_t n,
+__global__ __launch_bounds__(256) void wmse_finalize_kernel(const double* __restrict__ partial, int nblk, int64_t n,
                                      int ncol, LossW wt, float prw, int fieldwise,
                                      float* __restrict__ loss, double* __restrict__ stats) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double sq[8], df[8];
-    for (int c = 0; c < 7; ++c) sum_partials(partial, nblk, ncol, c, &sq[c], &df[c]);
+    __shared__ double s_sq[8], s_df[8];
+    for (int c = 0; c < 7; ++c) {   // block-parallel, fixed-order column sums
+        double a, b;
+        block_sum_partials(partial, nblk, ncol, c, &a, &b);
+        if (threadIdx.x == 0) {
+            s_sq[c] = a;
+            s_df[c] = b;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const double* sq = s_sq;
+    const double* df = s_df;
     const double dn = static_cast<double>(n);
     double L;
     if (fieldwise) {
@@ -472,7 +500,7 @@ extern "C" int mignn_col_sums(const float* x, int64_t ldx, int64_t n, int h, flo
     hipLaunchKernelGGL(col_reduce_kernel<RED_MOMENTS>, dim3(nb), dim3(256), 0, st, p, n, h, part);
     int rc = launch_status("col_reduce_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(sums_finalize_kernel, dim3((h + 255) / 256), dim3(256), 0, st, part, nb, h,
+    hipLaunchKernelGGL(sums_finalize_kernel, dim3(h), dim3(256), 0, st, part, nb, h,
                        sums, (float*)nullptr);
     return launch_status("sums_finalize_kernel");
 }
@@ -496,7 +524,7 @@ extern "C" int mignn_bn_train_stats(const float* z, int64_t ldz, int64_t n, int 
     hipLaunchKernelGGL(col_reduce_kernel<RED_MOMENTS>, dim3(nb), dim3(256), 0, st, p, n, h, part);
     int rc = launch_status("col_reduce_kernel");
     if (rc) return rc;
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((h + 255) / 256), dim3(256), 0, st, part,
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(h), dim3(256), 0, st, part,
                        nb, n, h, eps, momentum, mean, invstd, running_mean, running_var,
                        num_batches_tracked);
     return launch_status("bn_stats_finalize_kernel");
@@ -547,7 +575,7 @@ extern "C" int mignn_bn_act_backward(const float* dout, int64_t ldd, const float
                            part);
         int rc = launch_status("col_reduce_kernel<BN_BWD>");
         if (rc) return rc;
-        hipLaunchKernelGGL(sums_finalize_kernel, dim3((h + 255) / 256), dim3(256), 0, st, part,
+        hipLaunchKernelGGL(sums_finalize_kernel, dim3(h), dim3(256), 0, st, part,
                            nb, h, dbeta, dgamma);
         if ((rc = launch_status("sums_finalize_kernel"))) return rc;
     }
@@ -578,7 +606,7 @@ extern "C" int mignn_wmse_loss(const float* pred, int64_t ldp, const float* tgt,
     if (rc) return rc;
     LossW w{};
     for (int c = 0; c < 7; ++c) w.w[c] = weights[c];
-    hipLaunchKernelGGL(wmse_finalize_kernel, dim3(1), dim3(64), 0, st, part, nb, n, ncol, w, prw,
+    hipLaunchKernelGGL(wmse_finalize_kernel, dim3(1), dim3(256), 0, st, part, nb, n, ncol, w, prw,
                        fieldwise, loss, stats);
     return launch_status("wmse_finalize_kernel");
 }
