@@ -195,7 +195,7 @@ Drop make_drop(float p, uint64_t seed) {
 // ------------------------------------------------------- column reductions
 enum { RED_MOMENTS = 0, RED_BN_BWD = 1, RED_SQDIFF = 2 };
 constexpr int RED_CC = 8;          // h <= 64 * RED_CC
-constexpr int RED_MAX_BLOCKS = 512;
+constexpr int RED_MAX_BLOCKS = 2048;   // 8 blocks (32 waves) per CU to hide the row loads
 
 struct RedArgs {
     const float* a; int64_t lda;   // MOMENTS: x; BN_BWD: dout; SQDIFF: pred
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(RedArgs p, int64_t n, i
 // normalisation, unbiased for running_var, running = (1-m)*running + m*batch)
 // one 256-thread block per column: the block's threads take the partials
 // k = tid, tid + 256, ... and a fixed-shape LDS tree sums them (deterministic;
-// the one-thread-per-column loop over up to 512 partials was latency-bound)
+// the one-thread-per-column loop over the partials was latency-bound)
 __device__ __forceinline__ void block_sum_partials(const double* partial, int nblk, int h, int c,
                                                    double* s1, double* s2) {
     __shared__ double r1[256], r2[256];
