@@ -32,38 +32,6 @@ namespace {
 
 constexpr int kWaves = 4;   // rows per 256-thread block
 
-__device__ __forceinline__ uint32_t edge_hash(uint64_t seed, uint64_t idx) {
-    uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;   // splitmix64
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return static_cast<uint32_t>(z >> 32);
-}
-
-struct EdgeDrop {
-    uint64_t seed;
-    uint32_t thresh;   // drop if hash < thresh (0: no dropout)
-    float scale;       // 1 / (1 - p); 0 when p >= 1
-    int64_t n;
-    int heads;
-    __device__ __forceinline__ float keep(int64_t i, int64_t j, int k) const {
-        if (thresh == 0u) return scale;
-        const uint64_t idx = (static_cast<uint64_t>(i) * n + j) * heads + k;
-        return edge_hash(seed, idx) >= thresh ? scale : 0.f;
-    }
-};
-
-EdgeDrop make_edge_drop(float p, uint64_t seed, int64_t n, int heads) {
-    EdgeDrop d{seed, 0u, 1.f, n, heads};
-    if (p >= 1.f) {
-        d.thresh = 0xFFFFFFFFu;
-        d.scale = 0.f;
-    } else if (p > 0.f) {
-        d.thresh = static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
-        d.scale = 1.f / (1.f - p);
-    }
-    return d;
-}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
