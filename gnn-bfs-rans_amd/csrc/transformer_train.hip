@@ -44,6 +44,15 @@ __device__ __forceinline__ void load_row(const float* __restrict__ p, int lane, 
     }
 }
 
+// two independent wave reductions with their shuffle chains interleaved
+__device__ __forceinline__ void wave_sum2(float& a, float& b) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+}
+
 template <int VPL>
 __device__ __forceinline__ float dot_row(const float (&a)[VPL], const float* __restrict__ p, int lane,
                                          int h) {
@@ -147,15 +156,21 @@ __global__ __launch_bounds__(256) void tf_bwd_rows_kernel(
         for (int u = 0; u < VPL; ++u) dq[u] = 0.f;
         for (int e = beg; e < end; ++e) {
             const int64_t j = col[e];
-            const float* kj = t.kk(j, k);
-            const float alpha = expf(dot_row<VPL>(q, kj, lane, h) * scale - m) * inv;
-            const float da = dot_row<VPL>(dy, t.v(j, k), lane, h) * drop.keep(i, j, k);
-            const float ds = alpha * (da - cs) * scale;
+            float kv[VPL], vv[VPL];
+            load_row<VPL>(t.kk(j, k), lane, h, kv);
+            load_row<VPL>(t.v(j, k), lane, h, vv);
+            float d1 = 0.f, d2 = 0.f;
 #pragma unroll
             for (int u = 0; u < VPL; ++u) {
-                const int c = lane + 64 * u;
-                if (c < h) dq[u] += ds * kj[c];
+                d1 += q[u] * kv[u];
+                d2 += dy[u] * vv[u];
             }
+            wave_sum2(d1, d2);
+            const float alpha = expf(d1 * scale - m) * inv;
+            const float da = d2 * drop.keep(i, j, k);
+            const float ds = alpha * (da - cs) * scale;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) dq[u] += ds * kv[u];
         }
 #pragma unroll
         for (int u = 0; u < VPL; ++u) {
@@ -184,23 +199,28 @@ __global__ __launch_bounds__(256) void tf_bwd_cols_kernel(
         for (int u = 0; u < VPL; ++u) dk[u] = dv[u] = 0.f;
         for (int e = beg; e < end; ++e) {
             const int64_t i = colt[e];
-            const float* qi = t.q(i, k);
-            const float* gi = dz + i * lddz;
+            float qv[VPL], gv[VPL];
+            load_row<VPL>(t.q(i, k), lane, h, qv);
+            load_row<VPL>(dz + i * lddz, lane, h, gv);
             const float m = stats[i * 3 * heads + k];
             const float inv = stats[i * 3 * heads + heads + k];
             const float cs = stats[i * 3 * heads + 2 * heads + k];
-            const float alpha = expf(dot_row<VPL>(kj, qi, lane, h) * scale - m) * inv;
+            float d1 = 0.f, d2 = 0.f;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+                d1 += kj[u] * qv[u];
+                d2 += vj[u] * gv[u];
+            }
+            wave_sum2(d1, d2);
+            const float alpha = expf(d1 * scale - m) * inv;
             const float kp = drop.keep(i, j, k);
-            const float da = dot_row<VPL>(vj, gi, lane, h) * hinv * kp;
+            const float da = d2 * hinv * kp;
             const float ds = alpha * (da - cs) * scale;
             const float wv = alpha * kp * hinv;
 #pragma unroll
             for (int u = 0; u < VPL; ++u) {
-                const int c = lane + 64 * u;
-                if (c < h) {
-                    dv[u] += wv * gi[c];
-                    dk[u] += ds * qi[c];
-                }
+                dv[u] += wv * gv[u];
+                dk[u] += ds * qv[u];
             }
         }
 #pragma unroll
