@@ -92,9 +92,7 @@ __global__ __launch_bounds__(256) void tf_fwd_kernel(
         float m = -INFINITY, s = 0.f;
 #pragma unroll
         for (int u = 0; u < VPL; ++u) acc[u] = 0.f;
-        for (int e = beg; e < end; ++e) {   // online softmax
-            const int64_t j = col[e];
-            const float sc = dot_row<VPL>(q, t.kk(j, k), lane, h) * scale;
+        auto step = [&](int64_t j, float sc) {   // online softmax, edge order
             if (sc > m) {
                 const float r = expf(m - sc);
                 s *= r;
@@ -111,7 +109,24 @@ __global__ __launch_bounds__(256) void tf_fwd_kernel(
                 const int c = lane + 64 * u;
                 if (c < h) acc[u] += wk * vj[c];
             }
+        };
+        int e = beg;
+        for (; e + 1 < end; e += 2) {   // two scores per pass: interleaved reductions
+            const int64_t j0 = col[e], j1 = col[e + 1];
+            float k0[VPL], k1[VPL];
+            load_row<VPL>(t.kk(j0, k), lane, h, k0);
+            load_row<VPL>(t.kk(j1, k), lane, h, k1);
+            float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+            for (int u = 0; u < VPL; ++u) {
+                d0 += q[u] * k0[u];
+                d1 += q[u] * k1[u];
+            }
+            wave_sum2(d0, d1);
+            step(j0, d0 * scale);
+            step(j1, d1 * scale);
         }
+        if (e < end) step(col[e], dot_row<VPL>(q, t.kk(col[e], k), lane, h) * scale);
         const float inv = 1.f / (s + 1e-16f);
 #pragma unroll
         for (int u = 0; u < VPL; ++u) {
