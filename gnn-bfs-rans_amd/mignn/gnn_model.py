@@ -25,8 +25,9 @@ fp16 MFMAs on power-of-two-scaled hi/lo splits of both operands with fp32
 accumulation (relative error per product ~2^-22, 16x the f32 MFMA rate),
 where a kernel exists for the shape (fused GCN layer, H in {64, 128}); the
 measured field error stays well inside the north star's 1e-5 either way.  There is no CPU path: tensors must be on a
-ROCm device and the library must be built.  Eval mode only (training /
-backward is SURVEY.md §8f-3, not built yet).
+ROCm device and the library must be built.  model.train() runs the
+training path (mignn.train_ops): exact-fp32 kernels with
+batch-statistics BN, dropout and a HIP backward for every layer type.
 
 Weight re-association (one-time per weight version, float64 on the device):
 * GAT: logits a_src = x . (W_h^T att_src_h) -> an [N, 2*heads] GEMV-GEMM;
@@ -405,13 +406,6 @@ class FlowGNN(nn.Module):
 
     # ------------------------------------------------------------- internals
     def _check_runtime(self, x, edge_index):
-        if self.training and self.layer_type not in ("GCN", "GIN", "GAT", "Transformer"):
-            raise NotImplementedError(
-                f"mignn FlowGNN trains the GCN, GIN and GAT layer types (GCN is train.py's "
-                f"default); "
-                f"model.train() "
-                f"with layer_type={self.layer_type!r} is not implemented -- call .eval() for "
-                "the forward.")
         if x.device.type != "cuda" or edge_index.device.type != "cuda":
             raise RuntimeError(
                 "mignn FlowGNN runs on ROCm devices only (no CPU path): move the model and the "
