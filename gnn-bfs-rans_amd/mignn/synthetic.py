@@ -12,18 +12,29 @@
 
 from __future__ import annotations
 
+import math
 from typing import Dict, Optional, Tuple
 
 import torch
 
 
-def seeded_state_dict(template: Dict[str, torch.Tensor], seed: int = 0) -> Dict[str, torch.Tensor]:
+def seeded_state_dict(template: Dict[str, torch.Tensor], seed: int = 0,
+                      scale: str = "fan_in") -> Dict[str, torch.Tensor]:
     """Return a new state_dict with the same keys/shapes as `template`.
 
-    Linear weights/biases and attention vectors ~ U(-0.1, 0.1); BatchNorm
-    weight ~ U(0.5, 1.5), bias ~ U(-0.1, 0.1), running_mean ~ N(0, 0.1^2),
-    running_var ~ U(0.5, 1.5); GIN `eps` and `num_batches_tracked` are kept.
+    scale="fan_in" (default): matrix weights ~ U(-a, a) with a = sqrt(6 / fan_in)
+    (He-uniform, the scale of a trained ReLU network: activations and outputs
+    stay O(1) through the layers, so an absolute error bound bites);
+    attention vectors [1, heads, C] ~ U(-a, a) with a = sqrt(3 / C); biases
+    ~ U(-0.1, 0.1); GIN's first Linear (`nn.0`, fed a sum over deg + 1 rows,
+    not a mean) 1/8 of that, or deep GIN stacks grow without bound.  scale="uniform": every weight, bias and attention vector
+    ~ U(-0.1, 0.1) (SURVEY.md §8d's original draw; near-constant outputs).
+    Both: BatchNorm weight ~ U(0.5, 1.5), bias ~ U(-0.1, 0.1), running_mean
+    ~ N(0, 0.1^2), running_var ~ U(0.5, 1.5); GIN `eps` and
+    `num_batches_tracked` are kept.
     """
+    if scale not in ("fan_in", "uniform"):
+        raise ValueError(f"scale must be 'fan_in' or 'uniform', got {scale!r}")
     g = torch.Generator().manual_seed(seed)
     out = {}
     for k, t in template.items():
@@ -38,7 +49,15 @@ def seeded_state_dict(template: Dict[str, torch.Tensor], seed: int = 0) -> Dict[
         elif ".module.weight" in k and k.startswith("batch_norms"):
             v = torch.rand(shape, generator=g) + 0.5
         else:
-            v = (torch.rand(shape, generator=g) * 2 - 1) * 0.1
+            u = torch.rand(shape, generator=g) * 2 - 1
+            if scale == "fan_in" and len(shape) == 2:
+                v = u * math.sqrt(6.0 / shape[1])
+                if k.endswith(".nn.0.weight"):   # GIN: input is a SUM over deg+1 rows
+                    v = v / 8.0
+            elif scale == "fan_in" and len(shape) == 3:       # GAT att_src / att_dst
+                v = u * math.sqrt(3.0 / shape[2])
+            else:
+                v = u * 0.1
         out[k] = v.to(dtype)
     return out
 

@@ -35,6 +35,22 @@ int mignn_diag_gcn_layer0(int mode, const int32_t* row_ptr, const int32_t* col, 
 
 int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img, float* out,
                         void* stream);
+
+/* EXPERIMENTAL (not used by FlowGNN): the fused GCN layer of
+ * mignn_gcn_layer_f16x3 as a "tile ring" kernel (csrc/gcn_ring.hip): one
+ * 4-wave workgroup per CU walks consecutive 64-row tiles with the previous /
+ * current / next tile images in an LDS ring and the whole split W in AGPRs.
+ * Same arguments and results contract as mignn_gcn_layer_f16x3, plus
+ * seg_tiles (tiles per contiguous segment, 0 = one segment per workgroup).
+ * Measured slower than the producer/consumer kernel. */
+int mignn_gcn_layer_ring(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                         const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                         const float* w, const float* bias, const float* scale,
+                         const float* shift, int flags, float* out, int64_t ldo,
+                         int64_t seg_tiles, void* stream);
+/* Timeline buffer (uint64 [8 * 64 * 16]) for mignn_gcn_layer_ring: s_memtime
+ * of wave 0 of workgroups 0..7 at the 10 phase boundaries of steps 0..63. */
+int mignn_diag_set_trace_ring(void* buf);
 #ifdef __cplusplus
 }
 #endif

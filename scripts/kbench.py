@@ -34,13 +34,15 @@ if os.environ.get("KB_PERM"):
 if os.environ.get("KB_PANEL"):
     # 4x4x4-cell tiles; panels of PxP tile columns swept along k, tiles of a
     # panel's k-level consecutive (locality experiment)
-    pp = int(os.environ["KB_PANEL"])
+    # KB_PANEL="P" (P x P tile columns) or "PI,PJ"
+    pv = [int(v) for v in os.environ["KB_PANEL"].split(",")]
+    pi_, pj_ = (pv[0], pv[0]) if len(pv) == 1 else (pv[0], pv[1])
     ids = torch.arange(n, device=dev)
     i, j, k = ids % nx, (ids // nx) % ny, ids // (nx * ny)
     ti, tj, tk = i // 4, j // 4, k // 4
     ntk = (nz + 3) // 4
-    npi = ((nx + 3) // 4 + pp - 1) // pp
-    key = (((((tj // pp) * npi + ti // pp) * ntk + tk) * pp + tj % pp) * pp + ti % pp) * 64 \
+    npi = ((nx + 3) // 4 + pi_ - 1) // pi_
+    key = (((((tj // pj_) * npi + ti // pi_) * ntk + tk) * pj_ + tj % pj_) * pi_ + ti % pi_) * 64 \
         + (k % 4) * 16 + (j % 4) * 4 + i % 4
     pos = torch.empty_like(ids)
     pos[torch.argsort(key, stable=True)] = ids
@@ -90,9 +92,21 @@ def gcn(flags):
                                  P(b), P(sc), P(sh), flags, P(Y), H, st), "gcn")
 
 
+XFLAGS = int(os.environ.get("KB_XFLAGS", "0"))
+
+
 def gcn16(flags):
+    flags |= XFLAGS
     _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                        P(W), P(b), P(sc), P(sh), flags, P(Y), H, st), "gcn16")
+
+
+SEG = int(os.environ.get("KB_SEG", "0"))
+
+
+def ring(flags):
+    _lib.check(L.mignn_gcn_layer_ring(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                      P(W), P(b), P(sc), P(sh), flags, P(Y), H, SEG, st), "ring")
 
 
 def agg(_):
@@ -166,7 +180,7 @@ def diag(mode_blocks):
 
 
 cases = {
-    "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_chunks": (gcn16, 15 | 65536), "gcn16_no_produce": (gcn16, 15 | 256),
+    "ring": (ring, 15), "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_chunks": (gcn16, 15 | 65536), "gcn16_no_produce": (gcn16, 15 | 256),
     "gcn16_no_mfma": (gcn16, 15 | 512), "gcn16_no_ext": (gcn16, 15 | 4096),
     "gcn16_no_tables_ext": (gcn16, 15 | 4096 | 16384),
     "gcn16_plain": (gcn16, 15 | 32768), "gcn16_no_produce_plain": (gcn16, 15 | 256 | 32768),
@@ -228,6 +242,23 @@ if os.environ.get("KB_TRACE"):
          "c_epilogue": t[:, 1:60, 7] - t[:, 1:60, 6],
          "step": t[:, 2:61, 0] - t[:, 1:60, 0]}
     res["trace_cycles_median"] = {k: float(v.median()) for k, v in d.items()}
+if os.environ.get("KB_RTRACE"):
+    buf = torch.zeros(8 * 64 * 16, dtype=torch.int64, device=dev)
+    L.mignn_diag_set_trace_ring.argtypes = [_lib.c_void_p] if hasattr(_lib, "c_void_p") else None
+    import ctypes
+    L.mignn_diag_set_trace_ring.argtypes = [ctypes.c_void_p]
+    _lib.check(L.mignn_diag_set_trace_ring(P(buf)), "rtrace")
+    ring(15)
+    torch.cuda.synchronize()
+    _lib.check(L.mignn_diag_set_trace_ring(None), "rtrace")
+    t = buf.view(8, 64, 16).cpu().double()
+    names = ["idx", "dma", "decode", "ring_loop", "ext_sum", "split_seed", "mfma", "epilogue",
+             "issue_ext", "barrier"]
+    res["ring_trace_cycles_median"] = {}
+    for k in range(9):
+        res["ring_trace_cycles_median"][names[k]] = float((t[:, 2:60, k + 1] - t[:, 2:60, k]).median())
+    res["ring_trace_cycles_median"]["barrier"] = float((t[:, 3:61, 0] - t[:, 2:60, 9]).median())
+    res["ring_trace_cycles_median"]["step"] = float((t[:, 3:61, 0] - t[:, 2:60, 0]).median())
 if os.environ.get("KB_CHECK_HEAD"):
     head16(0)
     torch.cuda.synchronize()
@@ -247,6 +278,9 @@ if os.environ.get("KB_CHECK"):
     Y16 = torch.full_like(X, float("nan"))
     _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                        P(W), P(b), P(sc), P(sh), 15, P(Y16), H, st), "gcn16")
+    YR = torch.full_like(X, float("nan"))
+    _lib.check(L.mignn_gcn_layer_ring(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                      P(W), P(b), P(sc), P(sh), 15, P(YR), H, SEG, st), "ring")
     torch.cuda.synchronize()
     rows = torch.randint(0, n, (4096,), generator=torch.Generator().manual_seed(5))
     rp = csr.row_ptr.cpu().long()
@@ -273,6 +307,9 @@ if os.environ.get("KB_CHECK"):
     res["check"] = {"f32_vs_ref_max": (Y32[rr].double() - Yr).abs().max().item(),
                     "f16x3_vs_ref_max": (Y16[rr].double() - Yr).abs().max().item(),
                     "f16x3_vs_f32_max": (Y16 - Y32).abs().max().item(),
+                    "ring_vs_ref_max": (YR[rr].double() - Yr).abs().max().item(),
+                    "ring_vs_f32_max": (YR - Y32).abs().max().item(),
+                    "ring_nan_rows": int(torch.isnan(YR).any(1).sum().item()),
                     "f16x3_nan_rows": int(torch.isnan(Y16).any(1).sum().item()),
                     "f32_max": Y32.abs().max().item(), "X_max": X.abs().max().item()}
 print(json.dumps({"grid": [nx, ny, nz], "H": H, "ms": res}))

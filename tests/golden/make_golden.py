@@ -15,7 +15,10 @@ normalization.py -- and runs it:
 Outputs (all small, committed):
   bfs_graphs.npz       reference-built train-path / inference-path graphs
   models.npz           seeded state_dicts + forward outputs (fp32 wrapper run,
-                       fp64 oracle run) for every parity configuration
+                       fp64 oracle run, the fp32 run's own error) for every
+                       parity configuration, configs[1..4]'s models included
+  surrogate.npz        the reference's FlowGNNSurrogate (encoder -> + boundary
+                       conditions -> decoder), with and without bc
   tiny_graphs.npz      hand-checkable edge cases, all four layer types
   normalizer.json      FieldNormalizer.fit stats over time dirs 0/100/200/282
 
@@ -106,13 +109,21 @@ def main():
         json.dump(js, fh, indent=1)
 
     # --- model configurations ---
+    # weights: seeded_state_dict(scale="fan_in") -- He-uniform matrices, so
+    # activations and outputs are O(1)..O(10) and the 1e-5 bound bites
+    # (a U(-0.1, 0.1) draw gave near-constant outputs of |y| < 0.13)
     configs = {
         "c1_gcn_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GCN"),
         "c2_gcn_h128_l4": dict(hidden_dim=128, num_layers=4, layer_type="GCN"),
+        "gcn_h256_l4": dict(hidden_dim=256, num_layers=4, layer_type="GCN"),
         "gat_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GAT"),
-        "gat_h128_l4": dict(hidden_dim=128, num_layers=4, layer_type="GAT"),
+        "gat_h128_l4": dict(hidden_dim=128, num_layers=4, layer_type="GAT"),          # configs[2] model
         "gin_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="GIN"),
+        "gin_h128_l4": dict(hidden_dim=128, num_layers=4, layer_type="GIN"),
+        "gin_h256_l8": dict(hidden_dim=256, num_layers=8, layer_type="GIN"),          # configs[4] model
         "transformer_h64_l2": dict(hidden_dim=64, num_layers=2, layer_type="Transformer"),
+        "transformer_h128_l4": dict(hidden_dim=128, num_layers=4, layer_type="Transformer"),
+        "transformer_h256_l6": dict(hidden_dim=256, num_layers=6, layer_type="Transformer"),  # configs[3]
     }
     out = {}
     torch.manual_seed(0)
@@ -123,8 +134,7 @@ def main():
         model.load_state_dict(sd)
         model.eval()
         for gname, g in (("train", g_train), ("infer", g_inf)):
-            if gname == "infer" and cfg["layer_type"] not in ("GCN", "GIN") or \
-               gname == "infer" and cfg["hidden_dim"] != 64:
+            if gname == "infer" and cfg["hidden_dim"] != 64:
                 continue
             ea = None if cfg["layer_type"] == "Transformer" else g.edge_attr
             with torch.no_grad():
@@ -135,9 +145,13 @@ def main():
             d_64 = (y32.double() - y64).abs().max().item()
             print(f"{name:22s} {gname}: |ref-wrapper - oracle32| {d_wrap:.3e}  "
                   f"|fp32 - fp64| {d_64:.3e}  absmax {y64.abs().max().item():.3f}")
-            assert d_wrap <= 1e-6, "wrapper restatement drifted from reference wrapper"
+            assert d_wrap <= 1e-6 * max(1.0, y64.abs().max().item()), \
+                "wrapper restatement drifted from reference wrapper"
             out[f"{name}/{gname}/y32"] = y32.numpy()
             out[f"{name}/{gname}/y64"] = y64.numpy()
+            # the reference's own fp32 CPU error vs fp64: the parity yardstick
+            # for deep configs whose outputs reach O(10) (fp32 ulp ~1e-6 there)
+            out[f"{name}/{gname}/ref_err"] = np.array(d_64)
         if cfg["layer_type"] == "Transformer":
             try:
                 with torch.no_grad():
@@ -151,6 +165,42 @@ def main():
             out[f"{name}/sd/{k}"] = v.numpy()
         out[f"{name}/cfg"] = np.array(json.dumps(cfg))
     np.savez_compressed(os.path.join(HERE, "models.npz"), **out)
+
+    # --- FlowGNNSurrogate (gnn_model.py:223-291): encoder -> (+ bc) -> decoder ---
+    from gnn_model import FlowGNNSurrogate
+    sur = {}
+    for si, (lt, H, L) in enumerate((("GCN", 64, 4), ("GIN", 64, 4), ("GAT", 64, 2))):
+        name = f"surrogate_{lt.lower()}_h{H}_l{L}"
+        model = FlowGNNSurrogate(input_dim=3, hidden_dim=H, num_layers=L, layer_type=lt,
+                                 dropout=0.1)
+        sd = seeded_state_dict(model.state_dict(), seed=500 + si)
+        model.load_state_dict(sd)
+        model.eval()
+        g = g_train
+        bc = (torch.rand((g.x.shape[0], H), generator=torch.Generator().manual_seed(600 + si))
+              * 2 - 1)
+        half = dict(hidden_dim=H, num_layers=L // 2, layer_type=lt)
+        enc = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
+        dec = {k[len("decoder."):]: v for k, v in sd.items() if k.startswith("decoder.")}
+        for tag, b in (("nobc", None), ("bc", bc)):
+            with torch.no_grad():
+                y32 = model(g.x, g.edge_index, g.edge_attr, boundary_conditions=b)
+            e64 = orc.flowgnn_forward(enc, half, g.x, g.edge_index, g.edge_attr,
+                                      dtype=torch.float64)
+            if b is not None:
+                e64 = e64 + b.double()
+            y64 = orc.flowgnn_forward(dec, half, e64, g.edge_index, g.edge_attr,
+                                      dtype=torch.float64)
+            d_64 = (y32.double() - y64).abs().max().item()
+            print(f"{name} {tag}: |fp32 - fp64| {d_64:.3e} absmax {y64.abs().max().item():.3f}")
+            sur[f"{name}/{tag}/y32"] = y32.numpy()
+            sur[f"{name}/{tag}/y64"] = y64.numpy()
+            sur[f"{name}/{tag}/ref_err"] = np.array(d_64)
+        sur[f"{name}/bc"] = bc.numpy()
+        for k, v in sd.items():
+            sur[f"{name}/sd/{k}"] = v.numpy()
+        sur[f"{name}/cfg"] = np.array(json.dumps(dict(hidden_dim=H, num_layers=L, layer_type=lt)))
+    np.savez_compressed(os.path.join(HERE, "surrogate.npz"), **sur)
 
     # --- tiny hand-checkable graphs, every layer type, H = 8 ---
     tiny = {

@@ -77,7 +77,7 @@ def main():
         kw.setdefault("layer_type", "GCN")
         model = FlowGNN(input_dim=3, output_dim=7, use_edge_attr=True,
                         dropout=0.0, use_batch_norm=True, **kw)
-        sd = seeded_state_dict(model.state_dict(), seed=300 + ci)
+        sd = seeded_state_dict(model.state_dict(), seed=300 + ci, scale="uniform")
         for k, v in sd.items():
             out[f"{name}/sd/{k}"] = v.numpy().copy()
         out[f"{name}/target"] = target.numpy()
