@@ -8,6 +8,7 @@
 #include <cstdio>
 
 #include "../../include/mignn.h"
+#include "../../include/mignn_diag.h"
 
 namespace mignn {
 

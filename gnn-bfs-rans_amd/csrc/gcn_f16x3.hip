@@ -842,6 +842,17 @@ extern "C" int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col,
                                      const float* w, const float* bias, const float* scale,
                                      const float* shift, int flags, float* out, int64_t ldo,
                                      void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer_f16x3: unknown flags 0x%x", flags);
+    return mignn_diag_gcn_layer_f16x3(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift,
+                                      flags, out, ldo, stream);
+}
+
+extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col,
+                                          const float* ew, const float* x, int64_t ldx,
+                                          int64_t rb, int64_t re, int h, const float* w,
+                                          const float* bias, const float* scale,
+                                          const float* shift, int flags, float* out, int64_t ldo,
+                                          void* stream) {
     MIGNN_REQUIRE(row_ptr && col && ew && x && w && out, "gcn_layer_f16x3: null pointer");
     MIGNN_REQUIRE(h == 64 || h == 128, "gcn_layer_f16x3: h must be 64 or 128 (got %d)", h);
     MIGNN_REQUIRE(aligned16(x) && aligned16(w) && aligned16(out), "gcn_layer_f16x3: unaligned");

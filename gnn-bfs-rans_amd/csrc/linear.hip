@@ -138,6 +138,16 @@ extern "C" int mignn_linear(const float* a, int64_t lda, int64_t m, int k, const
                             int64_t lda2, int k2, const float* w, int n, const float* bias,
                             const float* residual, int64_t ldr, const float* scale,
                             const float* shift, int flags, float* c, int64_t ldc, void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "linear: unknown flags 0x%x", flags);
+    return mignn_diag_linear(a, lda, m, k, a2, lda2, k2, w, n, bias, residual, ldr, scale, shift,
+                             flags, c, ldc, stream);
+}
+
+extern "C" int mignn_diag_linear(const float* a, int64_t lda, int64_t m, int k, const float* a2,
+                                 int64_t lda2, int k2, const float* w, int n, const float* bias,
+                                 const float* residual, int64_t ldr, const float* scale,
+                                 const float* shift, int flags, float* c, int64_t ldc,
+                                 void* stream) {
     MIGNN_REQUIRE(m >= 0 && k > 0 && k2 >= 0 && n > 0, "linear: bad sizes m=%lld k=%d k2=%d n=%d",
                   (long long)m, k, k2, n);
     MIGNN_REQUIRE(k % 4 == 0 && k2 % 4 == 0, "linear: k=%d k2=%d must be multiples of 4", k, k2);

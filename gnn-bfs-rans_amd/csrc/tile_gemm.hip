@@ -615,6 +615,16 @@ extern "C" int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const
                                const float* w, const float* bias, const float* scale,
                                const float* shift, int flags, float* out, int64_t ldo,
                                void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer: unknown flags 0x%x", flags);
+    return mignn_diag_gcn_layer(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift, flags,
+                                out, ldo, stream);
+}
+
+extern "C" int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                                    const float* x, int64_t ldx, int64_t rb, int64_t re, int h,
+                                    const float* w, const float* bias, const float* scale,
+                                    const float* shift, int flags, float* out, int64_t ldo,
+                                    void* stream) {
     MIGNN_REQUIRE(row_ptr && col && ew && x && w && out, "gcn_layer: null pointer");
     MIGNN_REQUIRE(aligned16(x) && aligned16(w), "gcn_layer: unaligned x / w");
     MIGNN_REQUIRE(ldx % 4 == 0 && ldx >= h && ldo >= h, "gcn_layer: bad strides");
@@ -644,6 +654,7 @@ extern "C" int mignn_gin_layer(const int32_t* row_ptr, const int32_t* col, const
                   "gin_layer: unaligned");
     MIGNN_REQUIRE(ldx % 4 == 0 && ldt % 4 == 0, "gin_layer: bad strides");
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gin_layer: affine params");
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gin_layer: unknown flags 0x%x", flags);
     MIGNN_REQUIRE(x != out && tmp != x, "gin_layer: aliasing");
     if (re == rb) return MIGNN_OK;
     if (!tile_supported(AGG_SUM, h, h)) {

@@ -292,7 +292,12 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
     double s1, s2;
     block_sum_partials(partial, nblk, h, c, &s1, &s2);
     if (threadIdx.x != 0) return;
-    if (c == 0 && num_batches != nullptr) *num_batches += 1;
+    // momentum < 0: BatchNorm1d(momentum=None), the cumulative average with
+    // factor 1 / num_batches_tracked after this batch's increment (the
+    // counter itself is bumped by bn_count_kernel after this launch, so every
+    // block reads the same pre-increment value)
+    if (momentum < 0.f)
+        momentum = 1.f / static_cast<float>((num_batches != nullptr ? *num_batches : 0) + 1);
     const double mu = s1 / n;
     double var = s2 / n - mu * mu;
     if (var < 0.0) var = 0.0;
@@ -303,6 +308,10 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
         const double unb = n > 1 ? var * n / (n - 1) : var;
         running_var[c] = (1.f - momentum) * running_var[c] + momentum * static_cast<float>(unb);
     }
+}
+
+__global__ void bn_count_kernel(int64_t* __restrict__ num_batches) {
+    if (threadIdx.x == 0) *num_batches += 1;
 }
 
 // out1[c] = float(sum1), out2[c] = float(sum2) (either may be NULL)
@@ -527,7 +536,10 @@ extern "C" int mignn_bn_train_stats(const float* z, int64_t ldz, int64_t n, int 
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(h), dim3(256), 0, st, part,
                        nb, n, h, eps, momentum, mean, invstd, running_mean, running_var,
                        num_batches_tracked);
-    return launch_status("bn_stats_finalize_kernel");
+    rc = launch_status("bn_stats_finalize_kernel");
+    if (rc || num_batches_tracked == nullptr) return rc;
+    hipLaunchKernelGGL(bn_count_kernel, dim3(1), dim3(64), 0, st, num_batches_tracked);
+    return launch_status("bn_count_kernel");
 }
 
 extern "C" int mignn_bn_act_forward(const float* z, int64_t ldz, int64_t n, int h,

@@ -44,8 +44,6 @@ SIGNATURES = {
                                 c_int, _P, c_int64, _P]),
     "mignn_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                       _P, _P, c_int, _P, c_int64, _P]),
-    "mignn_gcn_layer_ring": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
-                                     _P, _P, c_int, _P, c_int64, c_int64, _P]),
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
     "mignn_mlp_head_prep": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int, c_int, _P, c_size_t,
                                     _P]),
@@ -121,6 +119,15 @@ DIAG_SIGNATURES = {
     "mignn_diag_gcn_layer0": (c_int, [c_int, _P, _P, _P, _P, c_int64, _P, _P, _P]),
     "mignn_diag_clock": (c_int, [c_int, c_int, _P, _P]),
     "mignn_diag_mlp_head": (c_int, [c_int, _P, c_int64, _P, _P, _P]),
+    "mignn_gcn_layer_ring": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
+                                     _P, _P, c_int, _P, c_int64, c_int64, _P]),
+    "mignn_diag_set_trace_ring": (c_int, [_P]),
+    "mignn_diag_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P,
+                                     _P, c_int, _P, c_int64, _P]),
+    "mignn_diag_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
+                                           _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_diag_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,
+                                  _P, c_int64, _P, _P, c_int, _P, c_int64, _P]),
 }
 
 _lib = None

@@ -128,13 +128,14 @@ class Csr:
     ids inside the CSR are the internal ids: internal row p is caller node
     perm[p], caller node v is internal row inv[v]."""
     __slots__ = ("row_ptr", "col", "dinv", "ew", "info", "num_nodes", "num_edges", "edge_index",
-                 "perm", "inv", "pos")
+                 "perm", "inv", "pos", "key_tensor")
 
     def __init__(self, row_ptr, col, dinv, info, num_nodes, num_edges, edge_index, ew=None):
         self.row_ptr, self.col, self.dinv, self.info = row_ptr, col, dinv, info
         self.num_nodes, self.num_edges, self.edge_index = num_nodes, num_edges, edge_index
         self.ew = ew
         self.perm = self.inv = self.pos = None
+        self.key_tensor = None   # the caller's edge_index the cache key was made from
 
     def compute_gcn_weights(self, row_begin: int = 0, row_end: Optional[int] = None):
         """Per-entry PyG gcn_norm weights (mignn_gcn_norm); call again after the
@@ -201,8 +202,8 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int,
 class _CsrCache:
     """Keyed by (edge_index storage, version, shape, N, mode, device) -- plus
     the positions' storage / version when a locality order is requested;
-    holds references to the keyed tensors so their storage cannot be recycled
-    while cached."""
+    holds references to the keyed tensors themselves (Csr.key_tensor,
+    Csr.pos) so their storage cannot be recycled while cached."""
 
     def __init__(self, capacity: int = 4):
         self.capacity = capacity
@@ -230,6 +231,11 @@ class _CsrCache:
         if hit is not None:
             return hit
         csr = self._build(edge_index, num_nodes, mode, pos)
+        # the key holds the caller's storage address: keep that tensor (not
+        # only the int64 copy build_csr may have made of an int32 or strided
+        # edge_index) alive so the allocator cannot hand its address to the
+        # next graph while this entry exists
+        csr.key_tensor = edge_index
         if len(self.entries) >= self.capacity:
             self.entries.pop(next(iter(self.entries)))
         self.entries[key] = csr
@@ -427,6 +433,25 @@ class FlowGNN(nn.Module):
         num_nodes = x.shape[0]
         if num_nodes == 0:
             raise ValueError("training forward on an empty graph")
+        H = self.hidden_dim
+        if self.layer_type in ("GAT", "Transformer") and H > 256:
+            raise NotImplementedError(
+                f"mignn training path: {self.layer_type} layers support hidden_dim <= 256 "
+                f"(got {H}); eval mode has no such limit")
+        if self.use_batch_norm and H > 512:
+            raise NotImplementedError(
+                f"mignn training path: BatchNorm statistics support hidden_dim <= 512 (got {H})")
+        try:
+            return self._forward_train_impl(x, edge_index, edge_attr)
+        finally:
+            # the BN kernels update running_mean / running_var in place through
+            # raw pointers (their _version does not move): drop every eval
+            # image derived from them (BN folds, layer-0 coefficients)
+            if self.use_batch_norm:
+                self._prep = {k: v for k, v in self._prep.items() if k[0] not in ("bn", "layer0")}
+
+    def _forward_train_impl(self, x, edge_index, edge_attr):
+        num_nodes = x.shape[0]
         xin = x.contiguous().float() if (x.dtype != torch.float32 or not x.is_contiguous()) else x
         mode = CSR_ONE_SELF_LOOP if self.layer_type in ("GCN", "GAT") else CSR_VERBATIM
         csr = self._csr.get(edge_index, num_nodes, mode)
@@ -484,9 +509,24 @@ class FlowGNN(nn.Module):
         return h
 
     def _layer_error(self, i, e, num_nodes, edge_index, x, edge_attr):
-        E = edge_index.shape[1]
+        """gnn_model.py:175-181, reporting the edge list the convs saw: after
+        the silent filtering of invalid indices (:133-141) and the all-invalid
+        self-loop fallback (:144-149), as the reference does."""
+        ei = edge_index
+        if ei.shape[1] > 0:
+            valid = (ei[0] >= 0) & (ei[0] < num_nodes) & (ei[1] >= 0) & (ei[1] < num_nodes)
+            if not bool(valid.all()):
+                ei = ei[:, valid]
+                if edge_attr is not None and edge_attr.shape[0] > 0:
+                    edge_attr = edge_attr[valid]
+            if ei.shape[1] == 0:
+                ei = torch.arange(num_nodes, device=ei.device).repeat(2, 1)
+                if edge_attr is not None:
+                    edge_attr = torch.zeros((num_nodes, edge_attr.shape[1]),
+                                            dtype=edge_attr.dtype, device=edge_attr.device)
+        E = ei.shape[1]
         if E > 0:
-            rng = f"[{edge_index.min().item()}, {edge_index.max().item()}]"
+            rng = f"[{ei.min().item()}, {ei.max().item()}]"
         else:
             rng = "[N/A, N/A]"
         return RuntimeError(

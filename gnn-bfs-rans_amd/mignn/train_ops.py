@@ -350,11 +350,15 @@ class _BNReluDropout(Function):
         dev = z.device
         mean = invstd = None
         if bn_mod is not None:
+            if n <= 1:   # torch.nn.functional.batch_norm's training-mode check
+                raise ValueError("Expected more than 1 value per channel when training, "
+                                 f"got input size {torch.Size([n, h])}")
             mean = torch.empty(h, dtype=torch.float32, device=dev)
             invstd = torch.empty_like(mean)
             s = _red_scratch(n, h, dev)
             track = bn_mod.track_running_stats and bn_mod.running_mean is not None
-            mom = bn_mod.momentum if bn_mod.momentum is not None else 0.0
+            # momentum=None (cumulative average, e.g. swa_utils.update_bn): -1
+            mom = bn_mod.momentum if bn_mod.momentum is not None else -1.0
             _lib.check(_lib.lib().mignn_bn_train_stats(
                 P(z), z.stride(0), n, h, float(bn_mod.eps), float(mom), P(mean), P(invstd),
                 P(bn_mod.running_mean) if track else None,

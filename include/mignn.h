@@ -100,19 +100,9 @@ enum {
     MIGNN_EPI_RESIDUAL = 2,
     MIGNN_EPI_AFFINE = 4, /* BatchNorm eval affine: v*scale + shift */
     MIGNN_EPI_RELU = 8,
-    /* diagnostic ablations of the fused tile kernels (timing studies only;
-     * results are wrong by design): skip the A-tile producer / the MFMA+store */
-    MIGNN_DIAG_NO_PRODUCE = 256,
-    MIGNN_DIAG_NO_MFMA = 512,
-    MIGNN_SCHED_XCD_MAJOR = 1024,
-    MIGNN_DIAG_TRACE = 2048,
-    MIGNN_DIAG_NO_EXT = 4096,   /* f16x3 GCN layer: skip the out-of-tile gathers */
-    MIGNN_DIAG_NO_LOCAL = 8192,  /* f16x3 GCN layer: skip the in-tile (LDS) pass */
-    MIGNN_DIAG_NO_TABLES = 16384, /* f16x3 GCN layer: skip the lookup-table build */
-    MIGNN_DIAG_PLAIN_STORE = 32768, /* f16x3 GCN layer: plain (not non-temporal) row stores */
-    /* f16x3 GCN layer tile schedule: each XCD walks a contiguous range of tiles
-     * (for CSRs in a locality order, mignn_locality_order) */
-    MIGNN_SCHED_XCD_CHUNKS = 65536
+    /* the product entry points reject any other flag bit (timing ablations
+     * live in include/mignn_diag.h, behind mignn_diag_* entry points) */
+    MIGNN_EPI_MASK = 15
 };
 int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
                  const float* a2, int64_t lda2, int k2,
@@ -343,7 +333,9 @@ int mignn_col_sums(const float* x, int64_t ldx, int64_t n, int h, float* sums, v
                    size_t scratch_bytes, void* stream);
 /* BatchNorm1d training statistics (gnn_model.py:87, 188 in model.train()):
  * batch mean / 1/sqrt(biased var + eps); running_mean/var (may be NULL)
- * updated with momentum and the unbiased variance; num_batches_tracked += 1. */
+ * updated with momentum and the unbiased variance; num_batches_tracked += 1.
+ * momentum < 0 means BatchNorm1d(momentum=None): cumulative average, factor
+ * 1 / num_batches_tracked (after the increment). */
 int mignn_bn_train_stats(const float* z, int64_t ldz, int64_t n, int h, float eps, float momentum,
                          float* mean, float* invstd, float* running_mean, float* running_var,
                          int64_t* num_batches_tracked, void* scratch, size_t scratch_bytes,

@@ -6,6 +6,36 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* Ablation / schedule flags of the fused layer kernels, OR-ed with the
+ * MIGNN_EPI_* flags; accepted only by the mignn_diag_* entry points below
+ * (the product entry points of mignn.h reject them): results are wrong by
+ * design for the NO_* ablations. */
+enum {
+    MIGNN_DIAG_NO_PRODUCE = 256,      /* skip the A-tile producer */
+    MIGNN_DIAG_NO_MFMA = 512,         /* skip the MFMA + store */
+    MIGNN_SCHED_XCD_MAJOR = 1024,     /* exact-fp32 tile kernel: XCD-major tile order */
+    MIGNN_DIAG_TRACE = 2048,          /* s_memtime timeline (mignn_diag_set_trace*) */
+    MIGNN_DIAG_NO_EXT = 4096,         /* f16x3 GCN layer: skip the out-of-tile gathers */
+    MIGNN_DIAG_NO_LOCAL = 8192,       /* f16x3 GCN layer: skip the in-tile (LDS) pass */
+    MIGNN_DIAG_NO_TABLES = 16384,     /* f16x3 GCN layer: skip the lookup-table build */
+    MIGNN_DIAG_PLAIN_STORE = 32768,   /* f16x3 GCN layer: plain (not non-temporal) stores */
+    MIGNN_SCHED_XCD_CHUNKS = 65536    /* f16x3 GCN layer: each XCD walks a contiguous tile range */
+};
+/* mignn_gcn_layer / mignn_gcn_layer_f16x3 / mignn_linear with the flags above */
+int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                         const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                         const float* w, const float* bias, const float* scale,
+                         const float* shift, int flags, float* out, int64_t ldo, void* stream);
+int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                               const float* x, int64_t ldx, int64_t row_begin, int64_t row_end,
+                               int h, const float* w, const float* bias, const float* scale,
+                               const float* shift, int flags, float* out, int64_t ldo,
+                               void* stream);
+int mignn_diag_linear(const float* a, int64_t lda, int64_t m, int k, const float* a2,
+                      int64_t lda2, int k2, const float* w, int n, const float* bias,
+                      const float* residual, int64_t ldr, const float* scale, const float* shift,
+                      int flags, float* c, int64_t ldc, void* stream);
+
 /* mode 0: CSR gather (h = 128); 1: stencil gather on the periodic grid;
  * 2: streaming copy.  blocks <= 0: one row group per row. */
 int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t* col, const float* ew,

@@ -88,7 +88,7 @@ st = _lib.stream()
 
 
 def gcn(flags):
-    _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
+    _lib.check(L.mignn_diag_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
                                  P(b), P(sc), P(sh), flags, P(Y), H, st), "gcn")
 
 
@@ -97,7 +97,7 @@ XFLAGS = int(os.environ.get("KB_XFLAGS", "0"))
 
 def gcn16(flags):
     flags |= XFLAGS
-    _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+    _lib.check(L.mignn_diag_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                        P(W), P(b), P(sc), P(sh), flags, P(Y), H, st), "gcn16")
 
 
@@ -115,7 +115,7 @@ def agg(_):
 
 
 def lin(flags):
-    _lib.check(L.mignn_linear(P(X), H, n, H, None, 0, 0, P(W), H, P(b), None, 0, None, None,
+    _lib.check(L.mignn_diag_linear(P(X), H, n, H, None, 0, 0, P(W), H, P(b), None, 0, None, None,
                               flags, P(Y), H, st), "lin")
 
 
@@ -273,10 +273,10 @@ if os.environ.get("KB_CHECK"):
     # fresh outputs: the fp32 kernel into zeros, the f16x3 kernel into NaNs; fp64
     # reference on 4096 sampled rows (CSR on the CPU)
     Y32 = torch.zeros_like(X)
-    _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
+    _lib.check(L.mignn_diag_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
                                  P(b), P(sc), P(sh), 15, P(Y32), H, st), "gcn")
     Y16 = torch.full_like(X, float("nan"))
-    _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+    _lib.check(L.mignn_diag_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                        P(W), P(b), P(sc), P(sh), 15, P(Y16), H, st), "gcn16")
     YR = torch.full_like(X, float("nan"))
     _lib.check(L.mignn_gcn_layer_ring(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,

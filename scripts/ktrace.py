@@ -34,7 +34,7 @@ _lib.check(L.mignn_diag_set_trace(P(tr)), "trace")
 for extra, name in ((0, "full"), (512, "no_mfma"), (256, "no_gather")):
     for _ in range(3):
         tr.zero_()
-        _lib.check(L.mignn_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
+        _lib.check(L.mignn_diag_gcn_layer(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(W),
                                      P(b), P(sc), P(sh), 15 | 2048 | extra, P(Y), H, st), "gcn")
         torch.cuda.synchronize()
     t = tr.view(8, 64, 8).cpu().double()

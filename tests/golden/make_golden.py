@@ -51,6 +51,21 @@ class _Data:  # stand-in for torch_geometric.data.Data (attribute bag)
             setattr(self, k, v)
 
 
+def sd_digest(sd):
+    """sha256 over the state_dict's keys and raw tensor bytes (sorted keys)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def sd_layout(sd):
+    """The reference model's state_dict layout: [[key, shape, dtype], ...] in order."""
+    return json.dumps([[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()])
+
+
 def _inject_pyg():
     pyg = types.ModuleType("torch_geometric")
     data = types.ModuleType("torch_geometric.data")
@@ -161,8 +176,11 @@ def main():
                 msg = str(e)
                 assert msg.startswith("Message passing failed in layer 0 (Transformer)"), msg
                 out[f"{name}/edge_attr_error"] = np.array(msg.split("\n")[0])
-        for k, v in sd.items():
-            out[f"{name}/sd/{k}"] = v.numpy()
+        # weights by seed (mignn.synthetic.seeded_state_dict is deterministic
+        # code in this repo) + a digest that pins them bit for bit
+        out[f"{name}/seed"] = np.array(100 + seed)
+        out[f"{name}/sd_sha256"] = np.array(sd_digest(sd))
+        out[f"{name}/sd_layout"] = np.array(sd_layout(model.state_dict()))
         out[f"{name}/cfg"] = np.array(json.dumps(cfg))
     np.savez_compressed(os.path.join(HERE, "models.npz"), **out)
 
@@ -196,9 +214,10 @@ def main():
             sur[f"{name}/{tag}/y32"] = y32.numpy()
             sur[f"{name}/{tag}/y64"] = y64.numpy()
             sur[f"{name}/{tag}/ref_err"] = np.array(d_64)
-        sur[f"{name}/bc"] = bc.numpy()
-        for k, v in sd.items():
-            sur[f"{name}/sd/{k}"] = v.numpy()
+        sur[f"{name}/bc_seed"] = np.array(600 + si)
+        sur[f"{name}/seed"] = np.array(500 + si)
+        sur[f"{name}/sd_sha256"] = np.array(sd_digest(sd))
+        sur[f"{name}/sd_layout"] = np.array(sd_layout(model.state_dict()))
         sur[f"{name}/cfg"] = np.array(json.dumps(dict(hidden_dim=H, num_layers=L, layer_type=lt)))
     np.savez_compressed(os.path.join(HERE, "surrogate.npz"), **sur)
 

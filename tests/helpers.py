@@ -30,11 +30,33 @@ def model_names():
     return sorted({k.split("/")[0] for k in m})
 
 
+def sd_digest(sd):
+    """sha256 over a state_dict's keys and raw tensor bytes (as make_golden.py)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def _fixture_sd(m, name):
+    """The fixture's weights, regenerated from the stored seed
+    (mignn.synthetic.seeded_state_dict) on the REFERENCE model's stored
+    state_dict layout (keys, order, shapes, dtypes) and checked bit for bit
+    against the stored digest."""
+    from mignn.synthetic import seeded_state_dict
+    template = {k: torch.zeros(shape, dtype=getattr(torch, dt))
+                for k, shape, dt in json.loads(str(m[f"{name}/sd_layout"]))}
+    sd = seeded_state_dict(template, seed=int(m[f"{name}/seed"]))
+    assert sd_digest(sd) == str(m[f"{name}/sd_sha256"]), f"{name}: regenerated weights differ"
+    return sd
+
+
 def model_fixture(name):
     m = npz("models.npz")
     cfg = json.loads(str(m[f"{name}/cfg"]))
-    pre = f"{name}/sd/"
-    sd = {k[len(pre):]: torch.from_numpy(v) for k, v in m.items() if k.startswith(pre)}
+    sd = _fixture_sd(m, name)
     outs = {}
     for gname in ("train", "infer"):
         if f"{name}/{gname}/y32" in m:
@@ -42,6 +64,35 @@ def model_fixture(name):
                            torch.from_numpy(m[f"{name}/{gname}/y64"]))
     err = str(m[f"{name}/edge_attr_error"]) if f"{name}/edge_attr_error" in m else None
     return cfg, sd, outs, err
+
+
+def ref_err(name, gname, which="models.npz"):
+    """The reference fp32 CPU forward's own max-abs error vs fp64 on that
+    fixture (the accuracy floor a faithful fp32 implementation sits at)."""
+    return float(npz(which)[f"{name}/{gname}/ref_err"])
+
+
+def parity_tol(name, gname, which="models.npz"):
+    """Max-abs bound vs the fp64 oracle: the north star's 1e-5, or twice the
+    reference fp32 CPU forward's own error where that alone exceeds half of
+    it (deep configs whose outputs reach O(10): fp32 ulp ~1e-6 there)."""
+    return max(1e-5, 2.0 * ref_err(name, gname, which))
+
+
+def surrogate_names():
+    return sorted({k.split("/")[0] for k in npz("surrogate.npz")})
+
+
+def surrogate_fixture(name):
+    m = npz("surrogate.npz")
+    cfg = json.loads(str(m[f"{name}/cfg"]))
+    sd = _fixture_sd(m, name)
+    outs = {tag: (torch.from_numpy(m[f"{name}/{tag}/y32"]), torch.from_numpy(m[f"{name}/{tag}/y64"]))
+            for tag in ("nobc", "bc")}
+    n = outs["bc"][0].shape[0]
+    bc = torch.rand((n, cfg["hidden_dim"]),
+                    generator=torch.Generator().manual_seed(int(m[f"{name}/bc_seed"]))) * 2 - 1
+    return cfg, sd, bc, outs
 
 
 def tiny_names():
@@ -94,3 +145,34 @@ def csr_np(ei, n, one_self_loop):
     row_ptr[1:] = np.cumsum([len(r) for r in rows])
     col = np.array([c for r in rows for c in r], np.int64)
     return row_ptr, col
+
+
+def khop_subgraph(edge_index, num_nodes, seeds, hops):
+    """Receptive field of `seeds` for an L-layer FlowGNN (hops = L): nodes at
+    in-distance <= L + 1 and every in-edge of the nodes at distance <= L.
+    Any L-layer forward on the subgraph gives the seeds exactly the outputs of
+    the forward on the whole graph -- GCN degrees (deg^-1/2 of sources at
+    distance L), GAT / Transformer softmax rows and GIN sums are all complete
+    there (test infrastructure: checks a GPU forward at full size against the
+    CPU oracle on a bounded sample).  Works on any device; returns
+    (node ids [M] (seeds first), relabelled edge_index [2, E'] int64)."""
+    dev = edge_index.device
+    src, dst = edge_index[0], edge_index[1]
+    valid = (src >= 0) & (src < num_nodes) & (dst >= 0) & (dst < num_nodes)
+    src, dst = src[valid], dst[valid]
+    dist = torch.full((num_nodes,), hops + 2, dtype=torch.int32, device=dev)
+    dist[seeds] = 0
+    for d in range(1, hops + 2):
+        frontier = dist[dst] == d - 1
+        nb = src[frontier]
+        dist[nb] = torch.minimum(dist[nb], torch.full_like(dist[nb], d))
+    seeds = seeds.to(dev)
+    others = torch.nonzero(dist <= hops + 1).flatten()
+    others = others[dist[others] > 0]
+    nodes = torch.cat([seeds, others[~torch.isin(others, seeds)]])
+    keep = dist[dst] <= hops
+    new = torch.full((num_nodes,), -1, dtype=torch.int64, device=dev)
+    new[nodes] = torch.arange(nodes.numel(), device=dev)
+    sub = torch.stack([new[src[keep]], new[dst[keep]]])
+    assert bool((sub >= 0).all())
+    return nodes, sub

@@ -13,8 +13,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import (bfs_graph, csr_np, grid_graph_np, model_fixture, model_names, tiny_fixture,
-                     tiny_names)
+from helpers import (bfs_graph, csr_np, grid_graph_np, model_fixture, model_names, parity_tol,
+                     surrogate_fixture, surrogate_names, tiny_fixture, tiny_names)
 import mignn
 from mignn import _lib
 from mignn.gnn_model import FlowGNN, build_csr, linear
@@ -333,7 +333,8 @@ def test_flowgnn_reorder_matches_natural(layer_type, precision):
             m.reorder = "1"
             y1 = m(x, ei)
         err = (y0 - y1).abs().max().item()
-        assert err < 2e-6, (layer_type, precision, seed, err)
+        # summation order only: a few fp32 ulps of the output scale
+        assert err < 2e-6 * max(1.0, y0.abs().max().item()), (layer_type, precision, seed, err)
 
 
 @pytest.mark.parametrize("H,bn,reorder", [(64, True, "0"), (128, True, "1"), (128, False, "0"),
@@ -352,7 +353,7 @@ def test_gcn_layer0_fusion_matches(H, bn, reorder, monkeypatch):
         y0 = m(x, ei)
         monkeypatch.setenv("MIGNN_FUSE_LAYER0", "1")
         y1 = m(x, ei)
-    assert (y0 - y1).abs().max().item() < 2e-6
+    assert (y0 - y1).abs().max().item() < 2e-6 * max(1.0, y0.abs().max().item())
 
 
 # ------------------------------------------------------------------ end-to-end parity
@@ -360,6 +361,9 @@ def test_gcn_layer0_fusion_matches(H, bn, reorder, monkeypatch):
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", model_names())
 def test_flowgnn_bfs_parity(name, precision, reorder):
+    """Every fixture model (configs[0..4]'s architectures among them) on the
+    reference-built BFS graphs vs the reference wrapper's fp32 CPU output and
+    the fp64 oracle; outputs are O(1)..O(10) (fan-in weights)."""
     cfg, sd, outs, err = model_fixture(name)
     m = make_model(cfg, sd, precision)
     m.reorder = reorder
@@ -370,9 +374,10 @@ def test_flowgnn_bfs_parity(name, precision, reorder):
             y = m(x.to(DEV), ei.to(DEV), ea_in).cpu()
         e32 = (y - y32).abs().max().item()
         e64 = (y.double() - y64).abs().max().item()
-        print(f"{name} {gname} {precision} reorder={reorder}: max|gpu-cpu32| {e32:.2e}  "
-              f"max|gpu-fp64| {e64:.2e}")
-        assert e32 <= TOL and e64 <= TOL
+        tol = parity_tol(name, gname)
+        print(f"{name} {gname} {precision} reorder={reorder}: |y| <= {y64.abs().max():.2f}  "
+              f"max|gpu-cpu32| {e32:.2e}  max|gpu-fp64| {e64:.2e}  (tol {tol:.1e})")
+        assert e64 <= tol and e32 <= tol + (y32.double() - y64).abs().max().item()
     if err is not None:
         x, ei, ea = bfs_graph("train")
         with pytest.raises(RuntimeError) as exc:
@@ -412,26 +417,23 @@ def test_synthetic_grid_vs_oracle(lt, H, precision):
     assert err <= TOL
 
 
-def test_full_size_properties_10M():
-    """BASELINE config size (10M nodes, avg degree 6, GCN H=128 x 4): checks
-    that need no CPU reference -- run-to-run bitwise determinism, and
-    permutation equivariance against the seeded relabelling of the mesh."""
-    cfg = dict(hidden_dim=128, num_layers=4, layer_type="GCN")
-    m0 = FlowGNN(input_dim=3, output_dim=7, **cfg)
-    m = make_model(cfg, seeded_state_dict(m0.state_dict(), seed=0))
-    x, ei = grid_graph(250, 200, 200, device=DEV)
-    with torch.no_grad():
-        y1 = m(x, ei)
-        y2 = m(x, ei)
-        assert torch.equal(y1, y2)
-        assert torch.isfinite(y1).all()
-        n = x.shape[0]
-        g = torch.Generator().manual_seed(9)
-        perm = torch.randperm(n, generator=g).to(DEV)    # old -> new
-        inv = torch.empty_like(perm)
-        inv[perm] = torch.arange(n, device=DEV)
-        yp = m(x[inv], perm[ei])
-        err = (yp[perm] - y1).abs().max().item()
-    del ei
-    print(f"10M permutation equivariance max err {err:.2e}")
-    assert err <= TOL
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("name", surrogate_names())
+def test_flowgnn_surrogate_parity(name, precision):
+    """FlowGNNSurrogate (gnn_model.py:223-291): encoder -> + boundary
+    conditions -> decoder (output_dim 8), with and without bc, vs the
+    reference's own module run (fp32 CPU) and the fp64 oracle."""
+    from mignn import FlowGNNSurrogate
+    cfg, sd, bc, outs = surrogate_fixture(name)
+    m = FlowGNNSurrogate(input_dim=3, dropout=0.1, **cfg)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    m.encoder.precision = m.decoder.precision = precision
+    x, ei, ea = bfs_graph("train")
+    for tag, b in (("nobc", None), ("bc", bc.to(DEV))):
+        y32, y64 = outs[tag]
+        with torch.no_grad():
+            y = m(x.to(DEV), ei.to(DEV), ea.to(DEV), boundary_conditions=b).cpu()
+        assert y.shape == (x.shape[0], 8)
+        assert (y.double() - y64).abs().max().item() <= TOL
+        assert (y - y32).abs().max().item() <= TOL
