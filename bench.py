@@ -21,14 +21,31 @@ Extra objects on the same JSON line:
                  traffic = PMC-measured HBM bytes per launch from profiles/
                  (rocprofv3 --pmc passes of this command, scripts/pmc.sh).
   exact_f32    : the same forward in the exact-fp32 mode (MIGNN_PRECISION=f32),
-                 graph cached, for reference.
+                 graph cached, with the roofline of its fused layer kernel
+                 (fused_tile_kernel on the f32 MFMA).
+  legs         : the other BASELINE.json configurations and SURVEY §8d legs,
+                 each an eval forward at its named size with the graph cached
+                 (steady state; edges/s = L*E/t) and a per-layer roofline
+                 (the layer's launches timed by HIP events; MFMA-bound layers
+                 against the dense f32 MFMA peak, executed flops):
+                   gcn_h64   : §8d's HBM-target layer, GCN L4 H64, 10M nodes
+                   shuffled  : the headline model on a seeded random node order
+                               (locality stress; the locality order is rebuilt
+                               inside every timed step, as in the headline)
+                   gat       : configs[2], GAT L4 H128 heads 4, 1M nodes
+                   transformer: configs[3], TransformerConv L6 H256, 10M nodes
+                   gin       : configs[4]'s model on one GPU's shard of the 100M
+                               mesh (500 x 400 x 63 = 12.6M nodes), GIN L8 H256
   cpu_baseline : the CPU oracle (pure-torch restatement of the reference
                  forward, the same op pattern PyG runs on the CPU) timed on
-                 this box's host cores on a bounded 1M-node sample (rank 0, N=1).
-  bfs_mesh     : the reference BFS mesh (train-path graph, 12,225 nodes /
-                 48,330 edges; configs[1]) -- edges/s and max-abs / mean-abs
-                 error of the raw [N,7] output vs the committed reference-CPU
-                 golden output.
+                 this box's host cores (every CPU this process may run on) on a
+                 bounded 1M-node sample of the headline model (rank 0, N=1).
+  bfs_mesh     : configs[1]'s model on the reference BFS mesh (train-path
+                 graph, 12,225 nodes / 48,330 edges) -- edges/s, max-abs /
+                 mean-abs error of the raw [N,7] output vs the committed
+                 reference-CPU golden output, and the per-field error after the
+                 reference's float64 denormalisation (inference.py:76-85,
+                 normalization.py:111-133, tests/golden/normalizer.json).
 """
 
 from __future__ import annotations
@@ -51,6 +68,28 @@ METRIC = "edges/s GNN forward (+MAE vs ref) on BFS mesh & 10M-node synthetic, 1/
 HBM_PEAK = 8.0e12      # B/s, MI355X spec (MI355X_MICROARCH.md)
 F32_MFMA_PEAK = 157.3e12  # FLOP/s, dense f32 MFMA (= f32 vector peak)
 F16_MFMA_PEAK = 2.5e15     # FLOP/s, dense f16 MFMA (MI355X_MICROARCH.md)
+HEADS = 4
+
+
+def layer_flops(lt, n_rows, e_rows, H):
+    """Executed flops of one layer over n_rows destination rows with e_rows
+    aggregation entries (E' incl. self-loops for GCN/GAT), as the engine runs
+    it (DESIGN.md §3 kernel table); the reference formulation's count differs
+    only for TransformerConv (26 N H^2 + 16 E H: Q/K/V/skip GEMMs, which the
+    engine re-associates to 18 N H^2)."""
+    if lt == "GCN":
+        return 2 * n_rows * H * H + 2 * e_rows * H
+    if lt == "GIN":
+        return 4 * n_rows * H * H + e_rows * H
+    if lt == "GAT":
+        return 8 * n_rows * H * H + 8 * e_rows * H + 16 * n_rows * H
+    return 18 * n_rows * H * H + 16 * e_rows * H          # Transformer (re-associated)
+
+
+def layer_bytes(n_rows, e_rows, H, gcn=False):
+    """Algorithmic HBM bytes of one fused layer: read x rows and write the
+    output rows once, the CSR arrays once."""
+    return 4 * (2 * n_rows * H + (n_rows + 1) + e_rows + (n_rows if gcn else 0))
 
 
 def parse():
@@ -71,6 +110,9 @@ def parse():
     p.add_argument("--cpu-grid", default="100,100,100")
     p.add_argument("--no-train", action="store_true", help="skip the training-step leg")
     p.add_argument("--train-grid", default="100,100,100")
+    p.add_argument("--no-legs", action="store_true", help="skip the other-config legs")
+    p.add_argument("--legs", default="gcn_h64,shuffled,gat,transformer,gin",
+                   help="comma list of legs (see the docstring)")
     return p.parse_args()
 
 
@@ -96,7 +138,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from mignn import FlowGNN
-    from mignn.dist import FlowGNNExecutor, SlabPartition, sharded_forward
+    from mignn.dist import DistExchange, DistRequests, FlowGNNShard, RangeLayout, sharded_forward
+    from mignn.gnn_model import locality_order
     from mignn.synthetic import grid_graph, seeded_state_dict
 
     nx, ny, nz = (int(v) for v in args.grid.split(","))
@@ -108,7 +151,6 @@ def main():
     model = model.to(dev).eval()
     model.precision = args.precision
 
-    part = SlabPartition(nx, ny, nz, rank, world)
     if world == 1:
         x, ei = grid_graph(nx, ny, nz, device=dev, permute_seed=0 if args.shuffle else None)
         E_local = ei.shape[1]
@@ -117,35 +159,36 @@ def main():
         def step():
             return model(x, ei)
     else:
-        x, ei_g = grid_graph(nx, ny, nz * world, device=dev, z_begin=rank * nz, z_count=nz)
-        ei = part.localize(ei_g)
-        del ei_g
+        # contiguous node ranges of the 250 x 200 x (200 N) mesh (natural order:
+        # k-slabs), this rank's in-edges with global ids, RCCL halo exchange
+        x, ei = grid_graph(nx, ny, nz * world, device=dev, z_begin=rank * nz, z_count=nz)
         E_local = ei.shape[1]
-        N_local = part.n_own
-        ex = FlowGNNExecutor(model, part, ei)
+        N_local = x.shape[0]
+        bounds = [r * N_local for r in range(world + 1)]
+        exch = DistExchange()
+        order = (lambda p, e: locality_order(p, e)[0]) if model._use_reorder(x) else None
+        shard_box = []
+
+        def setup():
+            lay = RangeLayout(ei, bounds, rank, DistRequests(device=dev), pos=x, order_fn=order)
+            sh = FlowGNNShard(model, lay, x)
+            sh.setup(exch, [sh])
+            shard_box[:] = [sh]
+
+        setup()
 
         def step():
             if model._csr.capacity <= 0:      # graph setup inside the step (see timed_loop)
-                ex.build_graph()
-            return sharded_forward(ex, part, x)
+                setup()
+            return sharded_forward(shard_box, exch, [x])[0]
 
     # ---- live per-launch timing of the dominant (GCN layer) kernel
-    launches = []   # (start_event, end_event, n_rows)
-    orig_layer = model._layer
+    launches = []   # (start_event, end_event, n_rows) of the headline loop
+    launches32 = []  # the same in the exact-fp32 loop
+    recording = [None]
+    restore = time_layers(model, recording)
 
-    def timed_layer(i, layer, csr, xin, out, rb, re):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        orig_layer(i, layer, csr, xin, out, rb, re)
-        e1.record()
-        if recording[0]:
-            launches.append((e0, e1, re - rb))
-
-    recording = [False]
-    model._layer = timed_layer
-
-    def timed_loop(cache_graph):
+    def timed_loop(cache_graph, rec_into=None):
         # cache_graph False: every forward rebuilds the CSR + GCN norm from
         # edge_index, as the reference's GCNConv(cached=False) recomputes its
         # normalisation each call; True: steady state on a fixed mesh
@@ -158,7 +201,7 @@ def main():
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
-            recording[0] = not cache_graph
+            recording[0] = rec_into
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 step()
@@ -167,7 +210,7 @@ def main():
                 dist.barrier()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            recording[0] = False
+            recording[0] = None
         el = t1 - t0
         if world > 1:
             t = torch.tensor([el], device=dev, dtype=torch.float64)
@@ -175,75 +218,36 @@ def main():
             el = t.item()
         return el
 
-    elapsed = timed_loop(cache_graph=False)
+    elapsed = timed_loop(cache_graph=False, rec_into=launches)
     elapsed_cached = timed_loop(cache_graph=True)
 
     # ---- roofline of the fused GCN layer kernel (this rank's launches)
     deg_plus_self = E_local / N_local + 1.0
-    tot_ms = 0.0
-    tot_bytes = tot_flops = 0.0
-    for e0, e1, n in launches:
-        tot_ms += e0.elapsed_time(e1)
-        b, f = gcn_layer_cost(n, n * deg_plus_self, H)
-        tot_bytes += b
-        tot_flops += f
+    traffic = None
+    tf = os.path.join(HERE, "profiles", "gcn_layer_traffic.json")
+    if os.path.exists(tf):
+        try:
+            with open(tf) as fh:
+                tj = json.load(fh)
+            if (tj.get("config") == f"{args.layer_type}_L{L}_H{H}_{nx}x{ny}x{nz}"
+                    and tj.get("precision", "f16x3") == model.precision):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
     roofline = None
-    if launches and args.layer_type == "GCN":
-        t_s = tot_ms / 1e3
-        gbs = tot_bytes / t_s
-        t_hbm = tot_bytes / HBM_PEAK
-        n_rows = sum(n for _, _, n in launches)
-        if model.precision == "f16x3":
-            # 3 fp16 MFMA products per fp32 product on the transform; the
-            # gather-aggregate FMAs on the fp32 VALU
-            t_comp = (3 * 2 * n_rows * H * H / F16_MFMA_PEAK
-                      + 2 * n_rows * deg_plus_self * H / F32_MFMA_PEAK)
-            kname = "gcn_f16x3_kernel<%d> (mignn_gcn_layer_f16x3)" % H
-            comp_peak, comp_note = F16_MFMA_PEAK, "f16 MFMA x3 (split fp32) + f32 VALU aggregate"
-        else:
-            t_comp = tot_flops / F32_MFMA_PEAK
-            kname = "fused_tile_kernel<%d, %d, 0, true> (mignn_gcn_layer)" % (H, H)
-            comp_peak, comp_note = F32_MFMA_PEAK, "f32 MFMA"
-        per_launch_bytes = tot_bytes / len(launches)
-        traffic = None
-        tf = os.path.join(HERE, "profiles", "gcn_layer_traffic.json")
-        if os.path.exists(tf):
-            try:
-                with open(tf) as fh:
-                    tj = json.load(fh)
-                if (tj.get("config") == f"{args.layer_type}_L{L}_H{H}_{nx}x{ny}x{nz}"
-                        and tj.get("kernel", "").split("<")[0] in kname):
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        bound_hbm = t_hbm >= t_comp
-        t_bound = max(t_hbm, t_comp)
-        roofline = {
-            "kernel": kname,
-            "bound": "hbm" if bound_hbm else "mfma",
-            "achieved": round((gbs / 1e9) if bound_hbm else (tot_flops / t_s / 1e12), 3),
-            "peak": round((HBM_PEAK / 1e9) if bound_hbm else (comp_peak / 1e12), 1),
-            "unit": "GB/s" if bound_hbm else "TFLOP/s",
-            "frac": round(t_bound / t_s, 4),
-            "traffic": traffic,
-            "avg_launch_ms": round(tot_ms / len(launches), 4),
-            "launches": len(launches),
-            "algorithmic_bytes_per_launch": int(per_launch_bytes),
-            "algorithmic_flops_per_launch": int(tot_flops / len(launches)),
-            "hbm_side": {"achieved_GBps": round(gbs / 1e9, 1), "peak_GBps": HBM_PEAK / 1e9,
-                         "frac": round(gbs / HBM_PEAK, 4), "t_min_ms": round(1e3 * t_hbm / len(launches), 4)},
-            "compute_side": {"model": comp_note, "t_min_ms": round(1e3 * t_comp / len(launches), 4),
-                             "frac": round(t_comp / t_s, 4)},
-        }
+    if args.layer_type == "GCN":
+        roofline = gcn_roofline(launches, H, deg_plus_self, model.precision, traffic)
 
-    model._layer = orig_layer
     exact = None
     if model.precision != "f32":
         model.precision = "f32"
-        el32 = timed_loop(cache_graph=True) if args.steps > 0 else 0.0
+        el32 = timed_loop(cache_graph=True, rec_into=launches32) if args.steps > 0 else 0.0
         model.precision = args.precision
         exact = {"ms_per_step_graph_cached": 1e3 * el32 / args.steps,
-                 "value_graph_cached": L * E_local * world * args.steps / el32}
+                 "value_graph_cached": L * E_local * world * args.steps / el32,
+                 "roofline": (gcn_roofline(launches32, H, deg_plus_self, "f32", None)
+                              if args.layer_type == "GCN" else None)}
+    restore()
 
     E_total = E_local * world
     value = L * E_total * args.steps / elapsed
@@ -253,7 +257,9 @@ def main():
         "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
         "graph_setup_in_step": True,
         "ms_per_step_graph_cached": 1e3 * elapsed_cached / args.steps,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "f16x3 (split fp32)" if model.precision == "f16x3" else "f32",
+        "data": "synthetic",
         "arithmetic": ("f16x3: fp32 values split into fp16 hi+lo, 3 fp16 MFMA products, fp32 "
                        "accumulate (GCN transform, output head); gathers / norms / biases fp32; "
                        "max-abs error <= 1e-5 (BASELINE tolerance)")
@@ -264,10 +270,11 @@ def main():
             "model": f"FlowGNN({args.layer_type}, layers={L}, hidden={H}, out=7), eval, "
                      "seeded random weights",
             "nodes_per_gpu": N_local, "edges_per_gpu": E_local, "global_batch": 1,
-            "parallelism": "single" if world == 1 else f"kslab{world}+rccl_halo",
+            "parallelism": "single" if world == 1 else f"node_range{world}+rccl_halo",
             "internal_node_order": ("locality (4x4-cell pencils, mignn_locality_order; part of "
-                                    "the per-step graph setup)")
-                                   if (world == 1 and model._use_reorder(x)) else "as given",
+                                    "the per-step graph setup)" + ("" if world == 1 else
+                                    ", inside each rank's range, interior rows first"))
+                                   if model._use_reorder(x) else "as given",
         },
         "roofline": roofline,
         "exact_f32": exact,
@@ -277,6 +284,17 @@ def main():
 
     if rank == 0 and not args.no_bfs:
         line["bfs_mesh"] = bfs_leg(dev)
+    if rank == 0 and world == 1 and not args.no_legs:
+        model._csr.entries.clear()
+        del x
+        ei = None
+        torch.cuda.empty_cache()
+        line["legs"] = {}
+        for name in [v for v in args.legs.split(",") if v]:
+            heavy = name in ("transformer", "gin")
+            line["legs"][name] = eval_leg(name, dev, args.precision,
+                                          steps=max(1, min(args.steps, 3 if heavy else 10)),
+                                          warmup=1 if heavy else 2)
     if rank == 0 and world == 1 and not args.no_graph:
         line["graph_build"] = graph_build_leg(dev, nx, ny, nz, not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_train:
@@ -290,6 +308,149 @@ def main():
         dist.destroy_process_group()
 
 
+def time_layers(model, recording):
+    """Wrap model._layer with HIP events on the current stream (the stream the
+    layer kernels are launched on); events go to recording[0] when it is a
+    list.  Returns the restore function."""
+    orig_layer = model._layer
+
+    def timed_layer(i, layer, csr, xin, out, rb, re, **kw):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        orig_layer(i, layer, csr, xin, out, rb, re, **kw)
+        e1.record()
+        if recording[0] is not None:
+            recording[0].append((e0, e1, re - rb))
+
+    model._layer = timed_layer
+
+    def restore():
+        model._layer = orig_layer
+    return restore
+
+
+def gcn_roofline(launches, H, deg_plus_self, precision, traffic):
+    """Roofline of the fused GCN layer kernel from its timed launches."""
+    if not launches:
+        return None
+    tot_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in launches)
+    n_rows = sum(n for _, _, n in launches)
+    tot_bytes = layer_bytes(n_rows, n_rows * deg_plus_self, H, gcn=True)
+    tot_flops = layer_flops("GCN", n_rows, n_rows * deg_plus_self, H)
+    t_s = tot_ms / 1e3
+    gbs = tot_bytes / t_s
+    t_hbm = tot_bytes / HBM_PEAK
+    if precision == "f16x3":
+        # 3 fp16 MFMA products per fp32 product on the transform; the
+        # gather-aggregate FMAs on the fp32 VALU
+        t_comp = (3 * 2 * n_rows * H * H / F16_MFMA_PEAK
+                  + 2 * n_rows * deg_plus_self * H / F32_MFMA_PEAK)
+        kname = "gcn_f16x3_kernel<%d> (mignn_gcn_layer_f16x3)" % H
+        comp_peak, comp_note = F16_MFMA_PEAK, "f16 MFMA x3 (split fp32) + f32 VALU aggregate"
+    else:
+        t_comp = tot_flops / F32_MFMA_PEAK
+        kname = "fused_tile_kernel<%d, %d, 0, true> (mignn_gcn_layer)" % (H, H)
+        comp_peak, comp_note = F32_MFMA_PEAK, "f32 MFMA"
+    bound_hbm = t_hbm >= t_comp
+    t_bound = max(t_hbm, t_comp)
+    nl = len(launches)
+    return {
+        "kernel": kname,
+        "bound": "hbm" if bound_hbm else "mfma",
+        "achieved": round((gbs / 1e9) if bound_hbm else (tot_flops / t_s / 1e12), 3),
+        "peak": round((HBM_PEAK / 1e9) if bound_hbm else (comp_peak / 1e12), 1),
+        "unit": "GB/s" if bound_hbm else "TFLOP/s",
+        "frac": round(t_bound / t_s, 4),
+        "traffic": traffic,
+        "avg_launch_ms": round(tot_ms / nl, 4),
+        "launches": nl,
+        "algorithmic_bytes_per_launch": int(tot_bytes / nl),
+        "algorithmic_flops_per_launch": int(tot_flops / nl),
+        "hbm_side": {"achieved_GBps": round(gbs / 1e9, 1), "peak_GBps": HBM_PEAK / 1e9,
+                     "frac": round(gbs / HBM_PEAK, 4), "t_min_ms": round(1e3 * t_hbm / nl, 4)},
+        "compute_side": {"model": comp_note, "t_min_ms": round(1e3 * t_comp / nl, 4),
+                         "frac": round(t_comp / t_s, 4)},
+    }
+
+
+LEGS = {
+    # name: (layer_type, hidden, layers, grid, shuffle, graph setup inside the step)
+    "gcn_h64": ("GCN", 64, 4, (250, 200, 200), None, True),
+    "shuffled": ("GCN", 128, 4, (250, 200, 200), 0, True),
+    "gat": ("GAT", 128, 4, (100, 100, 100), None, False),
+    "transformer": ("Transformer", 256, 6, (250, 200, 200), None, False),
+    "gin": ("GIN", 256, 8, (500, 400, 63), None, False),
+}
+LEG_CONFIG = {"gcn_h64": "SURVEY 8d H=64 HBM-target layer", "shuffled": "configs[1] model, shuffled order",
+              "gat": "configs[2]", "transformer": "configs[3]",
+              "gin": "configs[4] model, one GPU's shard of the 100M mesh"}
+
+
+def eval_leg(name, dev, precision, steps, warmup):
+    """One other-config forward (see the docstring): ms per forward, edges/s,
+    per-layer roofline."""
+    from mignn import FlowGNN
+    from mignn.synthetic import grid_graph, seeded_state_dict
+    lt, H, L, dims, shuffle, setup_in_step = LEGS[name]
+    cfg = dict(hidden_dim=H, num_layers=L, layer_type=lt)
+    model = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    model.load_state_dict(seeded_state_dict(model.state_dict(), seed=0))
+    model = model.to(dev).eval()
+    model.precision = precision
+    x, ei = grid_graph(*dims, device=dev, permute_seed=shuffle)
+    N, E = x.shape[0], ei.shape[1]
+    rec = [None]
+    launches = []
+    restore = time_layers(model, rec)
+    model._csr.capacity = 0 if setup_in_step else 4
+    with torch.no_grad():
+        for _ in range(warmup):
+            model(x, ei)
+        torch.cuda.synchronize()
+        rec[0] = launches
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            model(x, ei)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        rec[0] = None
+    restore()
+    e_rows = E + N if lt in ("GCN", "GAT") else E
+    out = {"config": LEG_CONFIG[name],
+           "workload": f"{lt.lower()}_L{L}_H{H}_periodic_hex_{dims[0]}x{dims[1]}x{dims[2]}"
+                       + ("_shuffled" if shuffle is not None else ""),
+           "nodes": N, "edges": E, "graph_setup_in_step": setup_in_step,
+           "ms_per_forward": round(1e3 * el / steps, 3), "edges_per_s": L * E * steps / el}
+    if lt == "GCN" and H in (64, 128):
+        out["roofline"] = gcn_roofline(launches, H, e_rows / N, precision, None)
+    else:
+        tot_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in launches)
+        n_rows = sum(n for _, _, n in launches)
+        fl = layer_flops(lt, n_rows, n_rows * e_rows / N, H)
+        by = layer_bytes(n_rows, n_rows * e_rows / N, H, gcn=lt == "GCN")
+        t_s = tot_ms / 1e3
+        t_comp, t_hbm = fl / F32_MFMA_PEAK, by / HBM_PEAK
+        nl = len(launches)
+        out["roofline"] = {
+            "unit_of_timing": "one layer (all its launches: aggregation + MFMA GEMMs), HIP events",
+            "bound": "mfma" if t_comp >= t_hbm else "hbm",
+            "achieved": round(fl / t_s / 1e12, 3) if t_comp >= t_hbm else round(by / t_s / 1e9, 1),
+            "peak": round(F32_MFMA_PEAK / 1e12, 1) if t_comp >= t_hbm else HBM_PEAK / 1e9,
+            "unit": "TFLOP/s" if t_comp >= t_hbm else "GB/s",
+            "frac": round(max(t_comp, t_hbm) / t_s, 4),
+            "avg_layer_ms": round(tot_ms / nl, 3), "layers_timed": nl,
+            "executed_flops_per_layer": int(fl / nl),
+            "reference_formulation_flops_per_layer": int(
+                (26 * N * H * H + 16 * E * H) if lt == "Transformer" else fl / nl),
+            "algorithmic_bytes_per_layer": int(by / nl),
+            "arithmetic": "exact fp32 (f32 MFMA GEMMs, f32 VALU aggregation)",
+        }
+    del model, x, ei
+    torch.cuda.empty_cache()
+    return out
+
+
 def bfs_leg(dev):
     """configs[1]: 4-layer GCN H=128 on the reference-built BFS mesh vs the
     committed reference-CPU output."""
@@ -298,10 +459,11 @@ def bfs_leg(dev):
 
     g = np.load(os.path.join(HERE, "tests", "golden", "bfs_graphs.npz"))
     m = np.load(os.path.join(HERE, "tests", "golden", "models.npz"))
+    from mignn.synthetic import seeded_state_dict_from_layout
     name = "c2_gcn_h128_l4"
     cfg = json.loads(str(m[f"{name}/cfg"]))
-    sd = {k[len(name) + 4:]: torch.from_numpy(m[k]) for k in m.files
-          if k.startswith(f"{name}/sd/")}
+    sd = seeded_state_dict_from_layout(str(m[f"{name}/sd_layout"]), int(m[f"{name}/seed"]),
+                                       str(m[f"{name}/sd_sha256"]))
     model = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
     model.load_state_dict(sd)
     model = model.to(dev).eval()
@@ -322,11 +484,37 @@ def bfs_leg(dev):
             times.append(e0.elapsed_time(e1) / 1e3)
     t = statistics.median(times)
     err = (y.cpu() - y32).abs()
+    # field space: the reference's float64 denormalisation (inference.py:76-85
+    # -> FieldNormalizer.inverse_transform, normalization.py:111-133) of both
+    # outputs, with the scalers FieldNormalizer.fit produced on the case
+    # (tests/golden/normalizer.json); ours through the engine's device path
+    import numpy as np
+    from mignn.normalization import FieldNormalizer
+    with open(os.path.join(HERE, "tests", "golden", "normalizer.json")) as fh:
+        js = json.load(fh)
+    norm = FieldNormalizer()
+    norm.scalers = {k: {"mean": np.asarray(v["mean"], dtype=np.float64) if v["per_component"]
+                        else np.float64(v["mean"]),
+                        "std": np.asarray(v["std"], dtype=np.float64) if v["per_component"]
+                        else np.float64(v["std"]),
+                        "per_component": v["per_component"]} for k, v in js.items()}
+    ours = {k: v.cpu().numpy() for k, v in norm.inverse_transform(model.predict_fields(y)).items()}
+    refs = {}
+    for k, v in model.predict_fields(y32).items():          # numpy float64, as the reference
+        sc = js[k]
+        refs[k] = v.numpy() * np.asarray(sc["std"], dtype=np.float64) + np.asarray(sc["mean"], dtype=np.float64)
+    fields = {}
+    for k in refs:
+        d = np.abs(np.asarray(ours[k], dtype=np.float64) - refs[k])
+        fields[k] = {"mae": float(d.mean()), "max_abs": float(d.max()),
+                     "field_std": float(np.std(refs[k])),
+                     "max_abs_over_field_std": float(d.max() / max(np.std(refs[k]), 1e-300))}
     return {"config": "configs[1]: GCN L4 H128, train-path BFS mesh",
             "nodes": int(x.shape[0]), "edges": int(ei.shape[1]),
             "ms_per_forward": round(t * 1e3, 4),
             "edges_per_s": cfg["num_layers"] * ei.shape[1] / t,
-            "max_abs_err_vs_ref_cpu": err.max().item(), "mae_vs_ref_cpu": err.mean().item()}
+            "max_abs_err_vs_ref_cpu": err.max().item(), "mae_vs_ref_cpu": err.mean().item(),
+            "denormalized_fields_vs_ref_cpu": fields}
 
 
 def train_leg(dev, args):
@@ -425,7 +613,10 @@ def cpu_leg(model, sd, cfg, args, dev):
     from oracle import flowgnn_oracle as orc
     from mignn.synthetic import grid_graph
 
-    threads = min(16, os.cpu_count() or 1)
+    # every CPU this process may run on (its cpuset / affinity: the box's share
+    # of the host when the pool restricts it, else the whole machine)
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, threads or 1)
     torch.set_num_threads(threads)
     cx, cy, cz = (int(v) for v in args.cpu_grid.split(","))
     xg, eig = grid_graph(cx, cy, cz, device=dev)
@@ -450,10 +641,13 @@ def cpu_leg(model, sd, cfg, args, dev):
     except OSError:
         pass
     return {"value": cfg["num_layers"] * ei.shape[1] / t, "unit": "edges/s", "cores": threads,
+            "os_cpu_count": os.cpu_count(),
             "kind": "port",
             "sample": f"{cfg['layer_type']} L{cfg['num_layers']} H{cfg['hidden_dim']} forward on "
                       f"the {cx}x{cy}x{cz} periodic mesh ({x.shape[0]} nodes, {ei.shape[1]} edges), "
-                      f"torch-CPU oracle fp32, median of 2 after 1 warm-up",
+                      f"torch-CPU oracle fp32, median of 2 after 1 warm-up; the CPU path is "
+                      f"O(L E H) with no cache effects at this size, so its edges/s is taken as "
+                      f"size-independent (extrapolated to the 10M headline mesh, not timed there)",
             "s_per_forward": round(t, 3), "cpu_model": cpu_model,
             "gpu_vs_cpu_max_abs_err": (yg - y).abs().max().item()}
 

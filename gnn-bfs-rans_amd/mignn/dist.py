@@ -1,189 +1,382 @@
-"""Node-range (k-slab) partitioning of a mesh across GPUs with a 1-hop halo
-exchange per layer.  One process per GPU; the exchange is
+"""Node-range partitioning of any graph across GPUs with a 1-hop halo
+exchange per layer (north star: "large meshes shard by
+contiguous node-range across the 8 GPUs ... with RCCL halo exchange of
+boundary node features").  One process per GPU; the exchange is
 point-to-point `torch.distributed` (backend "nccl" == RCCL over xGMI on
 MI355X, "gloo" on the CPU test path).
 
-Layout per rank (natural node order, i fastest, k slowest):
-    rows [0, n_own)                 owned nodes: k-planes [r*nzl, (r+1)*nzl)
-    rows [n_own, n_own+plane)       lower ghost plane  (global plane r*nzl - 1)
-    rows [n_own+plane, n_own+2pl)   upper ghost plane  (global plane (r+1)*nzl)
-A slab's halo is one contiguous i-j plane per side, so nothing is packed: the
-sends are x[0:plane] (to the lower peer, its upper ghost) and
-x[n_own-plane:n_own] (to the upper peer, its lower ghost).  The grid is
-periodic in k, so every rank has exactly two peers (one peer, twice, at P=2).
+Partition: rank r owns the global node ids [bounds[r], bounds[r+1]) and the
+in-edges of those nodes (the CSR rows it computes).  `RangeLayout` derives,
+from this rank's edges alone plus one exchange of requests:
+  * ghosts  : the sources of its in-edges owned by other ranks, sorted by
+              global id (so grouped by owner rank: one contiguous slice of the
+              activation buffer per peer -- received rows land in place);
+  * send lists: the owned rows each peer asked for (packed with
+              mignn_rows_gather on the GPU);
+  * a local order of the owned rows: interior rows (no ghost source) first,
+    boundary rows last, each group in the mesh locality order
+    (mignn_locality_order on the cell centres) when one is given -- so the
+    interior rows run while RCCL moves the halo, as one contiguous launch.
+Activation buffers are [n_own + n_ghost, H]: owned rows (local order), then
+the ghosts.  Static per-graph data crosses once: GCN's ghost deg^-1/2 and the
+ghost cell centres (the fused input_proj + GCN layer 0 reads coordinates, so
+layer 0 needs no feature exchange at all).
 
-Per layer: post the exchange, run the interior rows [plane, n_own-plane) --
-which read no ghost row -- on the compute stream while RCCL moves the planes,
-wait, then run the two boundary planes.  GCN additionally needs the ghost
-nodes' deg^-1/2, exchanged once when the graph is set up.  Eval-mode
-BatchNorm needs no communication.
+`sharded_forward` drives any list of shards with a halo-exchange object:
+`DistExchange` (this rank's shard, torch.distributed P2P) or `LocalExchange`
+(several shards in one process, the halo filled by device-to-device row
+copies) -- the same per-layer code either way, which is what the
+single-process multi-shard GPU tests exercise.
 """
 
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import Callable, List, Optional
+from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
-TAG_TO_LOWER = 11   # my first plane -> lower peer's upper ghost
-TAG_TO_UPPER = 12   # my last plane  -> upper peer's lower ghost
+TAG_HALO = 17
 
 
-@dataclass
-class SlabPartition:
-    nx: int
-    ny: int
-    nz_local: int
-    rank: int
-    world: int
+# ---------------------------------------------------------------------------
+# layout
+# ---------------------------------------------------------------------------
 
-    @property
-    def plane(self) -> int:
-        return self.nx * self.ny
-
-    @property
-    def nz_total(self) -> int:
-        return self.nz_local * self.world
-
-    @property
-    def n_own(self) -> int:
-        return self.plane * self.nz_local
-
-    @property
-    def n_total(self) -> int:
-        return self.n_own + (2 * self.plane if self.world > 1 else 0)
-
-    @property
-    def lower_peer(self) -> int:
-        return (self.rank - 1) % self.world
-
-    @property
-    def upper_peer(self) -> int:
-        return (self.rank + 1) % self.world
-
-    @property
-    def z_begin(self) -> int:
-        return self.rank * self.nz_local
-
-    def interior(self):
-        return (self.plane, self.n_own - self.plane)
-
-    def boundary(self):
-        return [(0, self.plane), (self.n_own - self.plane, self.n_own)]
-
-    def localize(self, edge_index_global: torch.Tensor) -> torch.Tensor:
-        """Map global node ids of this slab's edges to local rows (own, then
-        lower ghost plane, then upper ghost plane)."""
-        if self.world == 1:
-            return edge_index_global
-        pl = self.plane
-        base = self.z_begin * pl
-        g = edge_index_global
-        lo_plane = ((self.z_begin - 1) % self.nz_total) * pl
-        up_plane = ((self.z_begin + self.nz_local) % self.nz_total) * pl
-        local = g - base
-        own = (g >= base) & (g < base + self.n_own)
-        lo = (g >= lo_plane) & (g < lo_plane + pl) & ~own
-        up = (g >= up_plane) & (g < up_plane + pl) & ~own
-        local = torch.where(lo, g - lo_plane + self.n_own, local)
-        local = torch.where(up, g - up_plane + self.n_own + pl, local)
-        bad = ~(own | lo | up)
-        if bool(bad.any()):
-            raise ValueError("edge references a node outside the slab and its 1-hop halo")
-        return local
+def range_bounds(num_nodes: int, world: int) -> List[int]:
+    """Contiguous node ranges [r*N/P, (r+1)*N/P)."""
+    return [(r * num_nodes) // world for r in range(world + 1)]
 
 
-def halo_exchange(buf: torch.Tensor, part: SlabPartition, group=None) -> List:
-    """Post the two-plane exchange on `buf` ([n_total, F]); returns works to wait on."""
-    if part.world == 1:
-        return []
-    pl, n = part.plane, part.n_own
-    ops = [
-        dist.P2POp(dist.isend, buf[0:pl], part.lower_peer, group, TAG_TO_LOWER),
-        dist.P2POp(dist.irecv, buf[n + pl:n + 2 * pl], part.upper_peer, group, TAG_TO_LOWER),
-        dist.P2POp(dist.isend, buf[n - pl:n], part.upper_peer, group, TAG_TO_UPPER),
-        dist.P2POp(dist.irecv, buf[n:n + pl], part.lower_peer, group, TAG_TO_UPPER),
-    ]
-    return dist.batch_isend_irecv(ops)
+class RangeLayout:
+    """One rank's part of a contiguous node-range partition (see the module
+    docstring).  `edge_index` [2, E_r] holds global ids of the edges whose
+    destination this rank owns (int64, any device); `pos` [n_own, >=3]
+    optional cell centres of the owned nodes (caller order = global id
+    order), used only to pick the locality order via `order_fn(pos, ei)`
+    -> perm (local position -> owned offset)."""
+
+    def __init__(self, edge_index: torch.Tensor, bounds: Sequence[int], rank: int,
+                 requests: "RequestExchange", pos: Optional[torch.Tensor] = None,
+                 order_fn: Optional[Callable] = None):
+        dev = edge_index.device
+        self.rank, self.world = rank, len(bounds) - 1
+        self.bounds = [int(b) for b in bounds]
+        lo, hi = self.bounds[rank], self.bounds[rank + 1]
+        self.lo, self.hi, self.n_own = lo, hi, hi - lo
+        src, dst = edge_index[0].long(), edge_index[1].long()
+        if bool(((dst < lo) | (dst >= hi)).any()):
+            raise ValueError("edge_index holds an edge whose destination this rank does not own")
+        if src.numel() and bool(((src < 0) | (src >= self.bounds[-1])).any()):
+            raise ValueError("edge_index holds a source outside [0, N)")
+        own_src = (src >= lo) & (src < hi)
+        # ghosts: sorted global ids == grouped by owner rank (contiguous ranges)
+        ghost = torch.unique(src[~own_src])
+        self.ghost_gid = ghost
+        self.n_ghost = int(ghost.numel())
+        self.n_total = self.n_own + self.n_ghost
+        b = torch.tensor(self.bounds, dtype=torch.int64, device=dev)
+        owner = torch.searchsorted(b, ghost, right=True) - 1
+        counts = torch.bincount(owner, minlength=self.world).cpu().tolist()
+        self.ghost_ptr = [0]
+        for c in counts:
+            self.ghost_ptr.append(self.ghost_ptr[-1] + int(c))
+        # local order of the owned rows: interior first, boundary last
+        boundary = torch.zeros(self.n_own, dtype=torch.bool, device=dev)
+        boundary[dst[~own_src] - lo] = True
+        if order_fn is not None and pos is not None and self.n_own > 0:
+            keep = own_src
+            base = order_fn(pos, torch.stack([src[keep] - lo, dst[keep] - lo])).long()
+        else:
+            base = torch.arange(self.n_own, device=dev)
+        key = boundary[base].to(torch.int64)
+        perm = base[torch.sort(key, stable=True).indices]       # local position -> owned offset
+        self.perm = perm
+        self.inv = torch.empty_like(perm)
+        self.inv[perm] = torch.arange(self.n_own, device=dev)
+        self.n_int = int((~boundary).sum())
+        # local edge list: owned -> local position, ghost -> n_own + ghost index
+        lsrc = torch.where(own_src, self.inv[(src - lo).clamp(0, max(self.n_own - 1, 0))],
+                           self.n_own + torch.searchsorted(ghost, src))
+        self.edge_index = torch.stack([lsrc, self.inv[dst - lo]])
+        # send lists: every peer's ghost requests, answered with my local rows
+        req = {q: ghost[self.ghost_ptr[q]:self.ghost_ptr[q + 1]]
+               for q in range(self.world) if q != rank and counts[q] > 0}
+        got = requests.exchange(rank, req)
+        self.send_idx: Dict[int, torch.Tensor] = {
+            q: self.inv[ids.to(dev).long() - lo].to(torch.int32) for q, ids in got.items()
+            if ids.numel() > 0}
+
+    def ghost_slice(self, q: int) -> slice:
+        return slice(self.n_own + self.ghost_ptr[q], self.n_own + self.ghost_ptr[q + 1])
+
+    def peers(self) -> List[int]:
+        return sorted(set(self.send_idx) | {q for q in range(self.world)
+                                            if q != self.rank and self.ghost_ptr[q + 1] > self.ghost_ptr[q]})
 
 
-class LayerExecutor:
-    """What the sharded driver needs from a compute backend."""
+class RequestExchange:
+    """Setup-time exchange of ghost id lists (who needs which of my rows)."""
 
+    def exchange(self, rank: int, req: Dict[int, torch.Tensor]) -> Dict[int, torch.Tensor]:
+        raise NotImplementedError
+
+
+class DistRequests(RequestExchange):
+    """torch.distributed: counts by all_gather, id lists by P2P."""
+
+    def __init__(self, group=None, device=None):
+        self.group, self.device = group, device
+
+    def exchange(self, rank, req):
+        world = dist.get_world_size(self.group)
+        dev = self.device or torch.device("cpu")
+        mine = torch.zeros(world, dtype=torch.int64, device=dev)
+        for q, ids in req.items():
+            mine[q] = ids.numel()
+        allc = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine, group=self.group)
+        ops, got = [], {}
+        for q in range(world):
+            if q == rank:
+                continue
+            if q in req and req[q].numel():
+                ops.append(dist.P2POp(dist.isend, req[q].to(dev).contiguous(), q, self.group, TAG_HALO))
+            n = int(allc[q][rank])
+            if n:
+                got[q] = torch.empty(n, dtype=torch.int64, device=dev)
+                ops.append(dist.P2POp(dist.irecv, got[q], q, self.group, TAG_HALO))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return got
+
+
+class LocalRequests(RequestExchange):
+    """Several ranks' layouts built in one process: requests are handed over
+    directly (build rank 0..P-1 in order with the same object, then call
+    `resolve` -- see build_local_layouts)."""
+
+    def __init__(self):
+        self.posted: Dict[int, Dict[int, torch.Tensor]] = {}
+
+    def exchange(self, rank, req):
+        self.posted[rank] = req
+        return {}
+
+
+def build_local_layouts(edge_lists: Sequence[torch.Tensor], bounds: Sequence[int],
+                        pos: Optional[Sequence[torch.Tensor]] = None,
+                        order_fn: Optional[Callable] = None) -> List[RangeLayout]:
+    """All P layouts of a partition in one process (LocalExchange shards)."""
+    reqs = LocalRequests()
+    lays = [RangeLayout(ei, bounds, r, reqs, None if pos is None else pos[r], order_fn)
+            for r, ei in enumerate(edge_lists)]
+    for r, lay in enumerate(lays):          # answer the requests posted to each rank
+        lay.send_idx = {q: lay.inv[reqs.posted[q][r].long() - lay.lo].to(torch.int32)
+                        for q in range(len(lays)) if q != r and r in reqs.posted.get(q, {})
+                        and reqs.posted[q][r].numel() > 0}
+    return lays
+
+
+# ---------------------------------------------------------------------------
+# halo exchange
+# ---------------------------------------------------------------------------
+
+def _gather_rows(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor):
+    """dst[r] = src[idx[r]] (mignn_rows_gather on a ROCm device)."""
+    if src.is_cuda:
+        from . import _lib
+        _lib.check(_lib.lib().mignn_rows_gather(
+            _lib.ptr(src), src.stride(0), _lib.ptr(idx), idx.numel(), src.shape[1],
+            _lib.ptr(dst), dst.stride(0), _lib.stream(src.device)), "mignn_rows_gather")
+    else:
+        torch.index_select(src, 0, idx.long(), out=dst)
+
+
+class DistExchange:
+    """This rank's halo over torch.distributed P2P: pack each peer's rows,
+    isend; irecv straight into the peer's ghost slice."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def start(self, shards, bufs):
+        (sh,), (buf,) = shards, bufs
+        lay = sh.layout
+        ops = []
+        for q in lay.peers():
+            if q in lay.send_idx:
+                idx = lay.send_idx[q]
+                pk = torch.empty((idx.numel(), buf.shape[1]), dtype=buf.dtype, device=buf.device)
+                _gather_rows(buf, idx, pk)
+                ops.append(dist.P2POp(dist.isend, pk, q, self.group, TAG_HALO))
+            sl = lay.ghost_slice(q)
+            if sl.stop > sl.start:
+                ops.append(dist.P2POp(dist.irecv, buf[sl], q, self.group, TAG_HALO))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    def wait(self, handle):
+        for w in handle:
+            w.wait()
+
+
+class LocalExchange:
+    """All shards in one process: every send list is copied device-to-device
+    into the receiving shard's ghost slice (the stream orders the copies
+    before the boundary rows' launches)."""
+
+    def start(self, shards, bufs):
+        for r, sh in enumerate(shards):
+            for q, idx in sh.layout.send_idx.items():
+                dst = bufs[q][shards[q].layout.ghost_slice(r)]
+                _gather_rows(bufs[r], idx, dst)
+        return None
+
+    def wait(self, handle):
+        pass
+
+
+def exchange_static(shards, exchange, tensors: List[torch.Tensor]):
+    """One-off halo fill of per-row static data (owned rows already written)."""
+    exchange.wait(exchange.start(shards, tensors))
+
+
+# ---------------------------------------------------------------------------
+# driver
+# ---------------------------------------------------------------------------
+
+class Shard:
+    """What sharded_forward needs from a compute backend for one rank."""
+
+    layout: RangeLayout
     num_layers: int
     hidden_dim: int
-    overlap_ok: bool = True
 
-    def input_proj(self, x_own: torch.Tensor, out: torch.Tensor) -> None: ...
+    def first_layer(self, x_own: torch.Tensor, buf: torch.Tensor) -> int:
+        """Write layer-0 input (or, fused, layer 0's output) rows [0, n_own)
+        of buf; return the index of the first layer still to run."""
+        raise NotImplementedError
+
     def layer(self, i: int, x: torch.Tensor, out: torch.Tensor, rb: int, re: int) -> None: ...
+
+    def before_halo(self, i: int, x: torch.Tensor) -> None:
+        """Work of layer i that needs only owned rows (before the halo lands)."""
+
+    def after_halo(self, i: int, x: torch.Tensor) -> None:
+        """Work of layer i on the ghost rows once they have landed."""
+
     def output(self, x_own: torch.Tensor) -> torch.Tensor: ...
 
 
-def sharded_forward(ex: LayerExecutor, part: SlabPartition, x_own: torch.Tensor, group=None,
-                    timing_hook: Optional[Callable] = None) -> torch.Tensor:
-    """Forward of one rank's slab; returns the rank's [n_own, out] rows."""
-    H = ex.hidden_dim
-    dev = x_own.device
-    a = torch.empty((part.n_total, H), dtype=x_own.dtype, device=dev)
-    b = torch.empty_like(a)
-    ex.input_proj(x_own, a[:part.n_own])
-    cur, nxt = a, b
-    for i in range(ex.num_layers):
-        works = halo_exchange(cur, part, group)
-        if part.world > 1 and ex.overlap_ok:
-            rb, re = part.interior()
-            ex.layer(i, cur, nxt, rb, re)
-            for w in works:
-                w.wait()
-            for rb, re in part.boundary():
-                ex.layer(i, cur, nxt, rb, re)
-        else:
-            for w in works:
-                w.wait()
-            ex.layer(i, cur, nxt, 0, part.n_own)
+def sharded_forward(shards: List[Shard], exchange, xs_own: List[torch.Tensor]) -> List[torch.Tensor]:
+    """Forward of every shard in `shards` (one for DistExchange); returns each
+    shard's [n_own, out] rows in its owned-node (global id) order.
+    Per layer: post the halo exchange, run the interior rows, wait, run the
+    ghost-dependent work and the boundary rows."""
+    bufs_a, bufs_b, starts = [], [], []
+    for sh, x in zip(shards, xs_own):
+        lay = sh.layout
+        a = torch.empty((lay.n_total, sh.hidden_dim), dtype=torch.float32 if x.is_cuda else x.dtype,
+                        device=x.device)
+        bufs_a.append(a)
+        bufs_b.append(torch.empty_like(a))
+        starts.append(sh.first_layer(x, a))
+    first = starts[0]
+    assert all(s == first for s in starts)
+    cur, nxt = bufs_a, bufs_b
+    for i in range(first, shards[0].num_layers):
+        h = exchange.start(shards, cur)
+        for sh, x, o in zip(shards, cur, nxt):
+            sh.before_halo(i, x)
+            sh.layer(i, x, o, 0, sh.layout.n_int)
+        exchange.wait(h)
+        for sh, x, o in zip(shards, cur, nxt):
+            sh.after_halo(i, x)
+            sh.layer(i, x, o, sh.layout.n_int, sh.layout.n_own)
         cur, nxt = nxt, cur
-    return ex.output(cur[:part.n_own])
+    return [sh.output(x[:sh.layout.n_own]) for sh, x in zip(shards, cur)]
 
 
-class FlowGNNExecutor(LayerExecutor):
-    """GPU executor: FlowGNN's native layers on a rank-local CSR."""
+class FlowGNNShard(Shard):
+    """GPU shard: FlowGNN's native layers on the rank-local CSR (owned rows
+    in the interior/boundary locality order, then the ghosts)."""
 
-    def __init__(self, model, part: SlabPartition, edge_index_local: torch.Tensor, group=None):
-        self.model = model
-        self.part = part
-        self.group = group
-        self.edge_index_local = edge_index_local
-        self.num_layers = model.num_layers
-        self.hidden_dim = model.hidden_dim
-        self.overlap_ok = model.layer_type != "GAT"   # GAT logits read ghost rows
-        self.build_graph()
+    def __init__(self, model, layout: RangeLayout, x_own: torch.Tensor):
+        self.model, self.layout = model, layout
+        self.num_layers, self.hidden_dim = model.num_layers, model.hidden_dim
+        self.x_own = x_own
+        self.logits = None
+        self.csr = None
 
-    def build_graph(self):
-        """Rank-local CSR (+ GCN norm with the ghost rows' true degrees)."""
+    def setup(self, exchange, shards: List["FlowGNNShard"]):
+        """Per-graph setup of every shard in `shards` (collective over them):
+        local CSRs, GCN ghost degrees + edge weights, ghost cell centres."""
         from ._lib import CSR_ONE_SELF_LOOP, CSR_VERBATIM
         from .gnn_model import build_csr
+        m = self.model
+        mode = CSR_ONE_SELF_LOOP if m.layer_type in ("GCN", "GAT") else CSR_VERBATIM
+        for sh in shards:
+            sh.csr = build_csr(sh.layout.edge_index, sh.layout.n_total, mode)
+        if shards[0].csr.dinv is not None:
+            # ghost rows' true deg^-1/2 comes from their owners
+            exchange_static(shards, exchange, [sh.csr.dinv[:sh.layout.n_total].view(-1, 1)
+                                               for sh in shards])
+            for sh in shards:
+                sh.csr.compute_gcn_weights(0, sh.layout.n_own)
+        if m._fuse_layer0():
+            D = m.input_dim
+            poss = []
+            for sh in shards:
+                p = torch.zeros((sh.layout.n_total, D), dtype=torch.float32, device=sh.x_own.device)
+                p[:sh.layout.n_own] = sh.x_own.float()[sh.layout.perm]
+                poss.append(p)
+            exchange_static(shards, exchange, poss)
+            for sh, p in zip(shards, poss):
+                sh.pos = p
 
-        part = self.part
-        mode = CSR_ONE_SELF_LOOP if self.model.layer_type in ("GCN", "GAT") else CSR_VERBATIM
-        self.csr = build_csr(self.edge_index_local, part.n_total, mode)
-        if self.csr.dinv is not None and part.world > 1:
-            # ghost rows' true deg^-1/2 comes from their owner
-            d = self.csr.dinv[:part.n_total].view(-1, 1)
-            for w in halo_exchange(d, part, self.group):
-                w.wait()
-            self.csr.compute_gcn_weights(0, part.n_own)   # entries of owned rows, true ghost dinv
+    def first_layer(self, x_own, buf):
+        m, lay = self.model, self.layout
+        if m._fuse_layer0():
+            from . import _lib
+            _lib.check(_lib.lib().mignn_gcn_layer0_coords(
+                _lib.ptr(self.csr.row_ptr), _lib.ptr(self.csr.col), _lib.ptr(self.csr.ew),
+                _lib.ptr(self.pos), self.pos.stride(0), m.input_dim, 0, lay.n_own,
+                _lib.ptr(m._layer0_coef()), m.hidden_dim, _lib.ptr(buf), buf.stride(0),
+                _lib.stream(buf.device)), "mignn_gcn_layer0_coords")
+            return 1
+        xo = x_own.contiguous().float()
+        m._input_proj(xo, buf[:lay.n_own], rows=lay.perm.to(torch.int32))
+        return 0
 
-    def input_proj(self, x_own, out):
-        self.model._input_proj(x_own.contiguous(), out)
+    def before_halo(self, i, x):
+        if self.model.layer_type == "GAT":
+            from .gnn_model import linear
+            layer = self.model.gnn_layers[i]
+            wlog, _ = self.model._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
+                                         lambda: self.model._gat_weights(layer))
+            self.logits = torch.empty((self.layout.n_total, wlog.shape[0]), dtype=torch.float32,
+                                      device=x.device)
+            linear(x[:self.layout.n_own], wlog, out=self.logits[:self.layout.n_own])
+
+    def after_halo(self, i, x):
+        if self.model.layer_type == "GAT" and self.layout.n_ghost:
+            from .gnn_model import linear
+            layer = self.model.gnn_layers[i]
+            wlog, _ = self.model._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
+                                         lambda: self.model._gat_weights(layer))
+            linear(x[self.layout.n_own:], wlog, out=self.logits[self.layout.n_own:])
 
     def layer(self, i, x, out, rb, re):
-        self.model._layer(i, self.model.gnn_layers[i], self.csr, x, out, rb, re)
+        self.model._layer(i, self.model.gnn_layers[i], self.csr, x, out, rb, re,
+                          logits=self.logits)
 
     def output(self, x_own):
-        out = torch.empty((x_own.shape[0], self.model.output_dim), dtype=torch.float32,
+        m = self.model
+        out = torch.empty((x_own.shape[0], m.output_dim), dtype=torch.float32,
                           device=x_own.device)
         tmp = torch.empty_like(x_own)
-        self.model._output_mlp(x_own, tmp, out)   # x_own is scratch after the last layer
+        # local order -> owned (global id) order
+        m._output_mlp(x_own, tmp, out, rows=self.layout.perm.to(torch.int32),
+                      inv=self.layout.inv.to(torch.int32))
         return out

@@ -616,9 +616,11 @@ class FlowGNN(nn.Module):
                 hit = self._prep[key] = make()
         return hit
 
-    def _layer(self, i, layer, csr: Csr, x, out, rb: int, re: int, ldx_rows=None):
+    def _layer(self, i, layer, csr: Csr, x, out, rb: int, re: int, logits=None):
         """One conv + residual + BN + ReLU (gnn_model.py:162-192) for rows [rb, re).
-        `x` holds every row the CSR references (own rows + halo rows)."""
+        `x` holds every row the CSR references (own rows + halo rows).  GAT:
+        `logits` [rows, 2*heads] of every referenced row, precomputed by a
+        sharded caller (mignn.dist); None: computed here for all rows of x."""
         H = self.hidden_dim
         L = _lib.lib()
         st = _stream(x)
@@ -664,7 +666,8 @@ class FlowGNN(nn.Module):
         elif self.layer_type == "GAT":
             wlog, wcat = self._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
                                       lambda: self._gat_weights(layer))
-            logits = linear(x, wlog)                                   # [rows, 2*heads]
+            if logits is None:
+                logits = linear(x, wlog)                               # [rows, 2*heads]
             agg = torch.empty((n, HEADS * H), dtype=torch.float32, device=x.device)
             _lib.check(L.mignn_gat_aggregate(P(csr.row_ptr), P(csr.col), P(logits), P(x),
                                              x.stride(0), rb, re, H, HEADS,

@@ -62,6 +62,29 @@ def seeded_state_dict(template: Dict[str, torch.Tensor], seed: int = 0,
     return out
 
 
+def state_dict_digest(sd: Dict[str, torch.Tensor]) -> str:
+    """sha256 over a state_dict's keys and raw tensor bytes (sorted keys)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def seeded_state_dict_from_layout(layout_json: str, seed: int, digest: Optional[str] = None,
+                                  scale: str = "fan_in") -> Dict[str, torch.Tensor]:
+    """seeded_state_dict on a stored state_dict layout ([[key, shape, dtype], ...]
+    JSON, e.g. a reference model's), checked against `digest` when given."""
+    import json
+    template = {k: torch.zeros(shape, dtype=getattr(torch, dt))
+                for k, shape, dt in json.loads(layout_json)}
+    sd = seeded_state_dict(template, seed=seed, scale=scale)
+    if digest is not None and state_dict_digest(sd) != digest:
+        raise ValueError("regenerated state_dict does not match the stored digest")
+    return sd
+
+
 def grid_dims(num_nodes: int) -> Tuple[int, int, int]:
     """Named synthetic sizes."""
     named = {

@@ -42,23 +42,13 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "gnn-bfs-rans_amd"))
 
 from oracle import flowgnn_oracle as orc  # noqa: E402
-from mignn.synthetic import seeded_state_dict  # noqa: E402
+from mignn.synthetic import seeded_state_dict, state_dict_digest as sd_digest  # noqa: E402
 
 
 class _Data:  # stand-in for torch_geometric.data.Data (attribute bag)
     def __init__(self, **kw):
         for k, v in kw.items():
             setattr(self, k, v)
-
-
-def sd_digest(sd):
-    """sha256 over the state_dict's keys and raw tensor bytes (sorted keys)."""
-    import hashlib
-    h = hashlib.sha256()
-    for k in sorted(sd):
-        h.update(k.encode())
-        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
-    return h.hexdigest()
 
 
 def sd_layout(sd):

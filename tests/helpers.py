@@ -30,27 +30,14 @@ def model_names():
     return sorted({k.split("/")[0] for k in m})
 
 
-def sd_digest(sd):
-    """sha256 over a state_dict's keys and raw tensor bytes (as make_golden.py)."""
-    import hashlib
-    h = hashlib.sha256()
-    for k in sorted(sd):
-        h.update(k.encode())
-        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
-    return h.hexdigest()
-
-
 def _fixture_sd(m, name):
     """The fixture's weights, regenerated from the stored seed
     (mignn.synthetic.seeded_state_dict) on the REFERENCE model's stored
     state_dict layout (keys, order, shapes, dtypes) and checked bit for bit
     against the stored digest."""
-    from mignn.synthetic import seeded_state_dict
-    template = {k: torch.zeros(shape, dtype=getattr(torch, dt))
-                for k, shape, dt in json.loads(str(m[f"{name}/sd_layout"]))}
-    sd = seeded_state_dict(template, seed=int(m[f"{name}/seed"]))
-    assert sd_digest(sd) == str(m[f"{name}/sd_sha256"]), f"{name}: regenerated weights differ"
-    return sd
+    from mignn.synthetic import seeded_state_dict_from_layout
+    return seeded_state_dict_from_layout(str(m[f"{name}/sd_layout"]), int(m[f"{name}/seed"]),
+                                         str(m[f"{name}/sd_sha256"]))
 
 
 def model_fixture(name):

@@ -1,0 +1,87 @@
+"""The sharded forward on the GPU without a second GPU: P = 2 and 4 shards of
+one graph in one process, each a FlowGNNShard (the native layers on its
+rank-local CSR, owned rows in the interior/boundary locality order, fused
+GCN layer 0 from exchanged ghost coordinates), the halo filled by
+device-to-device row copies through the same sharded_forward code the
+multi-process RCCL path runs.  Must equal the unsharded forward up to fp32
+summation order, for all four layer types, on k-slabs (natural order) and on
+arbitrary node ranges (shuffled order)."""
+
+import pytest
+import torch
+
+from mignn import FlowGNN
+from mignn.dist import FlowGNNShard, LocalExchange, build_local_layouts, range_bounds, sharded_forward
+from mignn.gnn_model import locality_order
+from mignn.synthetic import grid_graph, seeded_state_dict
+from oracle import flowgnn_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm GPU")
+    from mignn import _lib
+    _lib.lib()
+
+
+def _sharded(model, x, ei, P, ordered=True):
+    n = x.shape[0]
+    b = range_bounds(n, P)
+    edges = [ei[:, (ei[1] >= b[r]) & (ei[1] < b[r + 1])] for r in range(P)]
+    pos = [x[b[r]:b[r + 1]] for r in range(P)]
+    order = (lambda p, e: locality_order(p, e)[0]) if ordered else None
+    lays = build_local_layouts(edges, b, pos=pos, order_fn=order)
+    shards = [FlowGNNShard(model, lay, p) for lay, p in zip(lays, pos)]
+    ex = LocalExchange()
+    shards[0].setup(ex, shards)
+    with torch.no_grad():
+        ys = sharded_forward(shards, ex, pos)
+    return torch.cat(ys, 0), lays
+
+
+@pytest.mark.parametrize("shuffle", [None, 2])
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("lt,H", [("GCN", 128), ("GCN", 64), ("GAT", 64), ("GIN", 64),
+                                  ("Transformer", 64)])
+def test_sharded_matches_unsharded(lt, H, P, shuffle):
+    cfg = dict(hidden_dim=H, num_layers=3, layer_type=lt)
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    sd = seeded_state_dict(m.state_dict(), seed=4)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    x, ei = grid_graph(24, 20, 16, device=DEV, permute_seed=shuffle)
+    with torch.no_grad():
+        y = m(x, ei)
+    ys, lays = _sharded(m, x, ei, P)
+    scale = max(1.0, y.abs().max().item())
+    err = (ys - y).abs().max().item()
+    ref = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
+    e64 = (ys.cpu().double() - ref).abs().max().item()
+    print(f"{lt} H{H} P={P} shuffle={shuffle}: ghosts/rank {[l.n_ghost for l in lays]}, "
+          f"interior {[l.n_int for l in lays]}, max|sharded-unsharded| {err:.2e}, "
+          f"max|sharded-fp64| {e64:.2e}")
+    if shuffle is None:
+        plane = 24 * 20
+        assert all(l.n_ghost == 2 * plane for l in lays)      # k-slabs: two halo planes
+    assert err <= 2e-6 * scale
+    assert e64 <= 1e-5 * scale
+
+
+def test_sharded_single_shard_is_plain_forward():
+    """P = 1: no ghosts, every row interior; identical to FlowGNN.forward
+    without the internal reorder (same CSR, same kernels)."""
+    cfg = dict(hidden_dim=128, num_layers=4, layer_type="GCN")
+    m = FlowGNN(input_dim=3, output_dim=7, **cfg)
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=1))
+    m = m.to(DEV).eval()
+    m.reorder = "0"
+    x, ei = grid_graph(30, 20, 10, device=DEV)
+    with torch.no_grad():
+        y = m(x, ei)
+    ys, lays = _sharded(m, x, ei, 1, ordered=False)
+    assert lays[0].n_ghost == 0 and lays[0].n_int == x.shape[0]
+    assert torch.equal(ys, y)
