@@ -92,6 +92,11 @@ def layer_bytes(n_rows, e_rows, H, gcn=False):
     return 4 * (2 * n_rows * H + (n_rows + 1) + e_rows + (n_rows if gcn else 0))
 
 
+def progress(msg):
+    """A progress line on stderr (stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -218,7 +223,9 @@ def main():
             el = t.item()
         return el
 
+    progress(f"headline workload ready: {N_local} nodes, {E_local} edges per GPU")
     elapsed = timed_loop(cache_graph=False, rec_into=launches)
+    progress(f"headline: {1e3 * elapsed / max(args.steps, 1):.2f} ms per step")
     elapsed_cached = timed_loop(cache_graph=True)
 
     # ---- roofline of the fused GCN layer kernel (this rank's launches)
@@ -295,12 +302,16 @@ def main():
             line["legs"][name] = eval_leg(name, dev, args.precision,
                                           steps=max(1, min(args.steps, 3 if heavy else 10)),
                                           warmup=1 if heavy else 2)
+            progress(f"leg {name}: {line['legs'][name]['ms_per_forward']} ms per forward")
     if rank == 0 and world == 1 and not args.no_graph:
         line["graph_build"] = graph_build_leg(dev, nx, ny, nz, not args.no_cpu)
+        progress("graph_build leg done")
     if rank == 0 and world == 1 and not args.no_train:
         line["train_step"] = train_leg(dev, args)
+        progress("train_step leg done")
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_leg(model, sd, cfg, args, dev)
+        progress("cpu_baseline leg done")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
