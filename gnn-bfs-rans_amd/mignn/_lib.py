@@ -30,6 +30,10 @@ SIGNATURES = {
     "mignn_csr_build": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_size_t, _P]),
     "mignn_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P, _P,
                              c_int64, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_linear_f16x3_prep_bytes": (c_size_t, [c_int, c_int]),
+    "mignn_linear_f16x3_prep": (c_int, [_P, c_int, c_int, _P, c_size_t, _P]),
+    "mignn_linear_f16x3": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,
+                                   _P, c_int64, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_input_proj": (c_int, [_P, c_int64, c_int, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_bn_fold": (c_int, [_P, _P, _P, _P, c_float, c_int, _P, _P, _P]),
     "mignn_gcn_aggregate": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,

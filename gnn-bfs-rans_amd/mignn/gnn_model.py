@@ -269,6 +269,36 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias=None, *, relu=False, residual=
     return out
 
 
+def f16x3_image(w: torch.Tensor) -> torch.Tensor:
+    """Split-fp16 image of W [n, k] for linear_f16x3 (mignn_linear_f16x3_prep)."""
+    L = _lib.lib()
+    w = w.detach().float().contiguous()
+    n, k = w.shape
+    img = torch.empty(L.mignn_linear_f16x3_prep_bytes(n, k), dtype=torch.uint8, device=w.device)
+    _lib.check(L.mignn_linear_f16x3_prep(_lib.ptr(w), n, k, _lib.ptr(img), img.numel(),
+                                         _stream(w)), "mignn_linear_f16x3_prep")
+    return img
+
+
+def linear_f16x3(a: torch.Tensor, img: torch.Tensor, n: int, bias=None, *, relu=False,
+                 residual=None, scale=None, shift=None, a2: Optional[torch.Tensor] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = epi([a | a2] @ w.T) in split-fp16 MFMA arithmetic (mignn_linear_f16x3);
+    `img` = f16x3_image(w), w [n, a.shape[1] + a2.shape[1]]."""
+    M, K1 = a.shape
+    K2 = 0 if a2 is None else a2.shape[1]
+    if out is None:
+        out = torch.empty((M, n), dtype=torch.float32, device=a.device)
+    flags = (EPI_BIAS if bias is not None else 0) | (EPI_RESIDUAL if residual is not None else 0) \
+        | (EPI_AFFINE if scale is not None else 0) | (EPI_RELU if relu else 0)
+    _lib.check(_lib.lib().mignn_linear_f16x3(
+        _lib.ptr(a), a.stride(0), M, K1, _lib.ptr(a2), 0 if a2 is None else a2.stride(0), K2,
+        _lib.ptr(img), n, _lib.ptr(bias), _lib.ptr(residual),
+        0 if residual is None else residual.stride(0), _lib.ptr(scale), _lib.ptr(shift), flags,
+        _lib.ptr(out), out.stride(0), _stream(a)), "mignn_linear_f16x3")
+    return out
+
+
 def bn_fold(bn: nn.BatchNorm1d) -> Tuple[torch.Tensor, torch.Tensor]:
     h = bn.num_features
     dev = bn.running_mean.device
@@ -616,6 +646,17 @@ class FlowGNN(nn.Module):
                 hit = self._prep[key] = make()
         return hit
 
+    def _mm(self, tag, i, srcs, w, a, bias=None, **kw):
+        """Node transform by W = w (w derived from the parameters `srcs`):
+        the split-fp16 GEMM (precision "f16x3") for the shapes the fused
+        kernels leave over (k or n > 128, n >= 64), its W image cached per
+        parameter version; exact fp32 MFMA (mignn_linear) otherwise."""
+        n, k = w.shape
+        if self.precision == "f16x3" and n >= 64 and (n > 128 or k > 128):
+            img = self._cached(tag, i, srcs, lambda: f16x3_image(w))
+            return linear_f16x3(a, img, n, bias, **kw)
+        return linear(a, w, bias, **kw)
+
     def _layer(self, i, layer, csr: Csr, x, out, rb: int, re: int, logits=None):
         """One conv + residual + BN + ReLU (gnn_model.py:162-192) for rows [rb, re).
         `x` holds every row the CSR references (own rows + halo rows).  GAT:
@@ -643,8 +684,8 @@ class FlowGNN(nn.Module):
                                                  x.stride(0), rb, re, H,
                                                  P(agg) - rb * agg.stride(0) * 4, agg.stride(0),
                                                  st), "mignn_gcn_aggregate")
-                linear(agg, w, b, relu=True, residual=x[rb:re], scale=scale, shift=shift,
-                       out=out[rb:re])
+                self._mm("w_gcn", i, (w,), w, agg, b, relu=True, residual=x[rb:re], scale=scale,
+                         shift=shift, out=out[rb:re])
         elif self.layer_type == "GIN":
             nn0, nn2 = layer.nn[0], layer.nn[2]
             eps = self._cached("eps", i, (layer.eps,), lambda: float(layer.eps.reshape(-1)[0]))
@@ -660,9 +701,9 @@ class FlowGNN(nn.Module):
                                              1.0 + eps, rb, re, H,
                                              P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st),
                        "mignn_sum_aggregate")
-            h1 = linear(agg, nn0.weight, nn0.bias, relu=True)
-            linear(h1, nn2.weight, nn2.bias, relu=True, residual=x[rb:re], scale=scale,
-                   shift=shift, out=out[rb:re])
+            h1 = self._mm("w_gin0", i, (nn0.weight,), nn0.weight, agg, nn0.bias, relu=True)
+            self._mm("w_gin2", i, (nn2.weight,), nn2.weight, h1, nn2.bias, relu=True,
+                     residual=x[rb:re], scale=scale, shift=shift, out=out[rb:re])
         elif self.layer_type == "GAT":
             wlog, wcat = self._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
                                       lambda: self._gat_weights(layer))
@@ -674,8 +715,8 @@ class FlowGNN(nn.Module):
                                              float(layer.negative_slope),
                                              P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st),
                        "mignn_gat_aggregate")
-            linear(agg, wcat, layer.bias, relu=True, residual=x[rb:re], scale=scale, shift=shift,
-                   out=out[rb:re])
+            self._mm("w_gat", i, (layer.lin.weight,), wcat, agg, layer.bias, relu=True,
+                     residual=x[rb:re], scale=scale, shift=shift, out=out[rb:re])
         elif self.layer_type == "Transformer":
             ts = (layer.lin_query.weight, layer.lin_query.bias, layer.lin_key.weight,
                   layer.lin_key.bias, layer.lin_value.weight, layer.lin_value.bias,
@@ -683,14 +724,14 @@ class FlowGNN(nn.Module):
             wqk, bqk, wout, bout = self._cached("tf", i, ts, lambda: self._tf_weights(layer))
             K1 = HEADS * H + HEADS
             qt = torch.empty((n, K1), dtype=torch.float32, device=x.device)
-            linear(x[rb:re], wqk, bqk, out=qt)
+            self._mm("w_tfq", i, ts, wqk, x[rb:re], bqk, out=qt)
             agg = torch.empty((n, K1), dtype=torch.float32, device=x.device)
             _lib.check(L.mignn_transformer_aggregate(
                 P(csr.row_ptr), P(csr.col), P(qt) - rb * qt.stride(0) * 4, qt.stride(0), P(x),
                 x.stride(0), rb, re, H, HEADS, 1.0 / math.sqrt(H),
                 P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st), "mignn_transformer_aggregate")
-            linear(agg, wout, bout, a2=x[rb:re], relu=True, residual=x[rb:re], scale=scale,
-                   shift=shift, out=out[rb:re])
+            self._mm("w_tfo", i, ts, wout, agg, bout, a2=x[rb:re], relu=True, residual=x[rb:re],
+                     scale=scale, shift=shift, out=out[rb:re])
         else:
             raise ValueError(f"Unknown layer type: {self.layer_type}")
 
@@ -751,13 +792,14 @@ class FlowGNN(nn.Module):
                                         P(out), out.stride(0), P(rows), _stream(x)),
                        "mignn_mlp_head")
             return
-        h1 = linear(x, l0.weight, l0.bias, relu=True, out=tmp)
-        h2 = linear(h1, l3.weight, l3.bias, relu=True, out=x)
-        h3 = linear(h2, l6.weight, l6.bias, relu=True)
+        mm = lambda j, l, a, **kw: self._mm("w_head", j, (l.weight,), l.weight, a, l.bias, **kw)  # noqa: E731
+        h1 = mm(0, l0, x, relu=True, out=tmp)
+        h2 = mm(1, l3, h1, relu=True, out=x)
+        h3 = mm(2, l6, h2, relu=True)
         if inv is None:
-            linear(h3, l8.weight, l8.bias, out=out)
+            mm(3, l8, h3, out=out)
             return
-        y = linear(h3, l8.weight, l8.bias)          # internal order -> caller order
+        y = mm(3, l8, h3)                           # internal order -> caller order
         _lib.check(_lib.lib().mignn_rows_gather(
             _lib.ptr(y), y.stride(0), _lib.ptr(inv), y.shape[0], y.shape[1], _lib.ptr(out),
             out.stride(0), _stream(y)), "mignn_rows_gather")

@@ -111,6 +111,25 @@ int mignn_linear(const float* a, int64_t lda, int64_t m, int k,
                  const float* scale, const float* shift, int flags,
                  float* c, int64_t ldc, void* stream);
 
+/* The same transform in split-fp16 MFMA arithmetic ("f16x3", ~2^-22 relative
+ * per product, 16x the f32 MFMA rate), for the shapes the fused layer kernels
+ * do not cover (k or n > 128: the H = 256 layers, GAT's head-mean GEMM,
+ * TransformerConv's Q~K / output GEMMs).  W [n, k + k2] is split once into a
+ * device image (mignn_linear_f16x3_prep_bytes(n, k + k2) bytes, 16-B aligned;
+ * fp16 hi/lo MFMA fragments + one scale exponent per output column); rebuild
+ * it whenever W changes.  A rows are scaled by an online per-row power of two
+ * (no pre-pass).  Same epilogue flags and layout rules as mignn_linear;
+ * k1, k2, lda, lda2 multiples of 4. */
+size_t mignn_linear_f16x3_prep_bytes(int n, int k);
+int mignn_linear_f16x3_prep(const float* w, int n, int k, void* img, size_t img_bytes,
+                            void* stream);
+int mignn_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1,
+                       const float* a2, int64_t lda2, int k2,
+                       const void* img, int n,
+                       const float* bias, const float* residual, int64_t ldr,
+                       const float* scale, const float* shift, int flags,
+                       float* c, int64_t ldc, void* stream);
+
 /* Linear(in_dim -> h) with in_dim <= 8 on the VALU (K too thin for MFMA):
  * input_proj, gnn_model.py:55, :159. */
 int mignn_input_proj(const float* x, int64_t n, int in_dim, const float* w, const float* b,
