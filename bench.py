@@ -86,6 +86,12 @@ def layer_flops(lt, n_rows, e_rows, H):
     return 18 * n_rows * H * H + 16 * e_rows * H          # Transformer (re-associated)
 
 
+def gemm_flops(lt, n_rows, H):
+    """The node-transform (MFMA GEMM) part of layer_flops; the rest is
+    edge-wise aggregation on the VALU."""
+    return {"GCN": 2, "GIN": 4, "GAT": 8, "Transformer": 18}[lt] * n_rows * H * H
+
+
 def layer_bytes(n_rows, e_rows, H, gcn=False):
     """Algorithmic HBM bytes of one fused layer: read x rows and write the
     output rows once, the CSR arrays once."""
@@ -441,21 +447,37 @@ def eval_leg(name, dev, precision, steps, warmup):
         fl = layer_flops(lt, n_rows, n_rows * e_rows / N, H)
         by = layer_bytes(n_rows, n_rows * e_rows / N, H, gcn=lt == "GCN")
         t_s = tot_ms / 1e3
-        t_comp, t_hbm = fl / F32_MFMA_PEAK, by / HBM_PEAK
+        g = gemm_flops(lt, n_rows, H)
+        if precision == "f16x3":
+            # the FlowGNN.precision "f16x3" GEMMs (every K or N > 128 transform:
+            # all of H = 256, GAT's head-mean GEMM): 3 f16 MFMAs per fp32
+            # product; the aggregation on the f32 VALU
+            t_comp = 3 * g / F16_MFMA_PEAK + (fl - g) / F32_MFMA_PEAK
+            arith = ("split-fp16 GEMMs (3 f16 MFMA per fp32 product, 2.5 PF) + f32 VALU "
+                     "aggregation (157 TF)")
+        else:
+            t_comp = fl / F32_MFMA_PEAK
+            arith = "exact fp32 (f32 MFMA GEMMs, f32 VALU aggregation)"
+        t_hbm = by / HBM_PEAK
         nl = len(launches)
+        mfma = t_comp >= t_hbm
         out["roofline"] = {
             "unit_of_timing": "one layer (all its launches: aggregation + MFMA GEMMs), HIP events",
-            "bound": "mfma" if t_comp >= t_hbm else "hbm",
-            "achieved": round(fl / t_s / 1e12, 3) if t_comp >= t_hbm else round(by / t_s / 1e9, 1),
-            "peak": round(F32_MFMA_PEAK / 1e12, 1) if t_comp >= t_hbm else HBM_PEAK / 1e9,
-            "unit": "TFLOP/s" if t_comp >= t_hbm else "GB/s",
+            "bound": "mfma" if mfma else "hbm",
+            "achieved": round(fl / t_s / 1e12, 3) if mfma else round(by / t_s / 1e9, 1),
+            # effective compute peak of this layer's flop mix (fp32-equivalent
+            # flops / t_comp) or HBM peak
+            "peak": round(fl / t_comp / 1e12, 1) if mfma else HBM_PEAK / 1e9,
+            "unit": "TFLOP/s" if mfma else "GB/s",
             "frac": round(max(t_comp, t_hbm) / t_s, 4),
             "avg_layer_ms": round(tot_ms / nl, 3), "layers_timed": nl,
+            "t_min_ms": {"compute": round(1e3 * t_comp / nl, 3), "hbm": round(1e3 * t_hbm / nl, 3)},
             "executed_flops_per_layer": int(fl / nl),
+            "gemm_flops_per_layer": int(g / nl),
             "reference_formulation_flops_per_layer": int(
                 (26 * N * H * H + 16 * E * H) if lt == "Transformer" else fl / nl),
             "algorithmic_bytes_per_layer": int(by / nl),
-            "arithmetic": "exact fp32 (f32 MFMA GEMMs, f32 VALU aggregation)",
+            "arithmetic": arith,
         }
     del model, x, ei
     torch.cuda.empty_cache()
@@ -625,9 +647,21 @@ def cpu_leg(model, sd, cfg, args, dev):
     from mignn.synthetic import grid_graph
 
     # every CPU this process may run on (its cpuset / affinity: the box's share
-    # of the host when the pool restricts it, else the whole machine)
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, threads or 1)
+    # of the host when the pool restricts it, else the whole machine); torch's
+    # CPU kernels do not scale to all hardware threads of a 2-socket host (256
+    # threads ran 3.6x slower than 16 in round 2), so the thread count is the
+    # fastest of a sweep up to that limit, timed on a small mesh
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    avail = max(1, avail or 1)
+    xs, eis = (t.cpu() for t in grid_graph(40, 40, 40, device=dev))
+    sweep = {}
+    for nt in sorted({c for c in (8, 16, 32, 64, 128, avail) if c <= avail}):
+        torch.set_num_threads(nt)
+        orc.flowgnn_forward(sd, cfg, xs, eis, None, dtype=torch.float32)
+        t0 = time.perf_counter()
+        orc.flowgnn_forward(sd, cfg, xs, eis, None, dtype=torch.float32)
+        sweep[nt] = round(time.perf_counter() - t0, 4)
+    threads = min(sweep, key=sweep.get)
     torch.set_num_threads(threads)
     cx, cy, cz = (int(v) for v in args.cpu_grid.split(","))
     xg, eig = grid_graph(cx, cy, cz, device=dev)
@@ -652,7 +686,8 @@ def cpu_leg(model, sd, cfg, args, dev):
     except OSError:
         pass
     return {"value": cfg["num_layers"] * ei.shape[1] / t, "unit": "edges/s", "cores": threads,
-            "os_cpu_count": os.cpu_count(),
+            "os_cpu_count": os.cpu_count(), "cpus_available": avail,
+            "thread_sweep_s_40x40x40": sweep,
             "kind": "port",
             "sample": f"{cfg['layer_type']} L{cfg['num_layers']} H{cfg['hidden_dim']} forward on "
                       f"the {cx}x{cy}x{cz} periodic mesh ({x.shape[0]} nodes, {ei.shape[1]} edges), "
