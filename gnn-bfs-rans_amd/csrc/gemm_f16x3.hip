@@ -20,12 +20,19 @@
 // the D fragment of lane (r, g) holds row r's columns 16cb + 4g + {0..3}: the
 // epilogue stores 16 B per lane.
 //
-// Tiling: 512 threads = 8 waves x 16 rows = 128 rows per block, 256 output
-// columns (16 column blocks) per block; W fragments of a k chunk (32 KB)
-// LDS-DMA'd once per block, double-buffered, one barrier per chunk; A loads
-// go straight to registers two chunks ahead.  Blocks of consecutive tiles
-// (the column tiles of a row tile first) share an XCD, so the A rows of the
-// column tiles are L2 hits.
+// Tiling: 512 threads = 8 waves x 16 RPW rows per block (RPW = 1: 128 rows,
+// two blocks per CU), 256 output columns (16 column blocks) per block; W
+// fragments of a k chunk (32 KB) LDS-DMA'd once per block, double-buffered,
+// one barrier per chunk; A loads go straight to registers two chunks ahead.
+// Blocks of consecutive tiles (the column tiles of a row tile first) share
+// an XCD, so the A rows of the column tiles are L2 hits.
+// Measured alternatives (scripts/gemm_bench.py, M = 2M rows, round 2):
+// RPW = 2 (half the W traffic), BN = 128, a 2x4 wave grid over a block-split
+// A image, and a persistent variant with 3-4-deep A prefetch across row
+// tiles were all 0-25 % slower than this form.  What mattered was the
+// compiler's wait placement: K-masking at load time, a conditional second
+// step of the unrolled pair, or an LDS-DMA issued before a wait the compiler
+// places made it wait for loads in flight (checked in the ISA).
 #include "common.hpp"
 
 namespace mignn {
@@ -36,8 +43,15 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int GW = 8;                 // waves per block
 constexpr int GNT = GW * 64;          // threads
-constexpr int GBM = 16 * GW;          // rows per block
-constexpr int CBT = 16;               // 16-column blocks per block
+#ifndef GEMM_RPW
+#define GEMM_RPW 1
+#endif
+constexpr int RPW = GEMM_RPW;         // 16-row blocks per wave
+constexpr int GBM = 16 * RPW * GW;    // rows per block
+#ifndef GEMM_CBT
+#define GEMM_CBT 16
+#endif
+constexpr int CBT = GEMM_CBT;         // 16-column blocks per block
 constexpr int GBN = 16 * CBT;         // columns per block
 constexpr int FRAG = 64 * 16;         // bytes of one fragment (64 lanes x 8 halfs)
 constexpr int CHUNK_BYTES = CBT * 2 * FRAG;   // one k chunk of a column tile: 32 KB
@@ -117,9 +131,10 @@ __global__ __launch_bounds__(256) void gprep_frag_kernel(const float* __restrict
 }
 
 // 8 A values of row `row` at k = kk..kk+7 from [A | A2] (k1 % 4 == 0: each
-// 4-float group lies in one segment); zeros past K.  Exactly one load per
-// group, also past K (a dummy read of k = 0): the chunk loop's vmcnt
-// bookkeeping counts on two loads per call.
+// 4-float group lies in one segment).  Exactly one load per group, also past
+// K (a dummy read of k = 0, which the caller zeroes when it consumes the
+// values -- masking here would make the compiler wait for the load at once):
+// the chunk loop's vmcnt bookkeeping counts on two loads per call.
 __device__ __forceinline__ void load_a8(const float* __restrict__ A, int64_t lda,
                                         const float* __restrict__ A2, int64_t lda2, int k1, int K,
                                         int64_t row, int kk, f32x4& lo4, f32x4& hi4) {
@@ -128,13 +143,12 @@ __device__ __forceinline__ void load_a8(const float* __restrict__ A, int64_t lda
         const int k = kk + 4 * h;
         const int kr = k < K ? k : 0;
         const float* p = kr < k1 ? A + row * lda + kr : A2 + row * lda2 + (kr - k1);
-        f32x4 v = *reinterpret_cast<const f32x4*>(p);
-        if (k >= K) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 v = *reinterpret_cast<const f32x4*>(p);   // past K: zeroed by the user
         if (h == 0) lo4 = v; else hi4 = v;
     }
 }
 
-__global__ __launch_bounds__(GNT, 2) void gemm_f16x3_kernel(
+__global__ __launch_bounds__(GNT, RPW == 1 ? 2 : 1) void gemm_f16x3_kernel(
     const float* __restrict__ A, int64_t lda, int64_t M, int k1, const float* __restrict__ A2,
     int64_t lda2, int K, const unsigned char* __restrict__ img, int kp, int npb, int N,
     const float* __restrict__ bias, const float* __restrict__ R, int64_t ldr,
@@ -154,9 +168,17 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f16x3_kernel(
     if (lin >= ntiles_m * ntiles_n) return;
     const int64_t tm = lin / ntiles_n;
     const int tn = static_cast<int>(lin - tm * ntiles_n);
-    const int64_t row0 = tm * GBM + 16 * wave;
-    const int64_t row = row0 + r;
-    const int64_t rowc = row < M ? row : M - 1;
+    // my two rows: RPW = 2 row blocks of 16 per wave
+    const int64_t row0 = tm * GBM + RPW * 16 * wave;
+    int64_t row[RPW], rowl[RPW];
+#pragma unroll
+    for (int h = 0; h < RPW; ++h) {
+        row[h] = row0 + 16 * h + r;
+        const int64_t rc = row[h] < M ? row[h] : M - 1;
+        // MIGNN_DIAG_NO_PRODUCE: the loads all read row 0 (L2 hits; not skipped
+        // -- a conditional load would make the compiler wait for it)
+        rowl[h] = (flags & MIGNN_DIAG_NO_PRODUCE) ? 0 : rc;
+    }
     const int cb0 = tn * CBT;                       // first column block of the tile
     const int ncb = min(CBT, (N + 15) / 16 - cb0);  // column blocks with columns (uniform)
 
@@ -186,76 +208,106 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f16x3_kernel(
         }
     };
 
-    f32x4 acc[CBT];
+    f32x4 acc[RPW][CBT];
 #pragma unroll
-    for (int i = 0; i < CBT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int p = 100;                                    // the row's running exponent
+    for (int h = 0; h < RPW; ++h)
+#pragma unroll
+        for (int i = 0; i < CBT; ++i) acc[h][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int p[RPW];                                     // the rows' running exponents
+#pragma unroll
+    for (int h = 0; h < RPW; ++h) p[h] = 100;
 
     // A chunks in two register buffers (even / odd chunks), the k loop
     // unrolled by two so no buffer is ever copied: a copy would wait for the
     // load in flight and serialise the HBM latency into every chunk
-    f32x4 xl, xh, yl, yh;
-    load_a8(A, lda, A2, lda2, k1, K, rowc, 8 * g, xl, xh);
-    load_a8(A, lda, A2, lda2, k1, K, rowc, 32 + 8 * g, yl, yh);
+    using AB = f32x4[RPW][2];
+    AB xa, ya;
+#pragma unroll
+    for (int h = 0; h < RPW; ++h) {
+        load_a8(A, lda, A2, lda2, k1, K, rowl[h], 8 * g, xa[h][0], xa[h][1]);
+        load_a8(A, lda, A2, lda2, k1, K, rowl[h], 32 + 8 * g, ya[h][0], ya[h][1]);
+    }
     w_dma(0);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0x70);              // vmcnt(0): chunk 0's W landed
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 
-    auto step = [&](int kc, f32x4& vl, f32x4& vh) {
-        w_dma(kc + 1);                              // next chunk's W, other buffer
-        // this chunk's 8 values of my row; the row max over its 4 lanes
-        uint32_t m = 0;
+    auto step = [&](int kc, AB& va) {
+        f16x8 bh[RPW], bl[RPW];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            m = max(m, max(__float_as_uint(fabsf(vl[j])), __float_as_uint(fabsf(vh[j]))));
-        m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), 16)));
-        m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), 32)));
-        const int pc = sexp(m);
-        if (pc < p) {                               // lower the row's scale: exact rescale
+        for (int h = 0; h < RPW; ++h) {
+            // this chunk's 8 values of row h (zero past K); the row max over its 4 lanes
+            f32x4 vl = va[h][0], vh = va[h][1];
+            if (32 * kc + 8 * g >= K) vl = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (32 * kc + 8 * g + 4 >= K) vh = f32x4{0.f, 0.f, 0.f, 0.f};
+            uint32_t m = 0;
 #pragma unroll
-            for (int i = 0; i < CBT; ++i)
+            for (int j = 0; j < 4; ++j)
+                m = max(m, max(__float_as_uint(fabsf(vl[j])), __float_as_uint(fabsf(vh[j]))));
+            m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), 16)));
+            m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), 32)));
+            const int pc = sexp(m);
+            if (pc < p[h]) {                        // lower the row's scale: exact rescale
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = ldexpf(acc[i][j], pc - p);
-            p = pc;
+                for (int i = 0; i < CBT; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[h][i][j] = ldexpf(acc[h][i][j], pc - p[h]);
+                p[h] = pc;
+            }
+            const float sp = p2(p[h]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = (j < 4 ? vl[j] : vh[j - 4]) * sp;
+                const _Float16 hh = static_cast<_Float16>(v);
+                bh[h][j] = hh;
+                bl[h][j] = static_cast<_Float16>(v - static_cast<float>(hh));
+            }
         }
-        const float sp = p2(p);
-        f16x8 bh, bl;
+        // next chunk's W into the other buffer -- after the split: the compiler
+        // does not count the DMA, so a wait it places for the split's registers
+        // must not have DMAs behind it
+        w_dma(kc + 1);
+        // the buffers are free: chunk kc+2 into them (2 loads per row, always issued)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float v = (j < 4 ? vl[j] : vh[j - 4]) * sp;
-            const _Float16 hh = static_cast<_Float16>(v);
-            bh[j] = hh;
-            bl[j] = static_cast<_Float16>(v - static_cast<float>(hh));
-        }
-        // the buffer is free: chunk kc+2 into it (two loads, always issued)
-        load_a8(A, lda, A2, lda2, k1, K, rowc, 32 * (kc + 2) + 8 * g, vl, vh);
+        for (int h = 0; h < RPW; ++h)
+            load_a8(A, lda, A2, lda2, k1, K, rowl[h], 32 * (kc + 2) + 8 * g, va[h][0], va[h][1]);
         const unsigned char* wb = lds + (kc & 1) * CHUNK_BYTES + lane * 16;
         // all CBT column blocks: the image pads a partial tile with zero columns
 #pragma unroll
         for (int cb = 0; cb < CBT; ++cb) {
+            if (flags & MIGNN_DIAG_NO_MFMA) break;
             const f16x8 wh = *reinterpret_cast<const f16x8*>(wb + (2 * cb) * FRAG);
             const f16x8 wl = *reinterpret_cast<const f16x8*>(wb + (2 * cb + 1) * FRAG);
-            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[cb], 0, 0, 0);
-            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, acc[cb], 0, 0, 0);
-            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, acc[cb], 0, 0, 0);
+#pragma unroll
+            for (int h = 0; h < RPW; ++h) {
+                acc[h][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh[h], acc[h][cb], 0, 0, 0);
+                acc[h][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl[h], acc[h][cb], 0, 0, 0);
+                acc[h][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh[h], acc[h][cb], 0, 0, 0);
+            }
         }
         // the next chunk's W must have landed before anyone reads it, and
         // every wave be done with this buffer before chunk kc+2 refills it;
-        // vmcnt(2): only the two A loads just issued may still fly
+        // vmcnt(2 RPW): only the A loads just issued may still fly
         asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_waitcnt(0x70 | 2);
+        __builtin_amdgcn_s_waitcnt(0x70 | (2 * RPW));
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    for (int kc = 0; kc < kp; kc += 2) {
-        step(kc, xl, xh);
-        if (kc + 1 < kp) step(kc + 1, yl, yh);
+    // (unconditional pairs: on the back edge the compiler then knows the
+    // explicit vmcnt has retired the buffer the next step reads)
+    int kc = 0;
+    for (; kc + 1 < kp; kc += 2) {
+        step(kc, xa);
+        step(kc + 1, ya);
     }
+    if (kc < kp) step(kc, xa);
 
-    // epilogue: D[n][row] in lane (r, g): columns 16cb + 4g + i of my row
-    if (row < M) {
+    // epilogue: D[n][row] in lane (r, g): columns 16cb + 4g + i of my rows
+    if (flags & MIGNN_DIAG_NO_EXT) return;
+#pragma unroll
+    for (int h = 0; h < RPW; ++h) {
+        if (row[h] >= M) continue;
 #pragma unroll
         for (int cb = 0; cb < CBT; ++cb) {
             if (cb < ncb) {
@@ -265,16 +317,17 @@ __global__ __launch_bounds__(GNT, 2) void gemm_f16x3_kernel(
                 const f32x4 bo = *reinterpret_cast<const f32x4*>(&BL[lc]);
                 const f32x4 so = *reinterpret_cast<const f32x4*>(&SL[lc]);
                 const f32x4 ho = *reinterpret_cast<const f32x4*>(&HL[lc]);
-                const float4 rv = (flags & MIGNN_EPI_RESIDUAL) ? ld4_masked(R + row * ldr, col, N)
-                                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 rv = (flags & MIGNN_EPI_RESIDUAL)
+                                      ? ld4_masked(R + row[h] * ldr, col, N)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
                 const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
                 const float res[4] = {rv.x, rv.y, rv.z, rv.w};
                 float o[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], res[i], so[i],
-                                    ho[i]);
-                float* dst = C + row * ldc + col;
+                    o[i] = epilogue(ldexpf(acc[h][cb][i], -(p[h] + qn[i])), flags, bo[i], res[i],
+                                    so[i], ho[i]);
+                float* dst = C + row[h] * ldc + col;
                 if (col + 4 <= N && (((uintptr_t)dst) & 15) == 0) {
                     *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
                 } else {
@@ -323,12 +376,21 @@ extern "C" int mignn_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1
                                   const float* residual, int64_t ldr, const float* scale,
                                   const float* shift, int flags, float* c, int64_t ldc,
                                   void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "linear_f16x3: unknown flags 0x%x", flags);
+    return mignn_diag_linear_f16x3(a, lda, m, k1, a2, lda2, k2, img, n, bias, residual, ldr, scale,
+                                   shift, flags, c, ldc, stream);
+}
+
+extern "C" int mignn_diag_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1,
+                                       const float* a2, int64_t lda2, int k2, const void* img,
+                                       int n, const float* bias, const float* residual,
+                                       int64_t ldr, const float* scale, const float* shift,
+                                       int flags, float* c, int64_t ldc, void* stream) {
     MIGNN_REQUIRE(m >= 0 && k1 > 0 && k2 >= 0 && n > 0, "linear_f16x3: bad sizes");
     MIGNN_REQUIRE(k1 % 4 == 0 && k2 % 4 == 0 && lda % 4 == 0 && (k2 == 0 || lda2 % 4 == 0),
                   "linear_f16x3: k and lda must be multiples of 4");
     MIGNN_REQUIRE(a && img && c && aligned16(a) && aligned16(img) && (k2 == 0 || (a2 && aligned16(a2))),
                   "linear_f16x3: null or unaligned operand");
-    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "linear_f16x3: unknown flags 0x%x", flags);
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bias, "linear_f16x3: bias flag without bias");
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_RESIDUAL) || residual, "linear_f16x3: residual flag without R");
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "linear_f16x3: affine w/o params");

@@ -116,6 +116,8 @@ SIGNATURES = {
 
 # diagnostic entry points (include/mignn_diag.h; timing studies only)
 DIAG_SIGNATURES = {
+    "mignn_diag_linear_f16x3": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P,
+                                        c_int, _P, _P, c_int64, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_diag_gather": (c_int, [c_int, _P, _P, _P, _P, c_int64, c_int, c_int, c_int, c_int, _P,
                                   _P]),
     "mignn_diag_set_trace": (c_int, [_P]),

@@ -35,6 +35,12 @@ int mignn_diag_linear(const float* a, int64_t lda, int64_t m, int k, const float
                       int64_t lda2, int k2, const float* w, int n, const float* bias,
                       const float* residual, int64_t ldr, const float* scale, const float* shift,
                       int flags, float* c, int64_t ldc, void* stream);
+/* mignn_linear_f16x3 with MIGNN_DIAG_NO_PRODUCE (no A loads), NO_MFMA (no
+ * MFMAs), NO_EXT (no C stores) */
+int mignn_diag_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1, const float* a2,
+                            int64_t lda2, int k2, const void* img, int n, const float* bias,
+                            const float* residual, int64_t ldr, const float* scale,
+                            const float* shift, int flags, float* c, int64_t ldc, void* stream);
 
 /* mode 0: CSR gather (h = 128); 1: stencil gather on the periodic grid;
  * 2: streaming copy.  blocks <= 0: one row group per row. */

@@ -7,7 +7,13 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "gnn-bfs-rans_amd"))
+from mignn import _lib  # noqa: E402
+
+if os.environ.get("GB_LIB"):                       # an alternative build (experiments)
+    _lib.LIB_PATH = os.environ["GB_LIB"]
 from mignn.gnn_model import f16x3_image, linear, linear_f16x3  # noqa: E402
+
+L, P = _lib.lib(), _lib.ptr
 
 M = int(os.environ.get("GB_M", 2_000_000))
 SHAPES = [  # (name, k1, k2, n, residual)
@@ -47,11 +53,20 @@ def main():
         c32 = out.clone()
         t16 = timeit(lambda: linear_f16x3(a, img, n, b, **kw))
         d = (out - c32).abs().max().item()
+        abl = {}
+        for nm, fl in (("no_A", 256), ("no_mfma", 512), ("no_store", 4096), ("no_A_mfma", 768),
+                       ("only_loop", 256 | 512 | 4096)):
+            flags = 1 | 8 | (2 if has_res else 0) | fl
+            abl[nm] = round(timeit(lambda: L.mignn_diag_linear_f16x3(
+                P(a), a.stride(0), M, k1, P(a2), a2.stride(0) if k2 else 0, k2, P(img), n, P(b),
+                P(res), res.stride(0) if has_res else 0, None, None, flags, P(out), out.stride(0),
+                _lib.stream())), 3)
         byts = 4 * M * (k1 + k2 + n + (n if has_res else 0))
         flops = 2 * M * (k1 + k2) * n
         print(f"{name:30s} M={M}: f32 {t32:8.3f} ms ({flops / t32 / 1e9:6.1f} TF)  "
               f"f16x3 {t16:8.3f} ms ({flops / t16 / 1e9:6.1f} TF, {byts / t16 / 1e6:6.0f} GB/s "
-              f"= {byts / t16 / 1e6 / 8000:.2f} of 8 TB/s)  max|f16x3-f32| {d:.2e}", flush=True)
+              f"= {byts / t16 / 1e6 / 8000:.2f} of 8 TB/s)  max|f16x3-f32| {d:.2e}  ablations {abl}",
+              flush=True)
         del a, a2, w, res, out, img, c32
         torch.cuda.empty_cache()
 
