@@ -3,19 +3,32 @@
 // degree), the synthetic periodic hex grid, the BatchNorm eval fold and the
 // halo row gather.
 //
-// CSR build (all on `stream`, no host sync):
-//   K0 csr_keys     : per edge, key = dst (valid, kept), N (dropped: invalid
-//                     index, or a self-loop in ONE_SELF_LOOP mode); value = src.
-//                     Counts kept / invalid edges with one atomic per block.
-//   K1 radix sort   : rocprim::radix_sort_pairs over the low ceil(log2(N+1))
-//                     bits -- stable, so in-row order == edge order.
-//   K2 row_bounds   : row_ptr0[i] = first sorted position with key >= i.
-//   K3 csr_expand   : final row_ptr/col; ONE_SELF_LOOP mode appends (i, i) to
+// CSR build (all on `stream`, no host sync): a counting sort by destination,
+// made deterministic and stable by a per-row sort on the edge index:
+//   K0 csr_count    : per edge, key = dst (valid, kept) or N (dropped: invalid
+//                     index, or a self-loop in ONE_SELF_LOOP mode), value = src
+//                     (both relabelled when a locality order is given);
+//                     deg[key]++ (atomic); kept / invalid counts, one atomic
+//                     per block.
+//   K1 scan         : row_ptr0 = exclusive prefix sum of deg (rocprim).
+//   K2 csr_scatter  : kept edge e -> slot row_ptr0[key] + (atomic fill index),
+//                     (edge index, value) stored there; a run of equal keys in
+//                     a wave takes consecutive slots with one atomic -- slot
+//                     order within a row is otherwise arbitrary here...
+//   K3 csr_finalize : ...and restored per row by sorting on the edge index
+//                     (already sorted: skipped; <= 16 entries: a register
+//                     network; longer: in memory): in-row order == edge order,
+//                     exactly as a stable sort by key.
+// K0 / K2 aggregate runs of equal keys in a wave into one atomic (a mesh edge
+// list keeps a node's edges together; same-address atomics serialise).
+//                     Final row_ptr / col; ONE_SELF_LOOP mode appends (i, i) to
 //                     every row and writes dinv = deg^-1/2; VERBATIM mode with
 //                     E > 0 and zero kept edges takes the reference's
 //                     all-invalid fallback (one self-loop per node,
 //                     gnn_model.py:144-149).
-#include <rocprim/device/device_radix_sort.hpp>
+// (Round 1 used a rocprim radix sort of (key, src) pairs for K1-K2: ~1.2 ms of
+// the 10M-node / 60M-edge build against ~0.4 ms for K1-K3 here.)
+#include <rocprim/device/device_scan.hpp>
 
 #include <cmath>
 #include <cstring>
@@ -37,20 +50,47 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__global__ void csr_keys_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t N, int mode,
-                                int transpose, const int32_t* __restrict__ relabel,
-                                uint32_t* __restrict__ keys, int32_t* __restrict__ vals,
-                                unsigned long long* __restrict__ counters) {
+// Runs of equal keys in consecutive lanes of a wave (mesh edge lists keep a
+// node's edges together): one atomic per run instead of per edge -- same-
+// address atomics of one wave serialise.  Returns whether this lane heads
+// its run; head_lane / run_len of the lane's run.  Every lane of the wave
+// must call it (inactive lanes with active = false).
+__device__ __forceinline__ bool wave_run(uint32_t key, bool active, int lane, int& head_lane,
+                                         int& run_len) {
+    const uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(key), 1));
+    const uint64_t act = __ballot(active);
+    const bool prev_active = lane > 0 && ((act >> (lane - 1)) & 1ull);
+    const bool head = active && (!prev_active || prev != key);
+    const uint64_t heads = __ballot(head);
+    const uint64_t below = heads & ((lane == 63) ? ~0ull : ((2ull << lane) - 1ull));
+    head_lane = below ? 63 - __clzll(static_cast<long long>(below)) : 0;
+    const uint64_t breaks = heads | ~act;               // a run ends before a head or an inactive lane
+    const uint64_t above = head_lane == 63 ? 0ull : (breaks & ~((2ull << head_lane) - 1ull));
+    run_len = (above ? __ffsll(static_cast<long long>(above)) - 1 : 64) - head_lane;
+    return head;
+}
+
+__global__ void csr_count_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t N, int mode,
+                                 int transpose, const int32_t* __restrict__ relabel,
+                                 uint32_t* __restrict__ keys, int32_t* __restrict__ vals,
+                                 int32_t* __restrict__ deg,
+                                 unsigned long long* __restrict__ counters) {
     __shared__ unsigned int s_kept, s_bad;
     if (threadIdx.x == 0) { s_kept = 0; s_bad = 0; }
     __syncthreads();
+    const int lane = threadIdx.x & 63;
     unsigned kept = 0, bad = 0;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        // transposed: rows keyed by the source (backward of the aggregation)
-        const int64_t s = ei[transpose ? E + e : e];
-        const int64_t d = ei[transpose ? e : E + e];
-        const bool valid = (s >= 0) & (s < N) & (d >= 0) & (d < N);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < E; base += stride) {
+        const int64_t e = base + threadIdx.x;           // uniform trip count: whole waves
+        const bool in = e < E;
+        int64_t s = -1, d = -1;
+        if (in) {
+            // transposed: rows keyed by the source (backward of the aggregation)
+            s = ei[transpose ? E + e : e];
+            d = ei[transpose ? e : E + e];
+        }
+        const bool valid = in & (s >= 0) & (s < N) & (d >= 0) & (d < N);
         bool keep = valid;
         if (mode == MIGNN_CSR_ONE_SELF_LOOP && s == d) keep = false;
         int64_t sn = s, dn = d;
@@ -58,10 +98,15 @@ __global__ void csr_keys_kernel(const int64_t* __restrict__ ei, int64_t E, int64
             sn = relabel[s];
             dn = relabel[d];
         }
-        keys[e] = keep ? static_cast<uint32_t>(dn) : static_cast<uint32_t>(N);
-        vals[e] = valid ? static_cast<int32_t>(sn) : 0;
+        const uint32_t key = keep ? static_cast<uint32_t>(dn) : static_cast<uint32_t>(N);
+        if (in) {
+            keys[e] = key;
+            vals[e] = valid ? static_cast<int32_t>(sn) : 0;
+        }
+        int hl, rl;
+        if (wave_run(key, keep, lane, hl, rl)) atomicAdd(&deg[key], rl);
         kept += keep ? 1u : 0u;
-        bad += valid ? 0u : 1u;
+        bad += (in && !valid) ? 1u : 0u;
     }
     if (kept) atomicAdd(&s_kept, kept);
     if (bad) atomicAdd(&s_bad, bad);
@@ -72,54 +117,149 @@ __global__ void csr_keys_kernel(const int64_t* __restrict__ ei, int64_t E, int64
     }
 }
 
-// row_ptr0[i] = lower_bound(keys, i) for i in [0, N]; keys sorted, capped at N.
-__global__ void row_bounds_kernel(const uint32_t* __restrict__ keys, int64_t E, int64_t N,
-                                  int32_t* __restrict__ row_ptr0) {
-    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= E;
-         p += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t prev = (p == 0) ? -1 : (int64_t)min<uint32_t>(keys[p - 1], (uint32_t)N);
-        const int64_t cur = (p == E) ? N : (int64_t)min<uint32_t>(keys[p], (uint32_t)N);
-        for (int64_t i = prev + 1; i <= cur; ++i) row_ptr0[i] = static_cast<int32_t>(p);
-    }
-}
-
-__global__ void csr_expand_nodes_kernel(const int32_t* __restrict__ row_ptr0,
-                                        const int32_t* __restrict__ sorted_src, int64_t E,
-                                        int64_t N, int mode,
-                                        const unsigned long long* __restrict__ counters,
-                                        int32_t* __restrict__ row_ptr, int32_t* __restrict__ col,
-                                        float* __restrict__ dinv) {
-    const bool fallback = (mode == MIGNN_CSR_VERBATIM) && (E > 0) && (counters[0] == 0);
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= N;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        if (mode == MIGNN_CSR_ONE_SELF_LOOP) {
-            const int32_t b = row_ptr0[i];
-            row_ptr[i] = b + static_cast<int32_t>(i);
-            if (i < N) {
-                const int32_t e = row_ptr0[i + 1];
-                const int32_t base = b + static_cast<int32_t>(i);
-                for (int32_t t = b; t < e; ++t) col[base + (t - b)] = sorted_src[t];
-                col[base + (e - b)] = static_cast<int32_t>(i);
-                // PyG gcn_norm: deg.pow(-0.5); deg >= 1 here (self-loop added).
-                if (dinv) dinv[i] = 1.0f / sqrtf(static_cast<float>(e - b + 1));
-            }
-        } else if (fallback) {
-            row_ptr[i] = static_cast<int32_t>(i);
-            if (i < N) col[i] = static_cast<int32_t>(i);
-        } else {
-            row_ptr[i] = row_ptr0[i];
+// kept edge e -> its slot in the final col array (row_ptr0[key] + fill index,
+// + key in ONE_SELF_LOOP mode: every earlier row gains its self-loop); a run
+// of equal keys takes consecutive slots in edge order with one atomic, so a
+// row filled by ONE run is in edge order already -- rows filled by several
+// runs are flagged for csr_finalize's sort
+__global__ void csr_scatter_kernel(const uint32_t* __restrict__ keys,
+                                   const int32_t* __restrict__ vals, int64_t E, int64_t N,
+                                   int one_loop, const int32_t* __restrict__ row_ptr0,
+                                   int32_t* __restrict__ fill, int32_t* __restrict__ slot_eid,
+                                   int32_t* __restrict__ col, uint8_t* __restrict__ unsorted) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < E; base += stride) {
+        const int64_t e = base + threadIdx.x;
+        const bool in = e < E;
+        const uint32_t k = in ? keys[e] : static_cast<uint32_t>(N);
+        const bool keep = k < static_cast<uint32_t>(N);
+        int hl, rl;
+        int32_t pos0 = 0;
+        if (wave_run(k, keep, lane, hl, rl)) {
+            const int32_t b = row_ptr0[k];
+            pos0 = b + atomicAdd(&fill[k], rl);
+            if (rl != row_ptr0[k + 1] - b) unsorted[k] = 1;
+        }
+        pos0 = __shfl(pos0, hl);
+        if (keep) {
+            const int32_t pos = pos0 + (lane - hl);
+            slot_eid[pos] = static_cast<int32_t>(e);
+            col[pos + (one_loop ? static_cast<int32_t>(k) : 0)] = vals[e];
         }
     }
 }
 
-__global__ void copy_i32_kernel(const int32_t* __restrict__ src, int32_t* __restrict__ dst,
-                                const int32_t* __restrict__ count_at, int64_t E,
-                                const unsigned long long* __restrict__ counters, int mode) {
-    if (mode != MIGNN_CSR_VERBATIM || (E > 0 && counters[0] == 0)) return;
-    const int64_t n = *count_at;
-    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
-         p += (int64_t)gridDim.x * blockDim.x)
-        dst[p] = src[p];
+// in-place sort of (eid, val)[b, e) by eid (distinct).  Short rows (the mesh
+// case) in registers by an odd-even transposition network over 16 slots;
+// longer rows by insertion sort (<= 64) or heap sort in memory.
+__device__ void sort_row(int32_t* __restrict__ ke, int32_t* __restrict__ kv, int b, int e) {
+    // kv = values at the same positions as ke (a shifted view of col)
+    const int n = e - b;
+    if (n <= 1) return;
+    if (n <= 16) {
+        int32_t K[16], V[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            K[t] = t < n ? ke[b + t] : 0x7fffffff;
+            V[t] = t < n ? kv[b + t] : 0;
+        }
+#pragma unroll
+        for (int round = 0; round < 16; ++round) {
+#pragma unroll
+            for (int t = round & 1; t + 1 < 16; t += 2) {
+                const bool sw = K[t] > K[t + 1];
+                const int32_t k0 = sw ? K[t + 1] : K[t], k1 = sw ? K[t] : K[t + 1];
+                const int32_t v0 = sw ? V[t + 1] : V[t], v1 = sw ? V[t] : V[t + 1];
+                K[t] = k0; K[t + 1] = k1; V[t] = v0; V[t + 1] = v1;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            if (t < n) {
+                ke[b + t] = K[t];
+                kv[b + t] = V[t];
+            }
+        return;
+    }
+    if (n <= 64) {
+        for (int a = b + 1; a < e; ++a) {
+            const int32_t k = ke[a], v = kv[a];
+            int c = a - 1;
+            while (c >= b && ke[c] > k) {
+                ke[c + 1] = ke[c];
+                kv[c + 1] = kv[c];
+                --c;
+            }
+            ke[c + 1] = k;
+            kv[c + 1] = v;
+        }
+        return;
+    }
+    int32_t* const K = ke + b;
+    int32_t* const V = kv + b;
+    auto sift = [&](int root, int end) {
+        while (true) {
+            int child = 2 * root + 1;
+            if (child >= end) break;
+            if (child + 1 < end && K[child + 1] > K[child]) ++child;
+            if (K[root] >= K[child]) break;
+            const int32_t tk = K[root], tv = V[root];
+            K[root] = K[child];
+            V[root] = V[child];
+            K[child] = tk;
+            V[child] = tv;
+            root = child;
+        }
+    };
+    for (int r = n / 2 - 1; r >= 0; --r) sift(r, n);
+    for (int end = n - 1; end > 0; --end) {
+        const int32_t tk = K[0], tv = V[0];
+        K[0] = K[end];
+        V[0] = V[end];
+        K[end] = tk;
+        V[end] = tv;
+        sift(0, end);
+    }
+}
+
+// per row: the flagged rows' sort (slot_eid, col), row_ptr, the self-loop
+// entry and dinv (ONE_SELF_LOOP); ew (optional) = the PyG gcn_norm weights
+// dinv[src] * dinv[i], dinv[j] = (deg_j + 1)^-1/2 from row_ptr0
+__global__ void csr_finalize_kernel(const int32_t* __restrict__ row_ptr0,
+                                    int32_t* __restrict__ slot_eid,
+                                    const uint8_t* __restrict__ unsorted, int64_t E, int64_t N,
+                                    int mode, const unsigned long long* __restrict__ counters,
+                                    int32_t* __restrict__ row_ptr, int32_t* __restrict__ col,
+                                    float* __restrict__ dinv, float* __restrict__ ew) {
+    const bool fallback = (mode == MIGNN_CSR_VERBATIM) && (E > 0) && (counters[0] == 0);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= N;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (fallback) {
+            row_ptr[i] = static_cast<int32_t>(i);
+            if (i < N) col[i] = static_cast<int32_t>(i);
+            continue;
+        }
+        const int32_t b = row_ptr0[i];
+        const int32_t off = mode == MIGNN_CSR_ONE_SELF_LOOP ? static_cast<int32_t>(i) : 0;
+        row_ptr[i] = b + off;
+        if (i == N) continue;
+        const int32_t e = row_ptr0[i + 1];
+        if (unsorted[i]) sort_row(slot_eid, col + off, b, e);
+        if (mode == MIGNN_CSR_ONE_SELF_LOOP) {
+            col[e + off] = static_cast<int32_t>(i);
+            // PyG gcn_norm: deg.pow(-0.5); deg >= 1 here (self-loop added).
+            const float di = 1.0f / sqrtf(static_cast<float>(e - b + 1));
+            if (dinv) dinv[i] = di;
+            if (ew) {
+                for (int32_t t = b + off; t < e + off; ++t) {
+                    const int32_t j = col[t];
+                    ew[t] = 1.0f / sqrtf(static_cast<float>(row_ptr0[j + 1] - row_ptr0[j] + 1)) * di;
+                }
+                ew[e + off] = di * di;
+            }
+        }
+    }
 }
 
 __global__ void csr_info_kernel(const unsigned long long* __restrict__ counters,
@@ -135,33 +275,29 @@ __global__ void csr_info_kernel(const unsigned long long* __restrict__ counters,
 
 inline size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 
-inline unsigned key_bits(int64_t N) {
-    unsigned bits = 1;
-    while ((uint64_t(1) << bits) <= static_cast<uint64_t>(N)) ++bits;
-    return bits;
-}
-
 struct CsrScratch {
-    size_t off_keys_in, off_keys_out, off_vals_in, off_vals_out, off_rowptr0, off_counters,
-        off_temp, temp_bytes, total;
+    size_t off_keys, off_vals, off_slot_eid, off_deg, off_fill, off_unsorted, off_rowptr0,
+        off_counters, off_temp, temp_bytes, total;
 };
 
 int csr_layout(int64_t E, int64_t N, CsrScratch* L) {
     size_t o = 0;
     const size_t e = static_cast<size_t>(E > 0 ? E : 1);
-    L->off_keys_in = o; o = align_up(o + e * 4);
-    L->off_keys_out = o; o = align_up(o + e * 4);
-    L->off_vals_in = o; o = align_up(o + e * 4);
-    L->off_vals_out = o; o = align_up(o + e * 4);
-    L->off_rowptr0 = o; o = align_up(o + static_cast<size_t>(N + 1) * 4);
+    const size_t n1 = static_cast<size_t>(N + 1);
+    L->off_keys = o; o = align_up(o + e * 4);
+    L->off_vals = o; o = align_up(o + e * 4);
+    L->off_slot_eid = o; o = align_up(o + e * 4);
+    L->off_deg = o; o = align_up(o + n1 * 4);       // deg | fill | unsorted: one memset
+    L->off_fill = o; o = align_up(o + n1 * 4);
+    L->off_unsorted = o; o = align_up(o + n1);
+    L->off_rowptr0 = o; o = align_up(o + n1 * 4);
     L->off_counters = o; o = align_up(o + 4 * sizeof(unsigned long long));
     L->off_temp = o;
     size_t temp = 0;
-    hipError_t err = rocprim::radix_sort_pairs(nullptr, temp, (uint32_t*)nullptr,
-                                               (uint32_t*)nullptr, (int32_t*)nullptr,
-                                               (int32_t*)nullptr, static_cast<size_t>(e), 0u, key_bits(N));
+    hipError_t err = rocprim::exclusive_scan(nullptr, temp, (int32_t*)nullptr, (int32_t*)nullptr,
+                                             0, n1, rocprim::plus<int32_t>());
     if (err != hipSuccess) {
-        set_error("rocprim::radix_sort_pairs size query: %s", hipGetErrorString(err));
+        set_error("rocprim::exclusive_scan size query: %s", hipGetErrorString(err));
         return MIGNN_ERR_HIP;
     }
     L->temp_bytes = temp;
@@ -274,6 +410,14 @@ extern "C" int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t E, i
                                          int mode, const int32_t* relabel, int32_t* row_ptr,
                                          int32_t* col, float* dinv, int64_t* info, void* scratch,
                                          size_t scratch_bytes, void* stream_) {
+    return mignn_csr_build_gcn(edge_index, E, N, mode, relabel, row_ptr, col, dinv, nullptr, info,
+                               scratch, scratch_bytes, stream_);
+}
+
+extern "C" int mignn_csr_build_gcn(const int64_t* edge_index, int64_t E, int64_t N, int mode,
+                                   const int32_t* relabel, int32_t* row_ptr, int32_t* col,
+                                   float* dinv, float* ew, int64_t* info, void* scratch,
+                                   size_t scratch_bytes, void* stream_) {
     MIGNN_REQUIRE(N >= 0 && E >= 0, "csr_build: negative sizes (E=%lld N=%lld)", (long long)E,
                   (long long)N);
     MIGNN_REQUIRE(E + N < (int64_t(1) << 31) - 1, "csr_build: E+N exceeds int32 CSR range");
@@ -283,6 +427,7 @@ extern "C" int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t E, i
                   "csr_build: bad mode %d", mode);
     MIGNN_REQUIRE(row_ptr && col && scratch && (E == 0 || edge_index),
                   "csr_build: null pointer");
+    MIGNN_REQUIRE(!ew || mode == MIGNN_CSR_ONE_SELF_LOOP, "csr_build: ew needs ONE_SELF_LOOP mode");
     hipStream_t st = as_stream(stream_);
     CsrScratch L;
     int rc = csr_layout(E, N, &L);
@@ -292,40 +437,39 @@ extern "C" int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t E, i
         return MIGNN_ERR_SCRATCH;
     }
     char* base = static_cast<char*>(scratch);
-    uint32_t* keys_in = reinterpret_cast<uint32_t*>(base + L.off_keys_in);
-    uint32_t* keys_out = reinterpret_cast<uint32_t*>(base + L.off_keys_out);
-    int32_t* vals_in = reinterpret_cast<int32_t*>(base + L.off_vals_in);
-    int32_t* vals_out = reinterpret_cast<int32_t*>(base + L.off_vals_out);
-    int32_t* row_ptr0 = reinterpret_cast<int32_t*>(base + L.off_rowptr0);
+    auto* keys = reinterpret_cast<uint32_t*>(base + L.off_keys);
+    auto* vals = reinterpret_cast<int32_t*>(base + L.off_vals);
+    auto* slot_eid = reinterpret_cast<int32_t*>(base + L.off_slot_eid);
+    auto* unsorted = reinterpret_cast<uint8_t*>(base + L.off_unsorted);
+    auto* deg = reinterpret_cast<int32_t*>(base + L.off_deg);
+    auto* fill = reinterpret_cast<int32_t*>(base + L.off_fill);
+    auto* row_ptr0 = reinterpret_cast<int32_t*>(base + L.off_rowptr0);
     auto* counters = reinterpret_cast<unsigned long long*>(base + L.off_counters);
+    MIGNN_HIP(hipMemsetAsync(deg, 0, L.off_rowptr0 - L.off_deg, st));   // deg, fill, unsorted
     MIGNN_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), st));
     if (E > 0) {
-        hipLaunchKernelGGL(csr_keys_kernel, dim3(grid_for(E, kBlock, 4096)), dim3(kBlock), 0, st,
-                           edge_index, E, N, mode, transpose, relabel, keys_in, vals_in,
-                           counters);
-        if ((rc = launch_status("csr_keys_kernel"))) return rc;
-        const unsigned bits = key_bits(N);
-        size_t temp = L.temp_bytes;
-        hipError_t err = rocprim::radix_sort_pairs(base + L.off_temp, temp, keys_in, keys_out,
-                                                   vals_in, vals_out, static_cast<size_t>(E), 0u,
-                                                   bits, st);
-        if (err != hipSuccess) {
-            set_error("rocprim::radix_sort_pairs: %s", hipGetErrorString(err));
-            return MIGNN_ERR_HIP;
-        }
+        hipLaunchKernelGGL(csr_count_kernel, dim3(grid_for(E, kBlock, 8192)), dim3(kBlock), 0, st,
+                           edge_index, E, N, mode, transpose, relabel, keys, vals, deg, counters);
+        if ((rc = launch_status("csr_count_kernel"))) return rc;
     }
-    hipLaunchKernelGGL(row_bounds_kernel, dim3(grid_for(E + 1, kBlock, 65536)), dim3(kBlock), 0,
-                       st, keys_out, E, N, row_ptr0);
-    if ((rc = launch_status("row_bounds_kernel"))) return rc;
-    hipLaunchKernelGGL(csr_expand_nodes_kernel, dim3(grid_for(N + 1, kBlock, 65536)),
-                       dim3(kBlock), 0, st, row_ptr0, vals_out, E, N, mode, counters, row_ptr,
-                       col, dinv);
-    if ((rc = launch_status("csr_expand_nodes_kernel"))) return rc;
-    if (mode == MIGNN_CSR_VERBATIM && E > 0) {
-        hipLaunchKernelGGL(copy_i32_kernel, dim3(grid_for(E, kBlock, 65536)), dim3(kBlock), 0,
-                           st, vals_out, col, row_ptr0 + N, E, counters, mode);
-        if ((rc = launch_status("copy_i32_kernel"))) return rc;
+    size_t temp = L.temp_bytes;
+    hipError_t err = rocprim::exclusive_scan(base + L.off_temp, temp, deg, row_ptr0, 0,
+                                             static_cast<size_t>(N + 1),
+                                             rocprim::plus<int32_t>(), st);
+    if (err != hipSuccess) {
+        set_error("rocprim::exclusive_scan: %s", hipGetErrorString(err));
+        return MIGNN_ERR_HIP;
     }
+    if (E > 0) {
+        hipLaunchKernelGGL(csr_scatter_kernel, dim3(grid_for(E, kBlock, 8192)), dim3(kBlock), 0,
+                           st, keys, vals, E, N, mode == MIGNN_CSR_ONE_SELF_LOOP ? 1 : 0, row_ptr0,
+                           fill, slot_eid, col, unsorted);
+        if ((rc = launch_status("csr_scatter_kernel"))) return rc;
+    }
+    hipLaunchKernelGGL(csr_finalize_kernel, dim3(grid_for(N + 1, kBlock, 65536)), dim3(kBlock), 0,
+                       st, row_ptr0, slot_eid, unsorted, E, N, mode, counters, row_ptr, col, dinv,
+                       ew);
+    if ((rc = launch_status("csr_finalize_kernel"))) return rc;
     if (info) {
         hipLaunchKernelGGL(csr_info_kernel, dim3(1), dim3(64), 0, st, counters, row_ptr, E, N,
                            mode, info);

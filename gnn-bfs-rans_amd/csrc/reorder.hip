@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kB) void spacing_kernel(const float* __restrict__ p
     for (int a = 0; a < 3; ++a) ext[a] = ord2f(st->hi[a]) - ord2f(st->lo[a]);
     double sum[3] = {0.0, 0.0, 0.0};
     unsigned long long cnt[3] = {0ull, 0ull, 0ull};
-    const int64_t ns = E < (int64_t(1) << 22) ? E : (int64_t(1) << 22);
+    const int64_t ns = E < (int64_t(1) << 18) ? E : (int64_t(1) << 18);
     for (int64_t t = blockIdx.x * (int64_t)kB + threadIdx.x; t < ns; t += (int64_t)gridDim.x * kB) {
         const int64_t e = ns == E ? t : (t * E) / ns;   // evenly strided sample
         const int64_t s = ei[e], d = ei[E + e];
@@ -274,9 +274,9 @@ extern "C" int mignn_locality_order(const float* pos, int64_t ldp, int64_t n,
                        stats);
     if ((rc = launch_status("bbox_kernel"))) return rc;
     if (E > 0) {
-        // the spacing is a mean over edges: a strided sample of <= 2^22 edges
+        // the spacing is a mean over edges: a strided sample of <= 2^18 edges
         // (every edge when fewer) is plenty and keeps the gathers off the step
-        hipLaunchKernelGGL(spacing_kernel, dim3(grid_for(E < (1 << 22) ? E : (1 << 22), kB, 1024)),
+        hipLaunchKernelGGL(spacing_kernel, dim3(grid_for(E < (1 << 18) ? E : (1 << 18), kB, 1024)),
                            dim3(kB), 0, st, pos, ldp, n, edge_index, E, stats);
         if ((rc = launch_status("spacing_kernel"))) return rc;
     }

@@ -52,6 +52,8 @@ SIGNATURES = {
     "mignn_mlp_head_prep": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int, c_int, _P, c_size_t,
                                     _P]),
     "mignn_mlp_head": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int, _P, c_int64, _P, _P]),
+    "mignn_csr_build_gcn": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P, _P,
+                                    c_size_t, _P]),
     "mignn_csr_build_relabeled": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
                                           c_size_t, _P]),
     "mignn_locality_order_scratch_bytes": (c_size_t, [c_int64]),

@@ -189,14 +189,13 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int,
     if nbytes == 0:
         raise _lib.MignnError("csr scratch query failed: " + _lib.last_error())
     scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    _lib.check(L.mignn_csr_build_relabeled(_lib.ptr(ei), E, N, mode, _lib.ptr(relabel),
-                                           _lib.ptr(row_ptr), _lib.ptr(col), _lib.ptr(dinv),
-                                           _lib.ptr(info), _lib.ptr(scratch), nbytes,
-                                           _lib.stream(dev)), "mignn_csr_build")
-    csr = Csr(row_ptr, col, dinv, info, N, E, ei)
-    if mode == CSR_ONE_SELF_LOOP:
-        csr.compute_gcn_weights()
-    return csr
+    # ONE_SELF_LOOP: the gcn_norm weights come out of the same pass
+    ew = torch.empty_like(col, dtype=torch.float32) if mode == CSR_ONE_SELF_LOOP else None
+    _lib.check(L.mignn_csr_build_gcn(_lib.ptr(ei), E, N, mode, _lib.ptr(relabel),
+                                     _lib.ptr(row_ptr), _lib.ptr(col), _lib.ptr(dinv), _lib.ptr(ew),
+                                     _lib.ptr(info), _lib.ptr(scratch), nbytes,
+                                     _lib.stream(dev)), "mignn_csr_build")
+    return Csr(row_ptr, col, dinv, info, N, E, ei, ew=ew)
 
 
 class _CsrCache:

@@ -70,6 +70,14 @@ int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t num_edges, int6
                               int mode, const int32_t* relabel, int32_t* row_ptr, int32_t* col,
                               float* dinv, int64_t* info, void* scratch, size_t scratch_bytes,
                               void* stream);
+/* As mignn_csr_build_relabeled; in ONE_SELF_LOOP mode `ew` (nullable, one
+ * float per CSR entry) also receives the PyG gcn_norm weights of
+ * mignn_gcn_norm over all rows (bit-identical: dinv[src] * dinv[i]) -- the
+ * GCN forward's CSR in one pass. */
+int mignn_csr_build_gcn(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, int mode,
+                        const int32_t* relabel, int32_t* row_ptr, int32_t* col, float* dinv,
+                        float* ew, int64_t* info, void* scratch, size_t scratch_bytes,
+                        void* stream);
 
 /* Locality order of the nodes for the internal activation layout (no
  * reference counterpart: the forward's results are the same up to fp32

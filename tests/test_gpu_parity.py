@@ -68,6 +68,15 @@ def _edge_sets():
     sets["random_invalid"] = (ei, 1000)
     ei = torch.randint(0, 50, (2, 5000), generator=g)   # heavy duplicates, hub rows
     sets["dense_dups"] = (ei, 60)
+    # rows of ~30 entries from scattered edges (in-memory insertion-sort path),
+    # many waves / blocks per row
+    ei = torch.randint(0, 5000, (2, 150000), generator=g)
+    sets["mid_degree"] = (ei, 5000)
+    # a mesh edge list (a node's edges consecutive: one run per row) with every
+    # 7th edge moved to the end (rows split over runs and waves)
+    ei = torch.from_numpy(grid_graph_np(12, 10, 9)[1])
+    sel = torch.arange(ei.shape[1]) % 7 == 3
+    sets["mesh_split_runs"] = (torch.cat([ei[:, ~sel], ei[:, sel]], 1), 12 * 10 * 9)
     return sets
 
 
@@ -84,6 +93,27 @@ def test_csr_build_bit_exact(mode):
         if mode == _lib.CSR_ONE_SELF_LOOP:
             deg = np.diff(rp)
             np.testing.assert_allclose(csr.dinv.cpu().numpy()[:n], 1 / np.sqrt(deg), rtol=2e-7)
+
+
+@pytest.mark.parametrize("mode", [_lib.CSR_VERBATIM, _lib.CSR_ONE_SELF_LOOP])
+def test_csr_build_relabeled_and_transposed(mode):
+    """relabel (a permutation of the node ids) and the transposed build equal
+    the CPU restatement on the mapped / reversed edge list."""
+    g = torch.Generator().manual_seed(7)
+    n = 3000
+    ei = torch.randint(-2, n + 2, (2, 40000), generator=g)
+    perm = torch.randperm(n, generator=g).to(torch.int32)
+    valid = (ei >= 0).all(0) & (ei < n).all(0)
+    mapped = ei.clone()
+    mapped[:, valid] = perm[ei[:, valid]].long()
+    csr = build_csr(ei.to(DEV), n, mode, relabel=perm.to(DEV))
+    rp, col = csr_np(mapped.numpy(), n, mode == _lib.CSR_ONE_SELF_LOOP)
+    assert np.array_equal(csr.row_ptr.cpu().numpy(), rp)
+    assert np.array_equal(csr.col[: rp[-1]].cpu().numpy(), col)
+    csr_t = build_csr(ei.to(DEV), n, mode | _lib.CSR_TRANSPOSE)
+    rp, col = csr_np(ei.flip(0).numpy(), n, mode == _lib.CSR_ONE_SELF_LOOP)
+    assert np.array_equal(csr_t.row_ptr.cpu().numpy(), rp)
+    assert np.array_equal(csr_t.col[: rp[-1]].cpu().numpy(), col)
 
 
 # ------------------------------------------------------------------ dense transforms
