@@ -100,6 +100,14 @@ struct SCfg {
     static constexpr int OFF_CNT = OFF_EPI + 3 * H * 4;             // cntX, cntA
     static constexpr int LDS_BYTES = OFF_CNT + 16;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+    // records mode (layer 1 from layer-0 records, gcn_layer0.hip): the
+    // expansion coefficients [H][8] after everything else
+    static constexpr int OFF_COEF = LDS_BYTES;
+    static constexpr int LDS_BYTES_REC = OFF_COEF + H * 32;
+    static_assert(LDS_BYTES_REC <= 160 * 1024, "LDS budget (records mode)");
+    static constexpr int CPL = H / 4;              // consumer expansion: lanes per row (16-B chunk each)
+    static constexpr int RG = 64 / CPL;            // rows per expansion instruction
+    static constexpr int RPL = 16 / RG;            // rows per lane (a consumer expands 16 rows)
     static_assert(NPIECE % NCW == 0, "DMA pieces per consumer");
     static_assert(NQD == 2, "two row quads per producer wave");
     static_assert(PROWS * LTS % 2 == 0 && PROWS * LTS / 2 <= 64 && PROWS * ETS <= 64, "tables");
@@ -157,6 +165,23 @@ __device__ __forceinline__ uint32_t row_max_u32(uint32_t v) {
 
 __device__ __forceinline__ f32x4 mfma16x16x32h(f16x8 a, f16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// Records mode: a layer-0 output element from its row's record r[0..6] (the
+// layer-0 aggregates c_i | C_i | s_i, gcn_layer0.hip) and its column's
+// coefficients ca | cb (cb[3] = the bias e): relu(e + sum_k coef_k r_k) in
+// gcn_layer0_kernel's fma order -- bit-identical to the materialised row.
+__device__ __forceinline__ float expand1(const f32x4& ca, const f32x4& cb, const f32x4& ra,
+                                         const f32x4& rb) {
+    float t = cb[3];
+    t = fmaf(ca[0], ra[0], t);
+    t = fmaf(ca[1], ra[1], t);
+    t = fmaf(ca[2], ra[2], t);
+    t = fmaf(ca[3], ra[3], t);
+    t = fmaf(cb[0], rb[0], t);
+    t = fmaf(cb[1], rb[1], t);
+    t = fmaf(cb[2], rb[2], t);
+    return t < 0.f ? 0.f : t;
 }
 
 // 32-bit LDS address of a pointer into the kernel's LDS array
@@ -242,15 +267,21 @@ __device__ __forceinline__ void p_load_entries(PIdx& t, const int32_t* __restric
     t.ew = lane < ne ? ew[e0 + lane] : 0.f;
 }
 
-template <int H>
+// REC: layer 1 from layer-0 records -- x rows are not read from HBM but
+// expanded from rec (8 floats per node) with coef8 ([H][8], copied to LDS)
+// on the fly, all by the producers: the own rows of tile s+2 into the image
+// at the end of step s (their records gathered at its start), the
+// out-of-tile rows in registers next to their gathered records.
+template <int H, bool REC>
 __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t row_begin,
     int64_t row_end, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift, int flags,
-    float* __restrict__ out, int64_t ldo, unsigned long long* trace) {
+    float* __restrict__ out, int64_t ldo, const float* __restrict__ rec,
+    const float* __restrict__ coef8, unsigned long long* trace) {
     using C = SCfg<H>;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[REC ? C::LDS_BYTES_REC : C::LDS_BYTES];
     int* const cntX = reinterpret_cast<int*>(lds + C::OFF_CNT);
     int* const cntA = cntX + 1;
     _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
@@ -296,6 +327,9 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         // zero row (read by the empty slots of the in-tile pass)
         for (int i = lane_ + pw * 64; i < C::ROWB / 4; i += C::NPW * 64)
             reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
+        if constexpr (REC)   // the expansion coefficients -> LDS (read after the first barrier)
+            for (int i = lane_ + pw * 64; i < H * 8; i += C::NPW * 64)
+                reinterpret_cast<float*>(lds + C::OFF_COEF)[i] = coef8[i];
         // lookup tables of tile parity tb: LT [PROWS][LTS] {P, w}, ET [PROWS][ETS] {col, w}
         auto LTb = [&](int tb) { return lds + C::OFF_TAB + (tb * C::NPW + pw) * C::TAB_BYTES; };
         auto ETb = [&](int tb) { return LTb(tb) + C::PROWS * C::LTS * 8; };
@@ -310,6 +344,57 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         uint32_t coff[C::CH];                         // byte offset of my chunks in a row
 #pragma unroll
         for (int j = 0; j < C::CH; ++j) coff[j] = static_cast<uint32_t>((c0 + 16 * j) << 4);
+        // REC: coefficients of columns 4 ch .. 4 ch + 3 from the LDS table
+        // (re-read per use: 64 registers for all of a lane's columns would
+        // spill; a global load issued after the out-of-tile gathers would make
+        // every wait for it drain them)
+        auto load_pc = [&](int ch, f32x4 (&ca)[4], f32x4 (&cb)[4]) {
+            const unsigned char* cp = lds + C::OFF_COEF + ch * 4 * 32;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                ca[r] = *reinterpret_cast<const f32x4*>(cp + r * 32);
+                cb[r] = *reinterpret_cast<const f32x4*>(cp + r * 32 + 16);
+            }
+        };
+        // ---- REC: the wave's rows [PROWS pw, +PROWS) of a tile: their
+        // records, one float per lane (row PROWS pw + l / 8, element l % 8),
+        // loaded at the start of a step (before the out-of-tile gathers, so
+        // waiting for them does not drain those) ...
+        auto load_own = [&](int64_t step) -> float {
+            const int64_t tile = tile_of(step);
+            if (tile >= ntiles) return 0.f;
+            int64_t row = row_begin + tile * C::BM + C::PROWS * pw + (lane_ >> 3);
+            if (row >= row_end) row = row_end - 1;          // any valid row: never read
+            return rec[row * 8 + (lane_ & 7)];
+        };
+        // ... and expanded into the own-row image at its end: lane (erg, ecl)
+        // = columns 4 ecl .. 4 ecl + 3 of rows PROWS pw + erg + RG k (chunk ecl
+        // of row lr at position ecl ^ (lr & 7)); a row's record broadcast
+        // from its 8 lanes
+        auto expand_tile = [&](int64_t step, float own) {
+            if (tile_of(step) >= ntiles) return;
+            const int sb = static_cast<int>(step % 3);      // its image buffer (xbuf_of)
+            const int erg = lane_ / C::CPL, ecl = lane_ % C::CPL;
+            f32x4 ca[4], cb[4];
+            load_pc(ecl, ca, cb);
+            unsigned char* X = lds + sb * C::X_BYTES;
+            const int vo = __builtin_bit_cast(int, own);
+#pragma unroll
+            for (int k = 0; k < C::PROWS / C::RG; ++k) {
+                const int rw = erg + C::RG * k;             // row within the wave's rows
+                const int lr = C::PROWS * pw + rw;
+                f32x4 ra, rb;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    ra[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((8 * rw + e) << 2, vo));
+                    rb[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((8 * rw + 4 + e) << 2, vo));
+                }
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = expand1(ca[r], cb[r], ra, rb);
+                *reinterpret_cast<f32x4*>(X + lr * C::ROWB + ((ecl ^ (lr & 7)) << 4)) = v;
+            }
+        };
         // out-of-tile row c (empty slot: c = ~0u -> the zero row)
         auto xrow = [&](uint32_t c) -> const unsigned char* {
             return c != 0xffffffffu ? reinterpret_cast<const unsigned char*>(x + (int64_t)c * ldx)
@@ -352,6 +437,15 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                         const uint32_t a = (xb + off * C::ROWB) +
                                            (static_cast<uint32_t>(loff) ^ ((off & 7u) << 4));
                         ldv<C::VPL>(reinterpret_cast<const float*>(lds + a), vv);
+                    } else if constexpr (REC) {
+                        const f32x4 ra = *reinterpret_cast<const f32x4*>(rec + (int64_t)c * 8);
+                        const f32x4 rb = *reinterpret_cast<const f32x4*>(rec + (int64_t)c * 8 + 4);
+#pragma unroll
+                        for (int k = 0; k < C::VPL; ++k) {
+                            const float* cp = coef8 + (C::VPL * lane_ + k) * 8;
+                            vv[k] = expand1(*reinterpret_cast<const f32x4*>(cp),
+                                            *reinterpret_cast<const f32x4*>(cp + 4), ra, rb);
+                        }
                     } else {
                         const i32x4 rs = buffer_rsrc(xbase + (uint64_t)static_cast<uint32_t>(c) * ldxb, H * 4);
                         if constexpr (C::VPL == 2) {
@@ -391,10 +485,12 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             unsigned char* const LT = LTb(tb);
             unsigned char* const ET = ETb(tb);
             {
-                const uint4 z4 = make_uint4(C::OFF_ZERO, 0u, C::OFF_ZERO, 0u);
+                uint32_t zo = C::OFF_ZERO, zz = 0u;
+                asm volatile("" : "+v"(zo), "+v"(zz));   // rematerialised per call, never spilled
+                const uint4 z4 = make_uint4(zo, zz, zo, zz);
                 if (lane_ < C::PROWS * C::LTS / 2) *reinterpret_cast<uint4*>(LT + 16 * lane_) = z4;
                 if (lane_ < C::PROWS * C::ETS)
-                    *reinterpret_cast<uint2*>(ET + 8 * lane_) = make_uint2(0xffffffffu, 0u);
+                    *reinterpret_cast<uint2*>(ET + 8 * lane_) = make_uint2(~zz, zz);
             }
             if (tile >= ntiles) return TInfo{0, 0, 0};
             const int64_t t0 = row_begin + tile * C::BM;
@@ -442,7 +538,9 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         };
 
         // ---- out-of-tile rows of a tile (tables tb) -> registers, EX per row
-        using XV = f32x4[C::NQD][C::EX][C::CH];
+        // REC: one float of the record per lane (lane i & 7 of the row's 16),
+        // broadcast within the row at expansion time
+        using XV = std::conditional_t<REC, float[C::NQD][C::EX], f32x4[C::NQD][C::EX][C::CH]>;
         auto issue_ext = [&](int tb, XV& xv) {
             asm volatile("" ::: "memory");   // after the table writes
             const unsigned char* const ET = ETb(tb);
@@ -458,6 +556,17 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                     if (e + 1 < C::EX) cc[qd][e + 1] = t.z;
                 }
             }
+            if constexpr (REC) {
+#pragma unroll
+                for (int qd = 0; qd < C::NQD; ++qd)
+#pragma unroll
+                    for (int e = 0; e < C::EX; ++e) {
+                        xv[qd][e] = 0.f;
+                        if (cc[qd][e] != 0xffffffffu)
+                            xv[qd][e] = rec[static_cast<uint64_t>(cc[qd][e]) * 8 + (iq & 7)];
+                    }
+                return;
+            } else {
 #pragma unroll
             for (int qd = 0; qd < C::NQD; ++qd)
 #pragma unroll
@@ -476,12 +585,67 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                             xv[qd][e][j] = *reinterpret_cast<const f32x4*>(rowp + coff[j]);
                     }
                 }
+            }
         };
         // their weighted sum, CSR order (empty slots: zeros, w 0), + the rest
         // beyond the register slots (rare; synchronous loads)
         using ACC = f32x4[C::NQD][C::CH];
         auto sum_ext = [&](int tb, const XV& xv, const TInfo& info, ACC& acc) {
             const unsigned char* const ET = ETb(tb);
+            if constexpr (REC) {
+#pragma unroll
+                for (int qd = 0; qd < C::NQD; ++qd) {
+                    const int row = 4 * qd + gq;
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j) acc[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    // chunk by chunk (its coefficients: 32 registers), slot by
+                    // slot: the slot's record broadcast from the row's lanes
+                    // 0..7 (lane' = (lane & 16) | k within each 32-lane half)
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j) {
+                        // (scheduling fence: keeps the next chunk's coefficient
+                        // loads from being hoisted over this one -- registers)
+                        __builtin_amdgcn_sched_barrier(0);
+                        f32x4 ca[4], cb[4];
+                        load_pc(c0 + 16 * j, ca, cb);
+#pragma unroll
+                        for (int e = 0; e < C::EX; ++e) {
+                            // slots past every row's last entry: nothing to add
+                            // (an empty slot adds 0 * relu(e_n): skipping is exact)
+                            if (e >= info.maxext) break;
+                            const float w = __builtin_bit_cast(
+                                float, *reinterpret_cast<const uint32_t*>(ET + (row * C::ETS + e) * 8 + 4));
+                            const int v = __builtin_bit_cast(int, xv[qd][e]);
+#define MIGNN_SWZ(k) __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(v, 0x10 | ((k) << 5)))
+                            const f32x4 ra = f32x4{MIGNN_SWZ(0), MIGNN_SWZ(1), MIGNN_SWZ(2), MIGNN_SWZ(3)};
+                            const f32x4 rb = f32x4{MIGNN_SWZ(4), MIGNN_SWZ(5), MIGNN_SWZ(6), MIGNN_SWZ(7)};
+#undef MIGNN_SWZ
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                acc[qd][j][r] = fmaf(w, expand1(ca[r], cb[r], ra, rb), acc[qd][j][r]);
+                        }
+                    }
+#pragma unroll 1
+                    for (int e = C::EX; e < info.maxext; ++e) {
+                        const uint2 cw = *reinterpret_cast<const uint2*>(ET + (row * C::ETS + e) * 8);
+                        const float w = __builtin_bit_cast(float, cw.y);
+                        const float* rp = cw.x != 0xffffffffu ? rec + static_cast<uint64_t>(cw.x) * 8
+                                                              : g_zero_row;
+                        const f32x4 ra = *reinterpret_cast<const f32x4*>(rp);
+                        const f32x4 rb = *reinterpret_cast<const f32x4*>(rp + 4);
+#pragma unroll
+                        for (int j = 0; j < C::CH; ++j) {
+                            f32x4 ca[4], cb[4];
+                            load_pc(c0 + 16 * j, ca, cb);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                acc[qd][j][r] = fmaf(w, expand1(ca[r], cb[r], ra, rb), acc[qd][j][r]);
+                        }
+                    }
+                }
+                return;
+            }
+            else {
 #pragma unroll
             for (int qd = 0; qd < C::NQD; ++qd) {
                 const int row = 4 * qd + gq;
@@ -509,15 +673,20 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                     }
                 }
             }
+            }
         };
 
         // ---- in-tile entries of a tile (tables tb) on top of acc, then scale,
         //      split and write the wave's rows to the A image
         auto finish_tile = [&](int tb, const TInfo& info, ACC& acc, int64_t s) {
             const unsigned char* const LT = LTb(tb);
+            // REC: lane-derived values laundered per call, so their address
+            // arithmetic is redone per step instead of pinned in registers
+            int gqs = gq, c0s = c0;
+            if constexpr (REC) asm volatile("" : "+v"(gqs), "+v"(c0s));
 #pragma unroll
             for (int qd = 0; qd < C::NQD; ++qd) {
-                const int row = 4 * qd + gq;
+                const int row = 4 * qd + gqs;
                 const int ndeg = (flags & MIGNN_DIAG_NO_LOCAL) ? 0 : info.maxdeg;
                 for (int u0 = 0; u0 < ndeg; u0 += C::UB) {
                     uint2 pw_[C::UB];
@@ -563,7 +732,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                 wait_a(s);
 #pragma unroll
                 for (int j = 0; j < C::CH; ++j) {
-                    const int hc = 4 * (c0 + 16 * j);   // first half of my chunk in the row
+                    const int hc = 4 * (c0s + 16 * j);  // first half of my chunk in the row
                     *reinterpret_cast<f16x4*>(&AH[lrow * C::AS + hc]) = h[j];
                     *reinterpret_cast<f16x4*>(&AL[lrow * C::AS + hc]) = l[j];
                 }
@@ -588,6 +757,11 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         issue_ext(0, xv);
         sum_ext(0, xv, ia, acc);
         int rpa = pa.rpv;
+        if constexpr (REC) {
+            block_barrier<0xC07F>();   // the coefficient table (written before the tables)
+            expand_tile(0, load_own(0));
+        }
+        float own_next = 0.f;           // REC: records of tile s+2's own rows
         block_barrier<0xC07F>();   // zero row, counters, own rows of tiles 0, 1 (lgkmcnt(0))
         for (int64_t s = -1; s < nsteps; ++s) {
             const int ta = static_cast<int>((s + 1) & 1), tbb = ta ^ 1;
@@ -596,6 +770,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             p_load_entries<C::PROWS>(pc, col, ew, lane_);                      // tile s+3
             const int rpd = p_load_rpv<C::PROWS>(row_ptr, first_row(tile_of(s + 4)), row_end, lane_);
             if (pw == 0) stamp(trace, lane_, s, 0);
+            if constexpr (REC) own_next = load_own(s + 2);   // expanded at the end of the step
             // (re)built every step: past the last tile this only resets the
             // tables to empty slots, so the gathers never see stale columns
             const bool prod = !(flags & MIGNN_DIAG_NO_PRODUCE);
@@ -616,6 +791,12 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             pb = pc;
             rpc = rpd;
             ia = ib;
+            // REC: tile s+2's rows (records DMA'd at step s-2, landed a step
+            // ago), read by the producers next step.  Placed at the END of the
+            // step: at its start the same expansion produced sporadic wrong
+            // chunks (a few rows per 10^5, run to run; scripts/rec_debug.py)
+            if constexpr (REC)
+                if (s + 2 < nsteps) expand_tile(s + 2, own_next);
             block_barrier<0xC07F>();   // this step's LDS writes done (lgkmcnt(0))
         }
         return;
@@ -692,8 +873,14 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     }
     const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
 
-    x_dma(tile_of(0));
-    x_dma(tile_of(1));
+    if constexpr (REC) {
+        // (the producers fill the coefficient table before the first barrier
+        // and expand tile 0 between the two, tile s+2 at the end of step s)
+        block_barrier<0x70>();
+    } else {
+        x_dma(tile_of(0));
+        x_dma(tile_of(1));
+    }
     block_barrier<0x70>();   // own rows of tiles 0 and 1 landed: vmcnt(0) lgkmcnt(0)
     for (int64_t s = -1; s < nsteps; ++s) {
         const int64_t tile = tile_of(s);
@@ -727,7 +914,8 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         if (s >= 0 && lane_ == 0) lds_bump(cntX);
         lds_wait(cntX, C::NCW * static_cast<int>(s + 1));
         if (wave == 0) stamp(trace, lane_, s, 4);
-        const bool dma = (s + 3 < nsteps) && x_dma(tile_of(s + 3));
+        bool dma = false;
+        if constexpr (!REC) dma = (s + 3 < nsteps) && x_dma(tile_of(s + 3));
         if (wave == 0) stamp(trace, lane_, s, 5);
         if (mm) {
             // fragments of block (kc, ib) = step t = kc * IB + ib; the next
@@ -795,18 +983,19 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         // the own rows DMA'd a step ago must have landed (producers read them
         // next step); this step's DMA (NPC) and row stores (NST), the youngest
         // vector-memory operations, may stay in flight
-        if (dma && stored) block_barrier<0x70 | (C::NPC + C::NST)>();
-        else if (dma) block_barrier<0x70 | C::NPC>();
+        constexpr int npc = C::NPC;
+        if (dma && stored) block_barrier<0x70 | (npc + C::NST)>();
+        else if (dma) block_barrier<0x70 | npc>();
         else if (stored) block_barrier<0x70 | C::NST>();
         else block_barrier<0x70>();
     }
 }
 
-template <int H>
+template <int H, bool REC>
 int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                  int64_t ldx, int64_t rb, int64_t re, const float* w, const float* bias,
                  const float* scale, const float* shift, int flags, float* out, int64_t ldo,
-                 hipStream_t st) {
+                 const float* rec, const float* coef8, hipStream_t st) {
     using C = SCfg<H>;
     static int grid_cache[64] = {0};
     int dev = 0;
@@ -821,8 +1010,8 @@ int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, co
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL(gcn_f16x3_kernel<H>, dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x,
-                       ldx, rb, re, w, bias, scale, shift, flags, out, ldo,
+    hipLaunchKernelGGL((gcn_f16x3_kernel<H, REC>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col,
+                       ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, rec, coef8,
                        (flags & MIGNN_DIAG_TRACE) ? g_trace16_host : nullptr);
     return launch_status("gcn_f16x3_kernel");
 }
@@ -864,8 +1053,33 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
     MIGNN_REQUIRE(x != out, "gcn_layer_f16x3: in-place not supported (neighbours read x)");
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
-    return h == 128 ? launch_f16x3<128>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
-                                        flags, out, ldo, st)
-                    : launch_f16x3<64>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
-                                       flags, out, ldo, st);
+    return h == 128 ? launch_f16x3<128, false>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,
+                                               shift, flags, out, ldo, nullptr, nullptr, st)
+                    : launch_f16x3<64, false>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,
+                                              shift, flags, out, ldo, nullptr, nullptr, st);
+}
+
+extern "C" int mignn_gcn_layer_f16x3_rec(const int32_t* row_ptr, const int32_t* col,
+                                         const float* ew, const float* rec, const float* coef8,
+                                         int64_t rb, int64_t re, int h, const float* w,
+                                         const float* bias, const float* scale,
+                                         const float* shift, int flags, float* out, int64_t ldo,
+                                         void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer_f16x3_rec: unknown flags 0x%x", flags);
+    MIGNN_REQUIRE(row_ptr && col && ew && rec && coef8 && w && out,
+                  "gcn_layer_f16x3_rec: null pointer");
+    MIGNN_REQUIRE(h == 64 || h == 128, "gcn_layer_f16x3_rec: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(aligned16(rec) && aligned16(coef8) && aligned16(w) && aligned16(out),
+                  "gcn_layer_f16x3_rec: unaligned");
+    MIGNN_REQUIRE(ldo % 4 == 0 && ldo >= h, "gcn_layer_f16x3_rec: bad ldo");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_layer_f16x3_rec: bad row range");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bias, "gcn_layer_f16x3_rec: bias");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gcn_layer_f16x3_rec: affine");
+    if (re == rb) return MIGNN_OK;
+    hipStream_t st = as_stream(stream);
+    // x is never read in records mode (rows are expanded from rec)
+    return h == 128 ? launch_f16x3<128, true>(row_ptr, col, ew, nullptr, h, rb, re, w, bias, scale,
+                                              shift, flags, out, ldo, rec, coef8, st)
+                    : launch_f16x3<64, true>(row_ptr, col, ew, nullptr, h, rb, re, w, bias, scale,
+                                             shift, flags, out, ldo, rec, coef8, st);
 }

@@ -22,7 +22,8 @@ namespace {
 
 constexpr int kWaves = 4;
 
-template <int D, int DIAG = 0>   // DIAG (timing ablations): 1 = no gathers, 2 = no stores
+template <int D, int DIAG = 0>   // DIAG (timing ablations): 1 = no gathers, 2 = no stores;
+                                 // 4 = records mode: write each row's aggregates (8 floats)
 __global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
@@ -41,7 +42,8 @@ __global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int k = 0; k < K; ++k) cf[q][k] = active ? coef[(int64_t)(cq + q) * K + k] : 0.f;
+        for (int k = 0; k < K; ++k)
+            cf[q][k] = (active && (DIAG & 4) == 0) ? coef[(int64_t)(cq + q) * K + k] : 0.f;
 
     const int64_t nrows = row_end - row_begin;
     const int64_t stride = (int64_t)gridDim.x * kWaves * 64;
@@ -90,6 +92,22 @@ __global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
 #pragma unroll
             for (int a = 0; a < D; ++a) { ag[lane][a] = c[a]; ag[lane][D + a] = C[a]; }
             ag[lane][2 * D] = s;
+        }
+        if constexpr ((DIAG & 4) != 0) {
+            // records: rec[i] = {c_i, C_i, s_i} padded to 8 floats (the REC layer
+            // kernel expands x0_i = relu(coef8 . rec_i) itself)
+            if (r < nrows) {
+                f32x4 ra = f32x4{0.f, 0.f, 0.f, 0.f}, rb = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 2 * D + 1; ++k) {
+                    if (k < 4) ra[k] = ag[lane][k];
+                    else rb[k - 4] = ag[lane][k];
+                }
+                f32x4* const dst = reinterpret_cast<f32x4*>(out + (row_begin + r) * 8);
+                dst[0] = ra;
+                dst[1] = rb;
+            }
+            continue;
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
@@ -146,6 +164,29 @@ extern "C" int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* co
     default: hipLaunchKernelGGL(gcn_layer0_kernel<4>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
     }
     return launch_status("gcn_layer0_kernel");
+}
+
+extern "C" int mignn_gcn_layer0_records(const int32_t* row_ptr, const int32_t* col,
+                                        const float* ew, const float* pos, int64_t ldp, int in_dim,
+                                        int64_t row_begin, int64_t row_end, float* rec,
+                                        void* stream) {
+    MIGNN_REQUIRE(row_ptr && col && ew && pos && rec, "gcn_layer0_records: null pointer");
+    MIGNN_REQUIRE(in_dim >= 1 && in_dim <= 3, "gcn_layer0_records: in_dim must be 1..3 (got %d)",
+                  in_dim);
+    MIGNN_REQUIRE(ldp >= in_dim, "gcn_layer0_records: ldp < in_dim");
+    MIGNN_REQUIRE(aligned16(rec), "gcn_layer0_records: rec must be 16-B aligned");
+    MIGNN_REQUIRE(row_begin >= 0 && row_end >= row_begin, "gcn_layer0_records: bad row range");
+    if (row_end == row_begin) return MIGNN_OK;
+    hipStream_t st = as_stream(stream);
+    const int64_t blocks = (row_end - row_begin + kWaves * 64 - 1) / (kWaves * 64);
+    const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);
+    // (coef / h / ldo unused in records mode)
+    switch (in_dim) {
+    case 1: hipLaunchKernelGGL((gcn_layer0_kernel<1, 4>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, nullptr, 4, rec, 8); break;
+    case 2: hipLaunchKernelGGL((gcn_layer0_kernel<2, 4>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, nullptr, 4, rec, 8); break;
+    default: hipLaunchKernelGGL((gcn_layer0_kernel<3, 4>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, nullptr, 4, rec, 8); break;
+    }
+    return launch_status("gcn_layer0_kernel(records)");
 }
 
 extern "C" int mignn_diag_gcn_layer0(int mode, const int32_t* row_ptr, const int32_t* col,

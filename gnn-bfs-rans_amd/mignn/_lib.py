@@ -46,6 +46,9 @@ SIGNATURES = {
                                             c_int, c_int, c_float, _P, c_int64, _P]),
     "mignn_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P, _P,
                                 c_int, _P, c_int64, _P]),
+    "mignn_gcn_layer_f16x3_rec": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P,
+                                          _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_layer0_records": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P, _P]),
     "mignn_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                       _P, _P, c_int, _P, c_int64, _P]),
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
