@@ -184,6 +184,16 @@ __device__ __forceinline__ float expand1(const f32x4& ca, const f32x4& cb, const
     return t < 0.f ? 0.f : t;
 }
 
+// lanes B .. B + 6 of each 16-lane row broadcast to the whole row (DPP
+// row_newbcast, VALU): a record held one element per lane
+template <int B>
+__device__ __forceinline__ void row_bcast7(int v, f32x4& ra, f32x4& rb) {
+#define MIGNN_BC(e) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(v, 0x150 + B + (e), 0xf, 0xf, false))
+    ra = f32x4{MIGNN_BC(0), MIGNN_BC(1), MIGNN_BC(2), MIGNN_BC(3)};
+    rb = f32x4{MIGNN_BC(4), MIGNN_BC(5), MIGNN_BC(6), 0.f};
+#undef MIGNN_BC
+}
+
 // 32-bit LDS address of a pointer into the kernel's LDS array
 __device__ __forceinline__ uint32_t lds_addr(const unsigned char* p) {
     return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)(p)));
@@ -356,39 +366,44 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                 cb[r] = *reinterpret_cast<const f32x4*>(cp + r * 32 + 16);
             }
         };
-        // ---- REC: the wave's rows [PROWS pw, +PROWS) of a tile: their
-        // records, one float per lane (row PROWS pw + l / 8, element l % 8),
-        // loaded at the start of a step (before the out-of-tile gathers, so
-        // waiting for them does not drain those) ...
-        auto load_own = [&](int64_t step) -> float {
-            const int64_t tile = tile_of(step);
-            if (tile >= ntiles) return 0.f;
-            int64_t row = row_begin + tile * C::BM + C::PROWS * pw + (lane_ >> 3);
-            if (row >= row_end) row = row_end - 1;          // any valid row: never read
-            return rec[row * 8 + (lane_ & 7)];
+        // ---- REC: the wave's rows [PROWS pw, +PROWS) of a tile.  Expansion
+        // lane (erg, ecl) = columns 4 ecl .. 4 ecl + 3 of rows erg + RG k (k <
+        // NK) of them; every 16-lane DPP row holds the records of its erg
+        // group's NK rows: register t, lane m of the DPP row = element m % 8
+        // of row erg + RG (2 t + m / 8) -- broadcast by row_newbcast.  Loaded
+        // at the start of a step (before the out-of-tile gathers, so waiting
+        // for them does not drain those) ...
+        constexpr int NK = C::PROWS / C::RG, NOWN = NK / 2;
+        static_assert(NK % 2 == 0, "own-record layout");
+        using OWN = float[NOWN];
+        auto load_own = [&](int64_t step, OWN& own) {    // always NOWN loads (never a
+            const int64_t tile = tile_of(step);             // conditional one: the
+            const int erg = lane_ / C::CPL, m = lane_ & 15; // merge would wait)
+#pragma unroll
+            for (int t = 0; t < NOWN; ++t) {
+                int64_t row = row_begin + tile * C::BM + C::PROWS * pw + erg + C::RG * (2 * t + (m >> 3));
+                if (tile >= ntiles || row >= row_end) row = row_end - 1;
+                own[t] = rec[row * 8 + (m & 7)];
+            }
         };
         // ... and expanded into the own-row image at its end: lane (erg, ecl)
         // = columns 4 ecl .. 4 ecl + 3 of rows PROWS pw + erg + RG k (chunk ecl
         // of row lr at position ecl ^ (lr & 7)); a row's record broadcast
         // from its 8 lanes
-        auto expand_tile = [&](int64_t step, float own) {
+        auto expand_tile = [&](int64_t step, const OWN& own) {
             if (tile_of(step) >= ntiles) return;
             const int sb = static_cast<int>(step % 3);      // its image buffer (xbuf_of)
             const int erg = lane_ / C::CPL, ecl = lane_ % C::CPL;
             f32x4 ca[4], cb[4];
             load_pc(ecl, ca, cb);
             unsigned char* X = lds + sb * C::X_BYTES;
-            const int vo = __builtin_bit_cast(int, own);
 #pragma unroll
-            for (int k = 0; k < C::PROWS / C::RG; ++k) {
-                const int rw = erg + C::RG * k;             // row within the wave's rows
-                const int lr = C::PROWS * pw + rw;
+            for (int k = 0; k < NK; ++k) {
+                const int lr = C::PROWS * pw + erg + C::RG * k;
+                const int vo = __builtin_bit_cast(int, own[k >> 1]);
                 f32x4 ra, rb;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    ra[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((8 * rw + e) << 2, vo));
-                    rb[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((8 * rw + 4 + e) << 2, vo));
-                }
+                if (k & 1) row_bcast7<8>(vo, ra, rb);
+                else row_bcast7<0>(vo, ra, rb);
                 f32x4 v;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = expand1(ca[r], cb[r], ra, rb);
@@ -594,20 +609,22 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             const unsigned char* const ET = ETb(tb);
             if constexpr (REC) {
 #pragma unroll
-                for (int qd = 0; qd < C::NQD; ++qd) {
-                    const int row = 4 * qd + gq;
+                for (int qd = 0; qd < C::NQD; ++qd)
 #pragma unroll
                     for (int j = 0; j < C::CH; ++j) acc[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    // chunk by chunk (its coefficients: 32 registers), slot by
-                    // slot: the slot's record broadcast from the row's lanes
-                    // 0..7 (lane' = (lane & 16) | k within each 32-lane half)
+                // chunk by chunk (its coefficients: 32 registers, read once per
+                // step), slot by slot: the slot's record broadcast from the row's
+                // lanes 0..7 (DPP row_newbcast: VALU, no LDS crossbar)
 #pragma unroll
-                    for (int j = 0; j < C::CH; ++j) {
-                        // (scheduling fence: keeps the next chunk's coefficient
-                        // loads from being hoisted over this one -- registers)
-                        __builtin_amdgcn_sched_barrier(0);
-                        f32x4 ca[4], cb[4];
-                        load_pc(c0 + 16 * j, ca, cb);
+                for (int j = 0; j < C::CH; ++j) {
+                    // (scheduling fence: keeps the next chunk's coefficient reads
+                    // from being hoisted over this one -- registers)
+                    __builtin_amdgcn_sched_barrier(0);
+                    f32x4 ca[4], cb[4];
+                    load_pc(c0 + 16 * j, ca, cb);
+#pragma unroll
+                    for (int qd = 0; qd < C::NQD; ++qd) {
+                        const int row = 4 * qd + gq;
 #pragma unroll
                         for (int e = 0; e < C::EX; ++e) {
                             // slots past every row's last entry: nothing to add
@@ -615,16 +632,17 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                             if (e >= info.maxext) break;
                             const float w = __builtin_bit_cast(
                                 float, *reinterpret_cast<const uint32_t*>(ET + (row * C::ETS + e) * 8 + 4));
-                            const int v = __builtin_bit_cast(int, xv[qd][e]);
-#define MIGNN_SWZ(k) __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(v, 0x10 | ((k) << 5)))
-                            const f32x4 ra = f32x4{MIGNN_SWZ(0), MIGNN_SWZ(1), MIGNN_SWZ(2), MIGNN_SWZ(3)};
-                            const f32x4 rb = f32x4{MIGNN_SWZ(4), MIGNN_SWZ(5), MIGNN_SWZ(6), MIGNN_SWZ(7)};
-#undef MIGNN_SWZ
+                            f32x4 ra, rb;
+                            row_bcast7<0>(__builtin_bit_cast(int, xv[qd][e]), ra, rb);
 #pragma unroll
                             for (int r = 0; r < 4; ++r)
                                 acc[qd][j][r] = fmaf(w, expand1(ca[r], cb[r], ra, rb), acc[qd][j][r]);
                         }
                     }
+                }
+#pragma unroll
+                for (int qd = 0; qd < C::NQD; ++qd) {
+                    const int row = 4 * qd + gq;
 #pragma unroll 1
                     for (int e = C::EX; e < info.maxext; ++e) {
                         const uint2 cw = *reinterpret_cast<const uint2*>(ET + (row * C::ETS + e) * 8);
@@ -759,9 +777,11 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         int rpa = pa.rpv;
         if constexpr (REC) {
             block_barrier<0xC07F>();   // the coefficient table (written before the tables)
-            expand_tile(0, load_own(0));
+            OWN own0;
+            load_own(0, own0);
+            expand_tile(0, own0);
         }
-        float own_next = 0.f;           // REC: records of tile s+2's own rows
+        OWN own_next;                   // REC: records of tile s+2's own rows
         block_barrier<0xC07F>();   // zero row, counters, own rows of tiles 0, 1 (lgkmcnt(0))
         for (int64_t s = -1; s < nsteps; ++s) {
             const int ta = static_cast<int>((s + 1) & 1), tbb = ta ^ 1;
@@ -770,7 +790,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             p_load_entries<C::PROWS>(pc, col, ew, lane_);                      // tile s+3
             const int rpd = p_load_rpv<C::PROWS>(row_ptr, first_row(tile_of(s + 4)), row_end, lane_);
             if (pw == 0) stamp(trace, lane_, s, 0);
-            if constexpr (REC) own_next = load_own(s + 2);   // expanded at the end of the step
+            if constexpr (REC) load_own(s + 2, own_next);   // expanded at the end of the step
             // (re)built every step: past the last tile this only resets the
             // tables to empty slots, so the gathers never see stale columns
             const bool prod = !(flags & MIGNN_DIAG_NO_PRODUCE);
