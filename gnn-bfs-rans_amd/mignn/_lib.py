@@ -133,6 +133,7 @@ DIAG_SIGNATURES = {
     "mignn_gcn_layer_ring": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                      _P, _P, c_int, _P, c_int64, c_int64, _P]),
     "mignn_diag_set_trace_ring": (c_int, [_P]),
+    "mignn_diag_set_agg_legacy": (c_int, [c_int]),
     "mignn_diag_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P,
                                      _P, c_int, _P, c_int64, _P]),
     "mignn_diag_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,

@@ -87,6 +87,10 @@ int mignn_gcn_layer_ring(const int32_t* row_ptr, const int32_t* col, const float
 /* Timeline buffer (uint64 [8 * 64 * 16]) for mignn_gcn_layer_ring: s_memtime
  * of wave 0 of workgroups 0..7 at the 10 phase boundaries of steps 0..63. */
 int mignn_diag_set_trace_ring(void* buf);
+/* on != 0: the eval aggregations (mignn_gcn/sum/gat/transformer_aggregate)
+ * use the entry-at-a-time kernels instead of the batched ones (A/B timing;
+ * results equal up to fp32 summation order).  Process-wide. */
+int mignn_diag_set_agg_legacy(int on);
 #ifdef __cplusplus
 }
 #endif
