@@ -677,6 +677,13 @@ def cpu_leg(model, sd, cfg, args, dev):
         if it > 0:
             times.append(dt)
     t = statistics.median(times)
+    # accuracy on the same 1M-node sample: both fp32 paths against the fp64
+    # oracle (the GPU-vs-fp32-CPU difference alone mixes both rounding errors)
+    y64 = orc.flowgnn_forward(sd, cfg, x, ei, None, dtype=torch.float64)
+    acc = {"gpu_vs_fp64_max_abs_err": (yg.double() - y64).abs().max().item(),
+           "cpu_fp32_vs_fp64_max_abs_err": (y.double() - y64).abs().max().item(),
+           "gpu_vs_cpu_fp32_max_abs_err": (yg - y).abs().max().item(),
+           "output_max_abs": y64.abs().max().item()}
     cpu_model = "unknown"
     try:
         for ln in open("/proc/cpuinfo"):
@@ -694,8 +701,7 @@ def cpu_leg(model, sd, cfg, args, dev):
                       f"torch-CPU oracle fp32, median of 2 after 1 warm-up; the CPU path is "
                       f"O(L E H) with no cache effects at this size, so its edges/s is taken as "
                       f"size-independent (extrapolated to the 10M headline mesh, not timed there)",
-            "s_per_forward": round(t, 3), "cpu_model": cpu_model,
-            "gpu_vs_cpu_max_abs_err": (yg - y).abs().max().item()}
+            "s_per_forward": round(t, 3), "cpu_model": cpu_model, "accuracy_1M": acc}
 
 
 if __name__ == "__main__":

@@ -8,6 +8,9 @@
 //           computed from the row id (no index loads) -> the memory system's
 //           best case for this access pattern
 //   mode 2  streaming copy out[i] = x[i] (16 B per lane)
+//   mode 3  the same copy in the store pattern of a 16x16 MFMA accumulator
+//           tile: a wave owns 16 rows, lane (r, g) moves 16 B at column
+//           16 cb + 4 g of row r -- every instruction 16 rows x 64 B
 //   | 4     XCD-aware block -> row remap (contiguous row chunks per XCD per step)
 //   | 8     non-temporal output stores
 #include "common.hpp"
@@ -64,6 +67,27 @@ __global__ __launch_bounds__(256) void diag_gather_kernel(
             for (int u = 0; u < 7; ++u) v[u] = ld4(x + nb[u] * H + 4 * c);
 #pragma unroll
             for (int u = 0; u < 7; ++u) acc = fma4(0.14285715f, v[u], acc);
+        } else if constexpr (MODE == 3) {
+            // row = this lane group's 16-row block id (LPR = 32 lanes -> 2
+            // groups per wave; use the wave instead: 16 rows per wave)
+            const int64_t wave = (blk * blockDim.x + threadIdx.x) >> 6;
+            const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+            const int r = lane & 15, g = lane >> 4;
+            for (int64_t b = wave; b * 16 < n; b += nwaves) {
+                const int64_t rr = b * 16 + r;
+                if (rr < n) {
+                    float4 v[8];
+#pragma unroll
+                    for (int cb = 0; cb < 8; ++cb) v[cb] = ld4(x + rr * H + 16 * cb + 4 * g);
+#pragma unroll
+                    for (int cb = 0; cb < 8; ++cb) {
+                        const f32x4 w = {v[cb].x, v[cb].y, v[cb].z, v[cb].w};
+                        if (NT) __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(out + rr * H + 16 * cb + 4 * g));
+                        else *reinterpret_cast<f32x4*>(out + rr * H + 16 * cb + 4 * g) = w;
+                    }
+                }
+            }
+            return;
         } else {
             acc = ld4(x + row * H + 4 * c);
         }
@@ -97,8 +121,10 @@ extern "C" int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t
     } else if (base == 1) {
         if (remap) { if (nt) MIGNN_DIAG(1, true, true); else MIGNN_DIAG(1, true, false); }
         else { if (nt) MIGNN_DIAG(1, false, true); else MIGNN_DIAG(1, false, false); }
-    } else {
+    } else if (base == 2) {
         if (nt) MIGNN_DIAG(2, false, true); else MIGNN_DIAG(2, false, false);
+    } else {
+        if (nt) MIGNN_DIAG(3, false, true); else MIGNN_DIAG(3, false, false);
     }
 #undef MIGNN_DIAG
     return launch_status("diag_gather_kernel");

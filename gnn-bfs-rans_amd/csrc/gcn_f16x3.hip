@@ -328,6 +328,11 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         cntA[0] = 0;
     }
 
+    // static wave priority (diagnostic schedules): consumers or producers
+    // win instruction arbitration on their SIMD
+    if ((flags & MIGNN_SCHED_PRIO_CONSUMERS) && wave < C::NCW) __builtin_amdgcn_s_setprio(1);
+    if ((flags & MIGNN_SCHED_PRIO_PRODUCERS) && wave >= C::NCW) __builtin_amdgcn_s_setprio(1);
+
     if (wave >= C::NCW) {
         // ================================================================ producer
         const int pw = wave - C::NCW;
@@ -934,8 +939,13 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         if (s >= 0 && lane_ == 0) lds_bump(cntX);
         lds_wait(cntX, C::NCW * static_cast<int>(s + 1));
         if (wave == 0) stamp(trace, lane_, s, 4);
+        // own rows of tile s+3 into the buffer just freed: before the MFMAs, or
+        // (MIGNN_SCHED_DMA_LATE) after the epilogue stores, away from the
+        // producers' gather burst at the start of the step
+        const bool dma_late = (flags & MIGNN_SCHED_DMA_LATE) != 0;
         bool dma = false;
-        if constexpr (!REC) dma = (s + 3 < nsteps) && x_dma(tile_of(s + 3));
+        if constexpr (!REC)
+            if (!dma_late) dma = (s + 3 < nsteps) && x_dma(tile_of(s + 3));
         if (wave == 0) stamp(trace, lane_, s, 5);
         if (mm) {
             // fragments of block (kc, ib) = step t = kc * IB + ib; the next
@@ -999,6 +1009,8 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                 }
             }
         }
+        if constexpr (!REC)
+            if (dma_late) dma = (s + 3 < nsteps) && x_dma(tile_of(s + 3));
         if (wave == 0) stamp(trace, lane_, s, 7);
         // the own rows DMA'd a step ago must have landed (producers read them
         // next step); this step's DMA (NPC) and row stores (NST), the youngest

@@ -276,7 +276,10 @@ __global__ __launch_bounds__(GNT, RPW == 1 ? 2 : 1) void gemm_f16x3_kernel(
         // all CBT column blocks: the image pads a partial tile with zero columns
 #pragma unroll
         for (int cb = 0; cb < CBT; ++cb) {
-            if (flags & MIGNN_DIAG_NO_MFMA) break;
+            // column blocks past N (a ragged last column tile, e.g. the 4
+            // per-head columns of TransformerConv's Q~K GEMM, N = 4H + 4):
+            // no MFMAs (uniform branch, nothing in flight behind it)
+            if ((flags & MIGNN_DIAG_NO_MFMA) || cb >= ncb) break;
             const f16x8 wh = *reinterpret_cast<const f16x8*>(wb + (2 * cb) * FRAG);
             const f16x8 wl = *reinterpret_cast<const f16x8*>(wb + (2 * cb + 1) * FRAG);
 #pragma unroll

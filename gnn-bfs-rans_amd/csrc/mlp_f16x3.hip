@@ -149,10 +149,14 @@ __device__ __forceinline__ int chain(f32x16* a, int pq, f16x8* oh, f16x8* ol,
 // 16-deep k-steps, three MFMAs per (nb, t); W fragments from LDS (fragment
 // (nb, t) at wl + (nb KT + t) FRAG, lane slice at byte offset loff), loaded
 // one step ahead.
-template <int NB, int KT>
+template <int NB, int KT, bool PRIO = false>
 __device__ __forceinline__ void layer_mfma(f32x16* acc, float sc, const unsigned char* wl,
                                            uint32_t loff, const f16x8* ah, const f16x8* al) {
     constexpr int FRAG = 2 * 64 * 16;
+    // PRIO: this wave's MFMA segment wins instruction arbitration over the
+    // SIMD partner's VALU segment (s_setprio), so the matrix pipe is fed
+    // first and the partner's split / ReLU work fills the gaps
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     auto ld = [&](int i, f16x8& hi, f16x8& lo) {
         hi = *reinterpret_cast<const f16x8*>(wl + i * FRAG + loff);
         lo = *reinterpret_cast<const f16x8*>(wl + i * FRAG + 64 * 16 + loff);
@@ -169,6 +173,7 @@ __device__ __forceinline__ void layer_mfma(f32x16* acc, float sc, const unsigned
         acc[nb] = mfma32(wo[i & 1], ah[t], acc[nb]);
         __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // ---- prep: one workgroup per layer -- exponent, split, permuted fragments,
@@ -225,7 +230,8 @@ __global__ __launch_bounds__(256) void mlp_prep_kernel(
 }
 
 // ---- head kernel (DIAG: timing ablations, results wrong by design:
-// 1 = no x loads, 2 = no MFMAs)
+// 1 = no x loads, 2 = no MFMAs; 4 = MFMA segments at raised priority, results
+// exact)
 template <int H, int DIAG = 0>
 __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t nrows, const unsigned char* __restrict__ img,
@@ -295,11 +301,11 @@ __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
         }
         // ---- L1 (H -> H) + ReLU
         if constexpr ((DIAG & 2) == 0)
-            layer_mfma<C::NB1, C::KT1>(acc, exp2_int(p + q1), lds, loff, ah, al);
+            layer_mfma<C::NB1, C::KT1, (DIAG & 4) != 0>(acc, exp2_int(p + q1), lds, loff, ah, al);
         p = chain<C::NB1, C::NB2>(acc, p + q1, ah, al, bimg + (C::BOFF2 >> 2));
         // ---- L2 (H -> H) + ReLU
         if constexpr ((DIAG & 2) == 0)
-            layer_mfma<C::NB2, C::KT2>(acc, exp2_int(p + q2), lds + C::W1_BYTES, loff, ah, al);
+            layer_mfma<C::NB2, C::KT2, (DIAG & 4) != 0>(acc, exp2_int(p + q2), lds + C::W1_BYTES, loff, ah, al);
         p = chain<C::NB2, C::NB3>(acc, p + q2, ah, al, bimg + (C::BOFF3 >> 2));
         // ---- L3 (H -> H/2) + ReLU.  Issued ahead of its MFMAs: W4 fragments,
         // L4's bias and the NEXT block's x rows (registers free from here on)
@@ -314,8 +320,8 @@ __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
         const int64_t row = blk * 32 + r32;
         load_x(blk + stride);
         if constexpr ((DIAG & 2) == 0)
-            layer_mfma<C::NB3, C::KT3>(acc, exp2_int(p + q3), lds + C::W1_BYTES + C::W2_BYTES,
-                                       loff, ah, al);
+            layer_mfma<C::NB3, C::KT3, (DIAG & 4) != 0>(acc, exp2_int(p + q3),
+                                                         lds + C::W1_BYTES + C::W2_BYTES, loff, ah, al);
         p = chain<C::NB3, 0>(acc, p + q3, ah, al, nullptr);
         // ---- L4 (H/2 -> out), no activation
         o *= exp2_int(p + q4);
@@ -402,7 +408,7 @@ extern "C" int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, con
 
 extern "C" int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img,
                                    float* out, void* stream) {
-    MIGNN_REQUIRE(x && img && out && n > 0 && mode >= 0 && mode <= 3, "diag_mlp_head: bad args");
+    MIGNN_REQUIRE(x && img && out && n > 0 && mode >= 0 && mode <= 4, "diag_mlp_head: bad args");
     hipStream_t st = as_stream(stream);
     int dev = 0, cus = 0;
     MIGNN_HIP(hipGetDevice(&dev));
@@ -414,7 +420,8 @@ extern "C" int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const vo
     case 0: hipLaunchKernelGGL((mlp_head_kernel<128, 0>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
     case 1: hipLaunchKernelGGL((mlp_head_kernel<128, 1>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
     case 2: hipLaunchKernelGGL((mlp_head_kernel<128, 2>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
-    default: hipLaunchKernelGGL((mlp_head_kernel<128, 3>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
+    case 3: hipLaunchKernelGGL((mlp_head_kernel<128, 3>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
+    default: hipLaunchKernelGGL((mlp_head_kernel<128, 4>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
     }
     return launch_status("mlp_head_kernel(diag)");
 }

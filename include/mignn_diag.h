@@ -19,7 +19,10 @@ enum {
     MIGNN_DIAG_NO_LOCAL = 8192,       /* f16x3 GCN layer: skip the in-tile (LDS) pass */
     MIGNN_DIAG_NO_TABLES = 16384,     /* f16x3 GCN layer: skip the lookup-table build */
     MIGNN_DIAG_PLAIN_STORE = 32768,   /* f16x3 GCN layer: plain (not non-temporal) stores */
-    MIGNN_SCHED_XCD_CHUNKS = 65536    /* f16x3 GCN layer: each XCD walks a contiguous tile range */
+    MIGNN_SCHED_XCD_CHUNKS = 65536,   /* f16x3 GCN layer: each XCD walks a contiguous tile range */
+    MIGNN_SCHED_PRIO_CONSUMERS = 131072, /* f16x3 GCN layer: consumer waves at s_setprio 1 */
+    MIGNN_SCHED_PRIO_PRODUCERS = 262144, /* f16x3 GCN layer: producer waves at s_setprio 1 */
+    MIGNN_SCHED_DMA_LATE = 524288        /* f16x3 GCN layer: own-row DMA after the epilogue */
 };
 /* mignn_gcn_layer / mignn_gcn_layer_f16x3 / mignn_linear with the flags above */
 int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
@@ -43,6 +46,7 @@ int mignn_diag_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1, cons
                             const float* shift, int flags, float* c, int64_t ldc, void* stream);
 
 /* mode 0: CSR gather (h = 128); 1: stencil gather on the periodic grid;
+ * 3: copy in the 16x16 MFMA-tile store pattern (16 rows x 64 B per instruction);
  * 2: streaming copy.  blocks <= 0: one row group per row. */
 int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t* col, const float* ew,
                       const float* x, int64_t n, int nx, int ny, int nz, int blocks, float* out,
@@ -57,7 +61,8 @@ int mignn_diag_set_trace(void* buf);
  * residual hand-off / before the step's barrier. */
 int mignn_diag_set_trace_f16x3(void* buf);
 
-/* Fused output head (H = 128, out_dim 7) timing ablations: mode bit 1 = no x
+/* Fused output head (H = 128, out_dim 7) timing ablations: mode 4 = MFMA
+ * segments at raised wave priority (exact results); mode bit 1 = no x
  * loads, bit 2 = no MFMAs (results wrong by design). */
 /* Shader clock probe: `blocks` workgroups of 4*iters dependent FMAs each;
  * out[2b] = s_memtime delta, out[2b+1] = s_memrealtime delta (100 MHz). */

@@ -180,7 +180,8 @@ def diag(mode_blocks):
 
 
 cases = {
-    "ring": (ring, 15), "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_chunks": (gcn16, 15 | 65536), "gcn16_no_produce": (gcn16, 15 | 256),
+    "ring": (ring, 15), "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_chunks": (gcn16, 15 | 65536), "gcn16_prio_cons": (gcn16, 15 | 131072), "gcn16_prio_prod": (gcn16, 15 | 262144), "gcn16_dma_late": (gcn16, 15 | 524288),
+    "gcn16_dma_late_plain": (gcn16, 15 | 524288 | 32768), "gcn16_no_produce": (gcn16, 15 | 256),
     "gcn16_no_mfma": (gcn16, 15 | 512), "gcn16_no_ext": (gcn16, 15 | 4096),
     "gcn16_no_tables_ext": (gcn16, 15 | 4096 | 16384),
     "gcn16_plain": (gcn16, 15 | 32768), "gcn16_no_produce_plain": (gcn16, 15 | 256 | 32768),
@@ -190,12 +191,13 @@ cases = {
     "gcn_xmaj": (gcn, 15 | 1024), "gcn_xmaj_no_mfma": (gcn, 15 | 1024 | 512),
     "layer0": (layer0, 0), "layer0_no_gather": (layer0diag, 1), "layer0_no_store": (layer0diag, 2),
     "layer0_neither": (layer0diag, 3), "head16": (head16, 0), "head16_no_xload": (headdiag, 1), "head16_no_mfma": (headdiag, 2),
-    "head16_valu_only": (headdiag, 3), "head32(4 launches)": (head32, 0),
+    "head16_valu_only": (headdiag, 3), "head16_prio": (headdiag, 4), "head32(4 launches)": (head32, 0),
     "gcn_aggregate_only(simple)": (agg, 0), "linear_rows": (lin, 9),
     "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0), "fill(torch)": (fill, 0), "colsum_read(torch)": (readsum, 0),
     "diag_csr_gather": (diag, (0, 0)), "diag_csr_gather_g2048": (diag, (0, 2048)),
     "diag_stencil_gather": (diag, (1, 0)), "diag_stencil_gather_g2048": (diag, (1, 2048)),
     "diag_copy": (diag, (2, 0)), "diag_copy_nt": (diag, (2 | 8, 0)),
+    "diag_tilecopy": (diag, (3, 0)), "diag_tilecopy_nt": (diag, (3 | 8, 0)),
     "diag_csr_remap": (diag, (0 | 4, 0)), "diag_csr_nt": (diag, (0 | 8, 0)),
     "diag_csr_remap_nt": (diag, (0 | 4 | 8, 0)), "diag_stencil_remap": (diag, (1 | 4, 0)),
     "diag_stencil_nt": (diag, (1 | 8, 0)), "diag_stencil_remap_nt": (diag, (1 | 4 | 8, 0)),
@@ -277,7 +279,9 @@ if os.environ.get("KB_CHECK"):
                                  P(b), P(sc), P(sh), 15, P(Y32), H, st), "gcn")
     Y16 = torch.full_like(X, float("nan"))
     _lib.check(L.mignn_diag_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
-                                       P(W), P(b), P(sc), P(sh), 15, P(Y16), H, st), "gcn16")
+                                       P(W), P(b), P(sc), P(sh),
+                                       15 | int(os.environ.get("KB_CHECK_FLAGS", "0")), P(Y16), H, st),
+               "gcn16")
     YR = torch.full_like(X, float("nan"))
     _lib.check(L.mignn_gcn_layer_ring(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                       P(W), P(b), P(sc), P(sh), 15, P(YR), H, SEG, st), "ring")

@@ -59,5 +59,11 @@ for k, disp in per.items():
             if c in mean:
                 row[c.replace("SQ_", "").lower() + "_frac"] = round(mean[c] / mean["SQ_WAVE_CYCLES"], 4)
     out[k] = row
-keep = {k: v for k, v in out.items() if "mignn" in k or k.endswith("_kernel") or "_kernel<" in k}
+def ours(k):
+    name = k.split(" [")[0]
+    return not name.startswith(("index_elementwise", "elementwise", "vectorized", "reduce_kernel",
+                                "trampoline", "init_lookback", "rocblas", "Cijk", "__amd"))
+
+
+keep = {k: v for k, v in out.items() if ours(k)}
 print(json.dumps(dict(sorted(keep.items())), indent=1))
