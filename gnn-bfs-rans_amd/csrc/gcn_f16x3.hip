@@ -21,10 +21,11 @@
 //
 // Structure: one 12-wave workgroup per CU, persistent over 64-row tiles,
 // XCD-aware tile order (as tile_gemm.hip), one barrier per tile step.
-//   * Own-row image (3 buffers): a tile's rows x[t0, t0+64) are copied
+//   * Own-row image (2 buffers; 3 in the records mode and the diagnostic
+//     MIGNN_SCHED_UNSTAGED form): a tile's rows x[t0, t0+64) are copied
 //     HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) issued by the consumer
-//     waves TWO steps ahead, unpadded, 16-B chunks XOR-swizzled by (row & 7)
-//     on the SOURCE address.  With a locality order (mignn_locality_order:
+//     waves one step ahead (two with 3 buffers), unpadded, 16-B chunks
+//     XOR-swizzled by (row & 7) on the SOURCE address.  With a locality order (mignn_locality_order:
 //     Morton curve) ~70 % of a mesh's CSR entries point inside their tile.
 //   * 8 producer waves, 8 rows each (two quads of 4 rows; a row = 16 lanes x
 //     32 B).  Per tile, vectorised over the wave's CSR entries (lane = entry),
@@ -39,7 +40,12 @@
 //   * 4 consumer waves (one per SIMD), 32 output columns each, split W held in
 //     registers for the whole launch.  (residual + bias) * 2^(p_row + q_w)
 //     seeds the accumulator, 3 MFMAs per 16x16x32 block, epilogue (unscale,
-//     BN affine, ReLU) from the accumulators, 16-B row-segment stores.
+//     BN affine, ReLU) from the accumulators into an LDS staging tile (the
+//     third image buffer's space), then whole rows out: a half-wave stores
+//     one 512-B row (H = 128) -- the accumulator layout would store 16 rows x
+//     64 B per instruction, measured 1.5x slower as a plain copy
+//     (profiles/r02_kbench_store_patterns.json) and 2 % (H = 128) / 9 %
+//     (H = 64) slower in this kernel.
 //   * Hand-offs (LDS counters, relaxed: a wave's LDS operations execute in
 //     order): consumers bump cntX once they hold their residual -- then the
 //     own-row buffer takes the tile three steps on; they bump cntA once their
@@ -56,7 +62,11 @@ using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 using f16x4 = __attribute__((ext_vector_type(4))) _Float16;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int H>
+// STG: two own-row image buffers (the own rows DMA'd one step ahead) and an
+// output staging tile in the LDS they free: the consumers write their
+// accumulator blocks there and store whole rows (512 B per half-wave at
+// H = 128) instead of 16 rows x 64 B per instruction
+template <int H, bool STG = false>
 struct SCfg {
     static_assert(H == 64 || H == 128, "f16x3 GCN layer: H in {64, 128}");
     static constexpr int BM = 64;                  // rows per tile
@@ -85,7 +95,7 @@ struct SCfg {
     static constexpr int LPR = 64 / RPP;           // lanes per row in a piece
     static constexpr int NPIECE = BM / RPP;        // pieces per tile
     static constexpr int NPC = NPIECE / NCW;       // DMA pieces per consumer per tile
-    static constexpr int XBUF = 3;                 // own-row image buffers
+    static constexpr int XBUF = STG ? 2 : 3;       // own-row image buffers
     static constexpr int X_BYTES = BM * ROWB;
     static constexpr int A_BYTES = BM * AS * 2;
     // Xs[3] | zero row | Ah | Al | rexp[BM] | tables[2][NPW] | epi | counters
@@ -97,8 +107,10 @@ struct SCfg {
     static constexpr int OFF_REXP = OFF_AL + A_BYTES;
     static constexpr int OFF_TAB = OFF_REXP + BM * 4;
     static constexpr int OFF_EPI = OFF_TAB + 2 * NPW * TAB_BYTES;   // bias | scale | shift [H]
-    static constexpr int OFF_CNT = OFF_EPI + 3 * H * 4;             // cntX, cntA
-    static constexpr int LDS_BYTES = OFF_CNT + 16;
+    static constexpr int OFF_CNT = OFF_EPI + 3 * H * 4;             // cntX, cntA, cntS
+    static constexpr int OFF_STG = OFF_CNT + 16;                     // STG: [BM][ROWB]
+    static constexpr int LDS_BYTES = OFF_STG + (STG ? BM * ROWB : 0);
+    static constexpr int NSTG = BM * ROWB / 1024 / NCW;             // STG row stores per consumer
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     // records mode (layer 1 from layer-0 records, gcn_layer0.hip): the
     // expansion coefficients [H][8] after everything else
@@ -282,7 +294,7 @@ __device__ __forceinline__ void p_load_entries(PIdx& t, const int32_t* __restric
 // on the fly, all by the producers: the own rows of tile s+2 into the image
 // at the end of step s (their records gathered at its start), the
 // out-of-tile rows in registers next to their gathered records.
-template <int H, bool REC>
+template <int H, bool REC, bool STG>
 __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t row_begin,
@@ -290,10 +302,12 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift, int flags,
     float* __restrict__ out, int64_t ldo, const float* __restrict__ rec,
     const float* __restrict__ coef8, unsigned long long* trace) {
-    using C = SCfg<H>;
+    static_assert(!(REC && STG), "records mode keeps three image buffers");
+    using C = SCfg<H, STG>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[REC ? C::LDS_BYTES_REC : C::LDS_BYTES];
     int* const cntX = reinterpret_cast<int*>(lds + C::OFF_CNT);
     int* const cntA = cntX + 1;
+    int* const cntS = cntX + 2;
     _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
     _Float16* const AL = reinterpret_cast<_Float16*>(lds + C::OFF_AL);
     int* const REXP = reinterpret_cast<int*>(lds + C::OFF_REXP);
@@ -309,12 +323,13 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const int slot = blockIdx.x >> 3;
     const int per_xcd = G >> 3;
     const int64_t nsteps = (ntiles + G - 1) / G;
-    // default: at step s the chip covers tiles [sG, (s+1)G), XCD x a run of
-    // per_xcd of them.  MIGNN_SCHED_XCD_CHUNKS: XCD x walks its own contiguous
-    // range of nsteps * per_xcd tiles (per_xcd per step), so in a locality
-    // order a tile's neighbours were read by the same XCD a step or two
-    // earlier and are still in its L2.
-    const bool chunks = (flags & MIGNN_SCHED_XCD_CHUNKS) != 0;
+    // XCD x walks its own contiguous range of nsteps * per_xcd tiles
+    // (per_xcd per step), so in the locality order (two z-levels of a 4x4
+    // block-column panel per step) a tile's lateral neighbours are read by the
+    // same XCD in the same step and its z neighbours a step apart, in its L2.
+    // MIGNN_SCHED_INTERLEAVED (the round-1 schedule): at step s the chip
+    // covers tiles [sG, (s+1)G), XCD x a run of per_xcd of them.
+    const bool chunks = (flags & MIGNN_SCHED_INTERLEAVED) == 0;
     const int64_t chunk = chunks ? nsteps * per_xcd : per_xcd;
     const int64_t sstride = chunks ? per_xcd : G;
     auto tile_of = [&](int64_t s) -> int64_t { return (int64_t)xcd * chunk + s * sstride + slot; };
@@ -326,6 +341,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     if (tid == 0) {
         cntX[0] = 0;
         cntA[0] = 0;
+        cntS[0] = 0;
     }
 
     // static wave priority (diagnostic schedules): consumers or producers
@@ -397,7 +413,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         // from its 8 lanes
         auto expand_tile = [&](int64_t step, const OWN& own) {
             if (tile_of(step) >= ntiles) return;
-            const int sb = static_cast<int>(step % 3);      // its image buffer (xbuf_of)
+            const int sb = static_cast<int>(step % C::XBUF); // its image buffer (xbuf_of)
             const int erg = lane_ / C::CPL, ecl = lane_ % C::CPL;
             f32x4 ca[4], cb[4];
             load_pc(ecl, ca, cb);
@@ -904,7 +920,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         block_barrier<0x70>();
     } else {
         x_dma(tile_of(0));
-        x_dma(tile_of(1));
+        if constexpr (!STG) x_dma(tile_of(1));   // (STG: tile 1 at step -1)
     }
     block_barrier<0x70>();   // own rows of tiles 0 and 1 landed: vmcnt(0) lgkmcnt(0)
     for (int64_t s = -1; s < nsteps; ++s) {
@@ -945,7 +961,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         const bool dma_late = (flags & MIGNN_SCHED_DMA_LATE) != 0;
         bool dma = false;
         if constexpr (!REC)
-            if (!dma_late) dma = (s + 3 < nsteps) && x_dma(tile_of(s + 3));
+            if (!dma_late) dma = (s + C::XBUF < nsteps) && x_dma(tile_of(s + C::XBUF));
         if (wave == 0) stamp(trace, lane_, s, 5);
         if (mm) {
             // fragments of block (kc, ib) = step t = kc * IB + ib; the next
@@ -1001,7 +1017,13 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                         if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
                         o[r] = v;
                     }
-                    if (row < row_end) {
+                    if constexpr (STG) {
+                        // staging tile: row lr, 16-B chunk ch at position ch ^ (lr & 15)
+                        const int lr = (wm * C::IB + ib) * 16 + rr;
+                        const int ch = ((n0 + 16 * jb) >> 2) + gg;
+                        *reinterpret_cast<f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4)) =
+                            f32x4{o[0], o[1], o[2], o[3]};
+                    } else if (row < row_end) {
                         f32x4* const dst = reinterpret_cast<f32x4*>(out + row * ldo + n0 + 16 * jb + 4 * gg);
                         if (flags & MIGNN_DIAG_PLAIN_STORE) *dst = f32x4{o[0], o[1], o[2], o[3]};
                         else __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, dst);
@@ -1009,26 +1031,53 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                 }
             }
         }
+        if constexpr (STG) {
+            // every consumer's blocks staged -> whole rows: consumer w stores
+            // rows 16 w .. 16 w + 15, two per instruction (a half-wave per row)
+            if (s >= 0 && lane_ == 0) lds_bump(cntS);
+            if (mm) {
+                lds_wait(cntS, C::NCW * static_cast<int>(s + 1));
+                const int64_t t0 = row_begin + tile * C::BM;
+                constexpr int LPRW = C::ROWB / 16;          // lanes per row (32 at H = 128)
+                constexpr int RPI = 64 / LPRW;              // rows per store instruction
+                const int ch = lane_ % LPRW;
+#pragma unroll
+                for (int i = 0; i < C::NSTG; ++i) {
+                    const int lr = wave * (C::BM / C::NCW) + i * RPI + lane_ / LPRW;
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(
+                        lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4));
+                    if (t0 + lr < row_end)
+                        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + 4 * ch));
+                }
+            }
+        }
         if constexpr (!REC)
-            if (dma_late) dma = (s + 3 < nsteps) && x_dma(tile_of(s + 3));
+            if (dma_late) dma = (s + C::XBUF < nsteps) && x_dma(tile_of(s + C::XBUF));
         if (wave == 0) stamp(trace, lane_, s, 7);
         // the own rows DMA'd a step ago must have landed (producers read them
         // next step); this step's DMA (NPC) and row stores (NST), the youngest
         // vector-memory operations, may stay in flight
         constexpr int npc = C::NPC;
-        if (dma && stored) block_barrier<0x70 | (npc + C::NST)>();
-        else if (dma) block_barrier<0x70 | npc>();
-        else if (stored) block_barrier<0x70 | C::NST>();
-        else block_barrier<0x70>();
+        if constexpr (STG) {
+            // two image buffers: this step's DMA (tile s+2) is read by the
+            // producers next step -- it must land now; the row stores may fly
+            if (stored) block_barrier<0x70 | C::NSTG>();
+            else block_barrier<0x70>();
+        } else {
+            if (dma && stored) block_barrier<0x70 | (npc + C::NST)>();
+            else if (dma) block_barrier<0x70 | npc>();
+            else if (stored) block_barrier<0x70 | C::NST>();
+            else block_barrier<0x70>();
+        }
     }
 }
 
-template <int H, bool REC>
+template <int H, bool REC, bool STG = false>
 int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                  int64_t ldx, int64_t rb, int64_t re, const float* w, const float* bias,
                  const float* scale, const float* shift, int flags, float* out, int64_t ldo,
                  const float* rec, const float* coef8, hipStream_t st) {
-    using C = SCfg<H>;
+    using C = SCfg<H, STG>;
     static int grid_cache[64] = {0};
     int dev = 0;
     MIGNN_HIP(hipGetDevice(&dev));
@@ -1042,7 +1091,7 @@ int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, co
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL((gcn_f16x3_kernel<H, REC>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col,
+    hipLaunchKernelGGL((gcn_f16x3_kernel<H, REC, STG>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col,
                        ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, rec, coef8,
                        (flags & MIGNN_DIAG_TRACE) ? g_trace16_host : nullptr);
     return launch_status("gcn_f16x3_kernel");
@@ -1085,6 +1134,13 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
     MIGNN_REQUIRE(x != out, "gcn_layer_f16x3: in-place not supported (neighbours read x)");
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
+    if (!(flags & MIGNN_SCHED_UNSTAGED))
+        return h == 128 ? launch_f16x3<128, false, true>(row_ptr, col, ew, x, ldx, rb, re, w, bias,
+                                                         scale, shift, flags, out, ldo, nullptr,
+                                                         nullptr, st)
+                        : launch_f16x3<64, false, true>(row_ptr, col, ew, x, ldx, rb, re, w, bias,
+                                                        scale, shift, flags, out, ldo, nullptr,
+                                                        nullptr, st);
     return h == 128 ? launch_f16x3<128, false>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,
                                                shift, flags, out, ldo, nullptr, nullptr, st)
                     : launch_f16x3<64, false>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,

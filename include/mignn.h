@@ -83,8 +83,9 @@ int mignn_csr_build_gcn(const int64_t* edge_index, int64_t num_edges, int64_t nu
  * reference counterpart: the forward's results are the same up to fp32
  * summation order).  pos: [n, >=3] cell centres (FlowGNN's node features,
  * reference graph_constructor.py:259), row stride ldp.  Cells of the mesh
- * spacing (per axis, from the edges) are grouped into 4x4 pencils swept along
- * the third axis, so a 64-row tile of the fused layer is a 4x4x4 block.
+ * spacing (per axis, from the edges) are grouped into 4x4x4 blocks (a 64-row
+ * tile of the fused layer each), the blocks into panels of 4x4 block columns
+ * swept along the third axis.
  * Outputs perm[new] = old node id and inv[old] = new (int32, n each); stable
  * (ties keep input order).  Scratch: mignn_locality_order_scratch_bytes(n). */
 size_t mignn_locality_order_scratch_bytes(int64_t n);

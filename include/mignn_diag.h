@@ -19,10 +19,14 @@ enum {
     MIGNN_DIAG_NO_LOCAL = 8192,       /* f16x3 GCN layer: skip the in-tile (LDS) pass */
     MIGNN_DIAG_NO_TABLES = 16384,     /* f16x3 GCN layer: skip the lookup-table build */
     MIGNN_DIAG_PLAIN_STORE = 32768,   /* f16x3 GCN layer: plain (not non-temporal) stores */
-    MIGNN_SCHED_XCD_CHUNKS = 65536,   /* f16x3 GCN layer: each XCD walks a contiguous tile range */
+    MIGNN_SCHED_INTERLEAVED = 65536,  /* f16x3 GCN layer: step s covers tiles [sG, (s+1)G) (the
+                                         default: each XCD walks a contiguous tile range) */
     MIGNN_SCHED_PRIO_CONSUMERS = 131072, /* f16x3 GCN layer: consumer waves at s_setprio 1 */
     MIGNN_SCHED_PRIO_PRODUCERS = 262144, /* f16x3 GCN layer: producer waves at s_setprio 1 */
-    MIGNN_SCHED_DMA_LATE = 524288        /* f16x3 GCN layer: own-row DMA after the epilogue */
+    MIGNN_SCHED_DMA_LATE = 524288,       /* f16x3 GCN layer: own-row DMA after the epilogue */
+    MIGNN_SCHED_UNSTAGED = 1048576       /* f16x3 GCN layer: the round-1 form -- 3 image buffers,
+                                            stores straight from the 16x16 accumulators (the
+                                            default stages whole output rows in LDS) */
 };
 /* mignn_gcn_layer / mignn_gcn_layer_f16x3 / mignn_linear with the flags above */
 int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,

@@ -300,11 +300,16 @@ def test_mlp_head_rejects_bad_shapes():
 
 # ------------------------------------------------------------------ locality order
 def _pencil_order_np(nx, ny, nz):
-    """numpy restatement of the 4x4-pencil key on the natural grid labels."""
+    """numpy restatement of the locality key on the natural grid labels:
+    4x4x4-cell blocks in panels of 4x4 block columns swept along z
+    (csrc/reorder.hip order_keys_kernel)."""
     v = np.arange(nx * ny * nz)
     i, j, k = v % nx, (v // nx) % ny, v // (nx * ny)
-    nbx = (nx + 3) // 4
-    key = (((j // 4) * nbx + i // 4) * nz + k) * 16 + (j % 4) * 4 + i % 4
+    ti, tj, tk = i // 4, j // 4, k // 4
+    npx = ((nx + 3) // 4 + 3) // 4
+    ntz = (nz + 3) // 4
+    blk = (((tj // 4) * npx + ti // 4) * ntz + tk) * 16 + (tj % 4) * 4 + ti % 4
+    key = blk * 64 + (k % 4) * 16 + (j % 4) * 4 + i % 4
     return np.argsort(key, kind="stable")
 
 
