@@ -5,6 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu --no-bfs}"
+mkdir -p gpurun_out/pmc
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
