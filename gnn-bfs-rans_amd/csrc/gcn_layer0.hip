@@ -137,6 +137,116 @@ __global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
     }
 }
 
+// Split-role form (the default for mignn_gcn_layer0_coords): a workgroup of
+// 4 gather waves + 4 store waves walks 256-row blocks.  At iteration i the
+// gather waves (lane = row, as pass 1 above) aggregate block i into LDS
+// buffer i % 2 while the store waves expand and write block i - 1 from the
+// other buffer; one barrier per block.  The write stream (N*H*4 bytes, the
+// bound) no longer waits behind each wave's three dependent gather round
+// trips (row_ptr -> col / ew -> pos).  Same fma order as gcn_layer0_kernel:
+// bit-identical output.
+constexpr int kSplitRows = kWaves * 64;   // rows per block
+
+template <int D>
+__global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
+    int64_t row_end, const float* __restrict__ coef, int h, float* __restrict__ out,
+    int64_t ldo) {
+    constexpr int K = 2 * D + 2;
+    __shared__ float agg[2][kSplitRows][K];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const bool gather = wave < kWaves;
+    const int64_t nrows = row_end - row_begin;
+    const int64_t nblk = (nrows + kSplitRows - 1) / kSplitRows;
+    // store role: lane owns columns cq .. cq + 3 of rps rows per instruction
+    const int cpl = h / 4, rps = 64 / cpl;
+    const int sub = lane / cpl, cq = (lane % cpl) * 4;
+    const bool active = sub < rps;
+    float cf[4][K];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            cf[q][k] = (!gather && active) ? coef[(int64_t)(cq + q) * K + k] : 0.f;
+    // blocks b = blockIdx.x + i * gridDim.x; iteration i gathers b_i, stores b_{i-1}
+    for (int64_t i = 0;; ++i) {
+        const int64_t bg = blockIdx.x + i * (int64_t)gridDim.x;        // gathered now
+        const int64_t bs = bg - gridDim.x;                              // stored now
+        if (bs >= nblk) break;
+        const int buf = static_cast<int>(i & 1);
+        if (gather) {
+            const int64_t r = bg * kSplitRows + wave * 64 + lane;
+            if (bg < nblk && r < nrows) {
+                const int64_t ri = row_begin + r;
+                float c[D], C[D], sum = 0.f;
+#pragma unroll
+                for (int a = 0; a < D; ++a) { c[a] = pos[ri * ldp + a]; C[a] = 0.f; }
+                const int32_t e0 = row_ptr[ri], e1 = row_ptr[ri + 1];
+                constexpr int kU = 8;
+                int32_t jj[kU];
+                float ww[kU];
+#pragma unroll
+                for (int k = 0; k < kU; ++k) {
+                    jj[k] = e0 + k < e1 ? col[e0 + k] : 0;
+                    ww[k] = e0 + k < e1 ? ew[e0 + k] : 0.f;
+                }
+                float pv[kU][D];
+#pragma unroll
+                for (int k = 0; k < kU; ++k)
+#pragma unroll
+                    for (int a = 0; a < D; ++a)
+                        pv[k][a] = e0 + k < e1 ? pos[(int64_t)jj[k] * ldp + a] : 0.f;
+#pragma unroll
+                for (int k = 0; k < kU; ++k) {
+                    if (e0 + k < e1) {
+                        sum += ww[k];
+#pragma unroll
+                        for (int a = 0; a < D; ++a) C[a] = fmaf(ww[k], pv[k][a], C[a]);
+                    }
+                }
+                for (int32_t e = e0 + kU; e < e1; ++e) {
+                    const int64_t j = col[e];
+                    const float w = ew[e];
+                    sum += w;
+#pragma unroll
+                    for (int a = 0; a < D; ++a) C[a] = fmaf(w, pos[j * ldp + a], C[a]);
+                }
+                float* const ag = agg[buf][wave * 64 + lane];
+#pragma unroll
+                for (int a = 0; a < D; ++a) { ag[a] = c[a]; ag[D + a] = C[a]; }
+                ag[2 * D] = sum;
+            }
+        } else if (bs >= 0) {
+            // store wave w - kWaves: rows [64 (w - kWaves), +64) of block bs
+            const int64_t base = bs * kSplitRows + (wave - kWaves) * 64;
+            const int64_t nb = nrows - base < 64 ? nrows - base : 64;
+            const float(*ag)[K] = agg[buf ^ 1] + (wave - kWaves) * 64;
+            for (int rr = 0; rr < nb; rr += rps) {
+                const int rl = rr + sub;
+                if (active && rl < nb) {
+                    float v[K - 1];
+#pragma unroll
+                    for (int k = 0; k < K - 1; ++k) v[k] = ag[rl][k];
+                    float o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float t = cf[q][K - 1];
+#pragma unroll
+                        for (int k = 0; k < K - 1; ++k) t = fmaf(cf[q][k], v[k], t);
+                        o[q] = t < 0.f ? 0.f : t;
+                    }
+                    __builtin_nontemporal_store(
+                        f32x4{o[0], o[1], o[2], o[3]},
+                        reinterpret_cast<f32x4*>(out + (row_begin + base + rl) * ldo + cq));
+                }
+            }
+        }
+        __syncthreads();   // buffer i % 2 filled; buffer (i - 1) % 2 drained
+    }
+}
+
 }  // namespace
 }  // namespace mignn
 
@@ -155,15 +265,16 @@ extern "C" int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* co
     MIGNN_REQUIRE(row_begin >= 0 && row_end >= row_begin, "gcn_layer0: bad row range");
     if (row_end == row_begin) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
-    const int64_t blocks = (row_end - row_begin + kWaves * 64 - 1) / (kWaves * 64);
-    const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);
+    // split roles: 8-wave workgroups, a few 256-row blocks each (2 per CU)
+    const int64_t blocks = (row_end - row_begin + kSplitRows - 1) / kSplitRows;
+    const unsigned grid = static_cast<unsigned>(blocks < 512 ? blocks : 512);
     switch (in_dim) {
-    case 1: hipLaunchKernelGGL(gcn_layer0_kernel<1>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
-    case 2: hipLaunchKernelGGL(gcn_layer0_kernel<2>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
-    case 3: hipLaunchKernelGGL(gcn_layer0_kernel<3>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
-    default: hipLaunchKernelGGL(gcn_layer0_kernel<4>, dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    case 1: hipLaunchKernelGGL(gcn_layer0_split_kernel<1>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    case 2: hipLaunchKernelGGL(gcn_layer0_split_kernel<2>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    case 3: hipLaunchKernelGGL(gcn_layer0_split_kernel<3>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    default: hipLaunchKernelGGL(gcn_layer0_split_kernel<4>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
     }
-    return launch_status("gcn_layer0_kernel");
+    return launch_status("gcn_layer0_split_kernel");
 }
 
 extern "C" int mignn_gcn_layer0_records(const int32_t* row_ptr, const int32_t* col,
@@ -192,7 +303,14 @@ extern "C" int mignn_gcn_layer0_records(const int32_t* row_ptr, const int32_t* c
 extern "C" int mignn_diag_gcn_layer0(int mode, const int32_t* row_ptr, const int32_t* col,
                                      const float* ew, const float* pos, int64_t n,
                                      const float* coef, float* out, void* stream) {
-    MIGNN_REQUIRE(mode >= 0 && mode <= 3 && n > 0, "diag_gcn_layer0: bad args");
+    MIGNN_REQUIRE(mode >= 0 && mode <= 4 && n > 0, "diag_gcn_layer0: bad args");
+    if (mode == 4) {   // the round-1 one-role kernel (exact results), for A/B timing
+        const int64_t b1 = (n + kWaves * 64 - 1) / (kWaves * 64);
+        hipLaunchKernelGGL((gcn_layer0_kernel<3, 0>), dim3(static_cast<unsigned>(b1 < 8192 ? b1 : 8192)),
+                           dim3(kWaves * 64), 0, as_stream(stream), row_ptr, col, ew, pos, 3, 0, n,
+                           coef, 128, out, 128);
+        return launch_status("gcn_layer0_kernel(diag)");
+    }
     hipStream_t st = as_stream(stream);
     const int64_t blocks = (n + kWaves * 64 - 1) / (kWaves * 64);
     const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);

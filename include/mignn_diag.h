@@ -72,7 +72,8 @@ int mignn_diag_set_trace_f16x3(void* buf);
  * out[2b] = s_memtime delta, out[2b+1] = s_memrealtime delta (100 MHz). */
 int mignn_diag_clock(int blocks, int iters, int64_t* out, void* stream);
 
-/* input_proj + GCN layer 0 (H = 128, D = 3) timing ablations: bit 1 = no
+/* input_proj + GCN layer 0 (H = 128, D = 3) timing ablations (mode 4: the
+ * one-role round-1 kernel, exact): bit 1 = no
  * neighbour gathers, bit 2 = no stores (results wrong by design). */
 int mignn_diag_gcn_layer0(int mode, const int32_t* row_ptr, const int32_t* col, const float* ew,
                           const float* pos, int64_t n, const float* coef, float* out,

@@ -190,7 +190,7 @@ cases = {
     "gcn16_only_dma": (gcn16, 15 | 256 | 512), "gcn_no_mfma": (gcn, 15 | 512), "gcn_no_gather": (gcn, 15 | 256),
     "gcn_xmaj": (gcn, 15 | 1024), "gcn_xmaj_no_mfma": (gcn, 15 | 1024 | 512),
     "layer0": (layer0, 0), "layer0_no_gather": (layer0diag, 1), "layer0_no_store": (layer0diag, 2),
-    "layer0_neither": (layer0diag, 3), "head16": (head16, 0), "head16_no_xload": (headdiag, 1), "head16_no_mfma": (headdiag, 2),
+    "layer0_neither": (layer0diag, 3), "layer0_onerole": (layer0diag, 4), "head16": (head16, 0), "head16_no_xload": (headdiag, 1), "head16_no_mfma": (headdiag, 2),
     "head16_valu_only": (headdiag, 3), "head16_prio": (headdiag, 4), "head32(4 launches)": (head32, 0),
     "gcn_aggregate_only(simple)": (agg, 0), "linear_rows": (lin, 9),
     "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0), "fill(torch)": (fill, 0), "colsum_read(torch)": (readsum, 0),
