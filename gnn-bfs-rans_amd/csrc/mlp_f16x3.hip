@@ -231,9 +231,11 @@ __global__ __launch_bounds__(256) void mlp_prep_kernel(
 
 // ---- head kernel (DIAG: timing ablations, results wrong by design:
 // 1 = no x loads, 2 = no MFMAs; 4 = MFMA segments at raised priority, results
-// exact)
-template <int H, int DIAG = 0>
-__global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
+// exact).  NWV waves per workgroup: 8 (two per SIMD, the next block's x rows
+// prefetched into registers during layer 3) or 12 (three per SIMD at <= 168
+// VGPRs: no register prefetch, the third wave covers the loads)
+template <int H, int DIAG = 0, int NWV = 8>
+__global__ __launch_bounds__(NWV * 64) void mlp_head_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t nrows, const unsigned char* __restrict__ img,
     int out_dim, float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
     using C = MCfg<H>;
@@ -243,14 +245,15 @@ __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
     const int h = lane >> 5, r32 = lane & 31;
 
     // W1..W3 images -> LDS (16 B per thread per step)
-    for (int i = threadIdx.x; i < C::LDS_BYTES / 16; i += C::NT)
+    for (int i = threadIdx.x; i < C::LDS_BYTES / 16; i += NWV * 64)
         reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(img)[i];
     const int* qv = reinterpret_cast<const int*>(img + C::EXP_AT);
     const int q1 = qv[0], q2 = qv[1], q3 = qv[2], q4 = qv[3];
     __syncthreads();
 
     const int64_t nblk = (nrows + 31) / 32;
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * C::NW;
+    constexpr bool PF = NWV == 8;        // register prefetch of the next block's x
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * NWV;
     // x row fragments of a block: k-step t -> x[row][16 t + 8 h .. +7];
     // rows past the end (and blocks past the last) read a valid row
     float xv[C::KT1][8];
@@ -270,9 +273,10 @@ __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
             xv[t][4] = v.x; xv[t][5] = v.y; xv[t][6] = v.z; xv[t][7] = v.w;
         }
     };
-    int64_t blk = static_cast<int64_t>(blockIdx.x) * C::NW + wave;
-    load_x(blk);
+    int64_t blk = static_cast<int64_t>(blockIdx.x) * NWV + wave;
+    if constexpr (PF) load_x(blk);
     for (; blk < nblk; blk += stride) {
+        if constexpr (!PF) load_x(blk);
         // opaque per-block offsets: keep the loop-invariant LDS fragment, W4
         // and bias loads inside the loop instead of hoisted into registers
         uint32_t loff = static_cast<uint32_t>(lane) * 16;
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(MCfg<H>::NT) void mlp_head_kernel(
         }
         f32x16 o = ldbias(bimg + (C::BOFF4 >> 2));
         const int64_t row = blk * 32 + r32;
-        load_x(blk + stride);
+        if constexpr (PF) load_x(blk + stride);
         if constexpr ((DIAG & 2) == 0)
             layer_mfma<C::NB3, C::KT3, (DIAG & 4) != 0>(acc, exp2_int(p + q3),
                                                          lds + C::W1_BYTES + C::W2_BYTES, loff, ah, al);
@@ -408,7 +412,7 @@ extern "C" int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, con
 
 extern "C" int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img,
                                    float* out, void* stream) {
-    MIGNN_REQUIRE(x && img && out && n > 0 && mode >= 0 && mode <= 4, "diag_mlp_head: bad args");
+    MIGNN_REQUIRE(x && img && out && n > 0 && mode >= 0 && mode <= 5, "diag_mlp_head: bad args");
     hipStream_t st = as_stream(stream);
     int dev = 0, cus = 0;
     MIGNN_HIP(hipGetDevice(&dev));
@@ -421,7 +425,13 @@ extern "C" int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const vo
     case 1: hipLaunchKernelGGL((mlp_head_kernel<128, 1>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
     case 2: hipLaunchKernelGGL((mlp_head_kernel<128, 2>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
     case 3: hipLaunchKernelGGL((mlp_head_kernel<128, 3>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
-    default: hipLaunchKernelGGL((mlp_head_kernel<128, 4>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
+    case 4: hipLaunchKernelGGL((mlp_head_kernel<128, 4>), dim3(grid), dim3(512), 0, st, x, 128, n, im, 7, out, 7, nullptr); break;
+    default: {   // 12 waves per workgroup (exact results)
+        const int64_t w12 = ((n + 31) / 32 + 11) / 12;
+        const int g12 = static_cast<int>(w12 < cus ? w12 : cus);
+        hipLaunchKernelGGL((mlp_head_kernel<128, 0, 12>), dim3(g12), dim3(768), 0, st, x, 128, n, im, 7, out, 7, nullptr);
+        break;
+    }
     }
     return launch_status("mlp_head_kernel(diag)");
 }

@@ -191,7 +191,7 @@ cases = {
     "gcn_xmaj": (gcn, 15 | 1024), "gcn_xmaj_no_mfma": (gcn, 15 | 1024 | 512),
     "layer0": (layer0, 0), "layer0_no_gather": (layer0diag, 1), "layer0_no_store": (layer0diag, 2),
     "layer0_neither": (layer0diag, 3), "layer0_onerole": (layer0diag, 4), "head16": (head16, 0), "head16_no_xload": (headdiag, 1), "head16_no_mfma": (headdiag, 2),
-    "head16_valu_only": (headdiag, 3), "head16_prio": (headdiag, 4), "head32(4 launches)": (head32, 0),
+    "head16_valu_only": (headdiag, 3), "head16_prio": (headdiag, 4), "head16_w12": (headdiag, 5), "head32(4 launches)": (head32, 0),
     "gcn_aggregate_only(simple)": (agg, 0), "linear_rows": (lin, 9),
     "linear_no_mfma": (lin, 9 | 512), "linear_no_load": (lin, 9 | 256), "copy(torch)": (copy, 0), "fill(torch)": (fill, 0), "colsum_read(torch)": (readsum, 0),
     "diag_csr_gather": (diag, (0, 0)), "diag_csr_gather_g2048": (diag, (0, 2048)),
@@ -262,7 +262,7 @@ if os.environ.get("KB_RTRACE"):
     res["ring_trace_cycles_median"]["barrier"] = float((t[:, 3:61, 0] - t[:, 2:60, 9]).median())
     res["ring_trace_cycles_median"]["step"] = float((t[:, 3:61, 0] - t[:, 2:60, 0]).median())
 if os.environ.get("KB_CHECK_HEAD"):
-    head16(0)
+    headdiag(int(os.environ.get("KB_CHECK_HEAD_MODE", "0"))) if os.environ.get("KB_CHECK_HEAD_MODE") else head16(0)
     torch.cuda.synchronize()
     rows = torch.randint(0, n, (8192,), generator=torch.Generator().manual_seed(5)).to(dev)
     h = X[rows].double()
