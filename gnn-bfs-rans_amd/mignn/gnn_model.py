@@ -703,15 +703,22 @@ class FlowGNN(nn.Module):
                 hit = self._prep[key] = make()
         return hit
 
-    def _mm(self, tag, i, srcs, w, a, bias=None, **kw):
-        """Node transform by W = w (w derived from the parameters `srcs`):
-        the split-fp16 GEMM (precision "f16x3") for the shapes the fused
-        kernels leave over (k or n > 128, n >= 64), its W image cached per
-        parameter version; exact fp32 MFMA (mignn_linear) otherwise."""
+    def _img(self, tag, i, srcs, w):
+        """The split-fp16 image of W = w (derived from the parameters `srcs`,
+        cached per parameter version) when the transform runs in split fp16
+        (precision "f16x3" and a shape the fused kernels leave over: k or n >
+        128, n >= 64); None: exact fp32 MFMA."""
         n, k = w.shape
         if self.precision == "f16x3" and n >= 64 and (n > 128 or k > 128):
-            img = self._cached(tag, i, srcs, lambda: f16x3_image(w))
-            return linear_f16x3(a, img, n, bias, **kw)
+            return self._cached(tag, i, srcs, lambda: f16x3_image(w))
+        return None
+
+    def _mm(self, tag, i, srcs, w, a, bias=None, **kw):
+        """Node transform by W = w: split-fp16 GEMM (mignn_linear_f16x3) or
+        exact fp32 MFMA (mignn_linear), as _img decides."""
+        img = self._img(tag, i, srcs, w)
+        if img is not None:
+            return linear_f16x3(a, img, w.shape[0], bias, **kw)
         return linear(a, w, bias, **kw)
 
     def _layer(self, i, layer, csr: Csr, x, out, rb: int, re: int, logits=None):
@@ -762,33 +769,37 @@ class FlowGNN(nn.Module):
             self._mm("w_gin2", i, (nn2.weight,), nn2.weight, h1, nn2.bias, relu=True,
                      residual=x[rb:re], scale=scale, shift=shift, out=out[rb:re])
         elif self.layer_type == "GAT":
+            # one C-ABI call (csrc/attn_layers.hip): logits (unless given by
+            # a sharded caller), softmax aggregation, head-mean transform
             wlog, wcat = self._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
                                       lambda: self._gat_weights(layer))
-            if logits is None:
-                logits = linear(x, wlog)                               # [rows, 2*heads]
-            agg = torch.empty((n, HEADS * H), dtype=torch.float32, device=x.device)
-            _lib.check(L.mignn_gat_aggregate(P(csr.row_ptr), P(csr.col), P(logits), P(x),
-                                             x.stride(0), rb, re, H, HEADS,
-                                             float(layer.negative_slope),
-                                             P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st),
-                       "mignn_gat_aggregate")
-            self._mm("w_gat", i, (layer.lin.weight,), wcat, agg, layer.bias, relu=True,
-                     residual=x[rb:re], scale=scale, shift=shift, out=out[rb:re])
+            img = self._img("w_gat", i, (layer.lin.weight,), wcat)
+            if logits is not None:
+                logits = logits.contiguous()
+            n_x = x.shape[0]
+            nb = L.mignn_gat_layer_scratch_bytes(0 if logits is not None else n_x, n, H, HEADS)
+            scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
+            _lib.check(L.mignn_gat_layer(
+                P(csr.row_ptr), P(csr.col), P(x), x.stride(0), n_x, rb, re, H, HEADS,
+                float(layer.negative_slope), P(wlog), P(logits), 2 * HEADS, P(wcat), P(img),
+                P(layer.bias), P(scale), P(shift), epi, P(scratch), nb, P(out), out.stride(0), st),
+                "mignn_gat_layer")
         elif self.layer_type == "Transformer":
             ts = (layer.lin_query.weight, layer.lin_query.bias, layer.lin_key.weight,
                   layer.lin_key.bias, layer.lin_value.weight, layer.lin_value.bias,
                   layer.lin_skip.weight, layer.lin_skip.bias)
             wqk, bqk, wout, bout = self._cached("tf", i, ts, lambda: self._tf_weights(layer))
-            K1 = HEADS * H + HEADS
-            qt = torch.empty((n, K1), dtype=torch.float32, device=x.device)
-            self._mm("w_tfq", i, ts, wqk, x[rb:re], bqk, out=qt)
-            agg = torch.empty((n, K1), dtype=torch.float32, device=x.device)
-            _lib.check(L.mignn_transformer_aggregate(
-                P(csr.row_ptr), P(csr.col), P(qt) - rb * qt.stride(0) * 4, qt.stride(0), P(x),
-                x.stride(0), rb, re, H, HEADS, 1.0 / math.sqrt(H),
-                P(agg) - rb * agg.stride(0) * 4, agg.stride(0), st), "mignn_transformer_aggregate")
-            self._mm("w_tfo", i, ts, wout, agg, bout, a2=x[rb:re], relu=True, residual=x[rb:re],
-                     scale=scale, shift=shift, out=out[rb:re])
+            # one C-ABI call (csrc/attn_layers.hip): Q~K transform, softmax
+            # aggregation, output transform over [agg | x]
+            img_q = self._img("w_tfq", i, ts, wqk)
+            img_o = self._img("w_tfo", i, ts, wout)
+            nb = L.mignn_transformer_layer_scratch_bytes(n, H, HEADS)
+            scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
+            _lib.check(L.mignn_transformer_layer(
+                P(csr.row_ptr), P(csr.col), P(x), x.stride(0), rb, re, H, HEADS,
+                1.0 / math.sqrt(H), P(wqk), P(img_q), P(bqk), P(wout), P(img_o), P(bout),
+                P(scale), P(shift), epi, P(scratch), nb, P(out), out.stride(0), st),
+                "mignn_transformer_layer")
         else:
             raise ValueError(f"Unknown layer type: {self.layer_type}")
 

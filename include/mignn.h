@@ -179,6 +179,34 @@ int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t* col, cons
                                 int64_t row_end, int h, int heads, float score_scale,
                                 float* out, int64_t ldo, void* stream);
 
+/* Whole GATConv / TransformerConv eval layers (+ residual, BN eval affine,
+ * ReLU: flags as mignn_linear) in one call each (csrc/attn_layers.hip), over
+ * rows [row_begin, row_end) of x (x holds every row the CSR references:
+ * n_x rows, own + halo).  Transforms in split-fp16 arithmetic when the
+ * weight's mignn_linear_f16x3_prep image is given, else exact fp32.
+ * GAT: wlog [2*heads, h] = per-head W^T att_src | W^T att_dst (re-associated
+ * logit weights), wcat [h, heads*h] = head-mean blocks of W; `logits`
+ * ([n_x, 2*heads], ldl = 2*heads) may be given instead of wlog (a sharded
+ * caller's exchanged logits).  Transformer: wqk [heads*h + heads, h] and bqk
+ * (q~ = Wk^T q per head and c = q . bk, see mignn_transformer_aggregate),
+ * wout [h, heads*h + heads + h] = [Wv / heads | bv / heads | W_skip], bout =
+ * b_skip.  scratch: the *_scratch_bytes sizes, 16-B aligned, device memory. */
+size_t mignn_gat_layer_scratch_bytes(int64_t n_x, int64_t rows, int h, int heads);
+int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx,
+                    int64_t n_x, int64_t row_begin, int64_t row_end, int h, int heads,
+                    float negative_slope, const float* wlog, const float* logits, int64_t ldl,
+                    const float* wcat, const void* wcat_img, const float* bias,
+                    const float* scale, const float* shift, int flags, void* scratch,
+                    size_t scratch_bytes, float* out, int64_t ldo, void* stream);
+size_t mignn_transformer_layer_scratch_bytes(int64_t rows, int h, int heads);
+int mignn_transformer_layer(const int32_t* row_ptr, const int32_t* col, const float* x,
+                            int64_t ldx, int64_t row_begin, int64_t row_end, int h, int heads,
+                            float score_scale, const float* wqk, const void* wqk_img,
+                            const float* bqk, const float* wout, const void* wout_img,
+                            const float* bout, const float* scale, const float* shift, int flags,
+                            void* scratch, size_t scratch_bytes, float* out, int64_t ldo,
+                            void* stream);
+
 /* PyG gcn_norm edge weights per CSR entry (rows [row_begin, row_end)):
  *   ew[e] = dinv[col[e]] * dinv[i]   (= dinv[src] * 1 * dinv[dst], GCNConv gnn_model.py:63) */
 int mignn_gcn_norm(const int32_t* row_ptr, const int32_t* col, const float* dinv,
