@@ -78,7 +78,9 @@ struct SCfg {
     static constexpr int F = H / 16;               // floats per lane of a row (16 lanes / row)
     static constexpr int CH = F / 4;               // 16-B chunks per lane of a row
     static constexpr int EX = H == 128 ? 4 : 6;    // out-of-tile register slots per row
-    static constexpr int UB = 2;                   // in-tile slots per LDS batch
+    static constexpr int UB = H == 128 ? 2 : 4;    // in-tile slots per LDS batch (H = 128: 4
+                                                   // spills at 3 waves / SIMD, 8 % slower;
+                                                   // H = 64: 4 is 7 % faster than 2)
     static constexpr int LTS = 12;                 // in-tile table slots per row
     static constexpr int ETS = 6;                  // out-of-tile table slots per row (even)
     static constexpr int TAB_BYTES = PROWS * (LTS + ETS) * 8;
@@ -108,7 +110,8 @@ struct SCfg {
     static constexpr int OFF_TAB = OFF_REXP + BM * 4;
     static constexpr int OFF_EPI = OFF_TAB + 2 * NPW * TAB_BYTES;   // bias | scale | shift [H]
     static constexpr int OFF_CNT = OFF_EPI + 3 * H * 4;             // cntX, cntA, cntS
-    static constexpr int OFF_STG = OFF_CNT + 16;                     // STG: [BM][ROWB]
+    static constexpr int OFF_CNT2 = OFF_CNT + 16;                    // cntP, cntD, cntR
+    static constexpr int OFF_STG = OFF_CNT2 + 16;                    // STG: [BM][ROWB]
     static constexpr int LDS_BYTES = OFF_STG + (STG ? BM * ROWB : 0);
     static constexpr int NSTG = BM * ROWB / 1024 / NCW;             // STG row stores per consumer
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -294,7 +297,12 @@ __device__ __forceinline__ void p_load_entries(PIdx& t, const int32_t* __restric
 // on the fly, all by the producers: the own rows of tile s+2 into the image
 // at the end of step s (their records gathered at its start), the
 // out-of-tile rows in registers next to their gathered records.
-template <int H, bool REC, bool STG>
+// DEC (with STG): no block barrier per step -- the hand-offs are LDS counters
+// only (cntP: producers finished a tile's A image / own-row reads; cntD: a
+// consumer's own-row DMA landed; cntR: staging tile read), so the producers'
+// table / gather phase of the next tile overlaps the consumers' epilogue.
+// UBT: in-tile entries per LDS batch of the producers' finish pass (0: SCfg::UB)
+template <int H, bool REC, bool STG, bool DEC = false, int UBT = 0>
 __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t row_begin,
@@ -303,11 +311,16 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     float* __restrict__ out, int64_t ldo, const float* __restrict__ rec,
     const float* __restrict__ coef8, unsigned long long* trace) {
     static_assert(!(REC && STG), "records mode keeps three image buffers");
+    static_assert(!DEC || STG, "counter hand-offs need the staged form");
     using C = SCfg<H, STG>;
+    constexpr int UBE = UBT ? UBT : C::UB;
     __shared__ __attribute__((aligned(16))) unsigned char lds[REC ? C::LDS_BYTES_REC : C::LDS_BYTES];
     int* const cntX = reinterpret_cast<int*>(lds + C::OFF_CNT);
     int* const cntA = cntX + 1;
     int* const cntS = cntX + 2;
+    int* const cntP = reinterpret_cast<int*>(lds + C::OFF_CNT2);
+    int* const cntD = cntP + 1;
+    int* const cntR = cntP + 2;
     _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
     _Float16* const AL = reinterpret_cast<_Float16*>(lds + C::OFF_AL);
     int* const REXP = reinterpret_cast<int*>(lds + C::OFF_REXP);
@@ -342,6 +355,9 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         cntX[0] = 0;
         cntA[0] = 0;
         cntS[0] = 0;
+        cntP[0] = 0;
+        cntD[0] = 0;
+        cntR[0] = 0;
     }
 
     // static wave priority (diagnostic schedules): consumers or producers
@@ -727,19 +743,19 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             for (int qd = 0; qd < C::NQD; ++qd) {
                 const int row = 4 * qd + gqs;
                 const int ndeg = (flags & MIGNN_DIAG_NO_LOCAL) ? 0 : info.maxdeg;
-                for (int u0 = 0; u0 < ndeg; u0 += C::UB) {
-                    uint2 pw_[C::UB];
+                for (int u0 = 0; u0 < ndeg; u0 += UBE) {
+                    uint2 pw_[UBE];
 #pragma unroll
-                    for (int uu = 0; uu < C::UB; ++uu)
+                    for (int uu = 0; uu < UBE; ++uu)
                         pw_[uu] = *reinterpret_cast<const uint2*>(LT + (row * C::LTS + u0 + uu) * 8);
-                    f32x4 v[C::UB][C::CH];
+                    f32x4 v[UBE][C::CH];
 #pragma unroll
-                    for (int uu = 0; uu < C::UB; ++uu)
+                    for (int uu = 0; uu < UBE; ++uu)
 #pragma unroll
                         for (int j = 0; j < C::CH; ++j)
                             v[uu][j] = *reinterpret_cast<const f32x4*>(lds + (pw_[uu].x ^ coff[j]));
 #pragma unroll
-                    for (int uu = 0; uu < C::UB; ++uu) {
+                    for (int uu = 0; uu < UBE; ++uu) {
                         const float w = __builtin_bit_cast(float, pw_[uu].y);
 #pragma unroll
                         for (int j = 0; j < C::CH; ++j)
@@ -821,11 +837,16 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             if (dext) issue_ext(tbb, xv);
             if (pw == 0) stamp(trace, lane_, s, 1);
             a_free = s < 0;
+            // DEC: tile s+1's own rows (DMA'd at consumer step s-1) landed
+            if constexpr (DEC) lds_wait(cntD, C::NCW * static_cast<int>(s + 1));
             const int64_t t1 = tile_of(s + 1);
             if (s + 1 < nsteps && t1 < ntiles && prod) {
                 if (ia.slow) slow_rows(t1, rpa, s);
                 else finish_tile(ta, ia, acc, s);
             }
+            // DEC: tile s+1's A image / exponents written, its own rows read
+            if constexpr (DEC)
+                if (lane_ == 0) lds_bump(cntP);
             if (pw == 0) stamp(trace, lane_, s, 3);
             if (dext) sum_ext(tbb, xv, ib, acc);
             rpa = pb.rpv;
@@ -838,7 +859,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             // chunks (a few rows per 10^5, run to run; scripts/rec_debug.py)
             if constexpr (REC)
                 if (s + 2 < nsteps) expand_tile(s + 2, own_next);
-            block_barrier<0xC07F>();   // this step's LDS writes done (lgkmcnt(0))
+            if constexpr (!DEC) block_barrier<0xC07F>();   // this step's LDS writes done (lgkmcnt(0))
         }
         return;
     }
@@ -929,6 +950,9 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         const bool mm = work && !(flags & MIGNN_DIAG_NO_MFMA);
         f32x4 acc[C::IB][C::JB];
         int pr[C::IB];
+        // DEC: the producers finished tile s (A image, exponents, own-row reads)
+        if constexpr (DEC)
+            if (s >= 0) lds_wait(cntP, C::NPW * static_cast<int>(s + 1));
         if (work) {
             // seed: (residual + bias) * 2^(p_row + q_w)
             const unsigned char* const X = lds + xbuf_of(tile) * C::X_BYTES;
@@ -998,6 +1022,9 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         if (s >= 0 && lane_ == 0) lds_bump(cntA);
         if (wave == 0) stamp(trace, lane_, s, 6);
         bool stored = false;
+        // DEC: every consumer has read the staging tile of step s-1
+        if constexpr (DEC)
+            if (mm) lds_wait(cntR, C::NCW * static_cast<int>(s));
         if (mm) {
             // epilogue: unscale, BN affine, ReLU; lane (r, g) stores 16 B of row r
             const int64_t t0 = row_begin + tile * C::BM;
@@ -1050,6 +1077,8 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                         __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + 4 * ch));
                 }
             }
+            if constexpr (DEC)
+                if (s >= 0 && lane_ == 0) lds_bump(cntR);
         }
         if constexpr (!REC)
             if (dma_late) dma = (s + C::XBUF < nsteps) && x_dma(tile_of(s + C::XBUF));
@@ -1058,7 +1087,15 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         // next step); this step's DMA (NPC) and row stores (NST), the youngest
         // vector-memory operations, may stay in flight
         constexpr int npc = C::NPC;
-        if constexpr (STG) {
+        if constexpr (DEC) {
+            // this step's DMA (tile s+2, read by the producers' next step)
+            // landed -- the row stores may fly -- then tell the producers
+            asm volatile("" ::: "memory");
+            if (stored) __builtin_amdgcn_s_waitcnt(0x70 | C::NSTG);
+            else __builtin_amdgcn_s_waitcnt(0x70);
+            asm volatile("" ::: "memory");
+            if (lane_ == 0) lds_bump(cntD);
+        } else if constexpr (STG) {
             // two image buffers: this step's DMA (tile s+2) is read by the
             // producers next step -- it must land now; the row stores may fly
             if (stored) block_barrier<0x70 | C::NSTG>();
@@ -1072,7 +1109,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     }
 }
 
-template <int H, bool REC, bool STG = false>
+template <int H, bool REC, bool STG = false, bool DEC = false, int UBT = 0>
 int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                  int64_t ldx, int64_t rb, int64_t re, const float* w, const float* bias,
                  const float* scale, const float* shift, int flags, float* out, int64_t ldo,
@@ -1091,7 +1128,7 @@ int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, co
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL((gcn_f16x3_kernel<H, REC, STG>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col,
+    hipLaunchKernelGGL((gcn_f16x3_kernel<H, REC, STG, DEC, UBT>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col,
                        ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, rec, coef8,
                        (flags & MIGNN_DIAG_TRACE) ? g_trace16_host : nullptr);
     return launch_status("gcn_f16x3_kernel");
@@ -1134,6 +1171,20 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
     MIGNN_REQUIRE(x != out, "gcn_layer_f16x3: in-place not supported (neighbours read x)");
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
+    if (flags & MIGNN_SCHED_UB4)
+        return h == 128 ? launch_f16x3<128, false, true, false, 4>(row_ptr, col, ew, x, ldx, rb, re,
+                                                                   w, bias, scale, shift, flags,
+                                                                   out, ldo, nullptr, nullptr, st)
+                        : launch_f16x3<64, false, true, false, 4>(row_ptr, col, ew, x, ldx, rb, re,
+                                                                  w, bias, scale, shift, flags,
+                                                                  out, ldo, nullptr, nullptr, st);
+    if (flags & MIGNN_SCHED_DECOUPLED)
+        return h == 128 ? launch_f16x3<128, false, true, true>(row_ptr, col, ew, x, ldx, rb, re, w,
+                                                               bias, scale, shift, flags, out, ldo,
+                                                               nullptr, nullptr, st)
+                        : launch_f16x3<64, false, true, true>(row_ptr, col, ew, x, ldx, rb, re, w,
+                                                              bias, scale, shift, flags, out, ldo,
+                                                              nullptr, nullptr, st);
     if (!(flags & MIGNN_SCHED_UNSTAGED))
         return h == 128 ? launch_f16x3<128, false, true>(row_ptr, col, ew, x, ldx, rb, re, w, bias,
                                                          scale, shift, flags, out, ldo, nullptr,

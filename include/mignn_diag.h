@@ -26,7 +26,10 @@ enum {
     MIGNN_SCHED_DMA_LATE = 524288,       /* f16x3 GCN layer: own-row DMA after the epilogue */
     MIGNN_SCHED_UNSTAGED = 1048576       /* f16x3 GCN layer: the round-1 form -- 3 image buffers,
                                             stores straight from the 16x16 accumulators (the
-                                            default stages whole output rows in LDS) */
+                                            default stages whole output rows in LDS) */,
+    MIGNN_SCHED_DECOUPLED = 2097152,     /* f16x3 GCN layer: LDS-counter hand-offs only, no
+                                            block barrier per step (staged form) */
+    MIGNN_SCHED_UB4 = 4194304            /* f16x3 GCN layer: in-tile entries 4 per LDS batch */
 };
 /* mignn_gcn_layer / mignn_gcn_layer_f16x3 / mignn_linear with the flags above */
 int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
