@@ -297,10 +297,14 @@ __device__ __forceinline__ void p_load_entries(PIdx& t, const int32_t* __restric
 // on the fly, all by the producers: the own rows of tile s+2 into the image
 // at the end of step s (their records gathered at its start), the
 // out-of-tile rows in registers next to their gathered records.
-// DEC (with STG): no block barrier per step -- the hand-offs are LDS counters
-// only (cntP: producers finished a tile's A image / own-row reads; cntD: a
-// consumer's own-row DMA landed; cntR: staging tile read), so the producers'
-// table / gather phase of the next tile overlaps the consumers' epilogue.
+// DEC (with STG; EXPERIMENTAL, diagnostic flag MIGNN_SCHED_DECOUPLED): no
+// block barrier per step -- the hand-offs are LDS counters only (cntP:
+// producers finished a tile's A image / own-row reads; cntD: a consumer's
+// own-row DMA landed; cntR: staging tile read), so the producers' table /
+// gather phase of the next tile overlaps the consumers' epilogue.  1-2 %
+// faster on the 10M locality-ordered mesh and correct there, but it gave
+// wrong rows in a 1M natural-order model test (slow-path tiles): not the
+// default until that hand-off is found.  Every wait is a bounded spin.
 // UBT: in-tile entries per LDS batch of the producers' finish pass (0: SCfg::UB)
 template <int H, bool REC, bool STG, bool DEC = false, int UBT = 0>
 __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
@@ -1171,6 +1175,13 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
     MIGNN_REQUIRE(x != out, "gcn_layer_f16x3: in-place not supported (neighbours read x)");
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
+    if (flags & MIGNN_SCHED_UB3)
+        return h == 128 ? launch_f16x3<128, false, true, false, 3>(row_ptr, col, ew, x, ldx, rb, re,
+                                                                   w, bias, scale, shift, flags,
+                                                                   out, ldo, nullptr, nullptr, st)
+                        : launch_f16x3<64, false, true, false, 3>(row_ptr, col, ew, x, ldx, rb, re,
+                                                                  w, bias, scale, shift, flags,
+                                                                  out, ldo, nullptr, nullptr, st);
     if (flags & MIGNN_SCHED_UB4)
         return h == 128 ? launch_f16x3<128, false, true, false, 4>(row_ptr, col, ew, x, ldx, rb, re,
                                                                    w, bias, scale, shift, flags,
@@ -1178,7 +1189,7 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
                         : launch_f16x3<64, false, true, false, 4>(row_ptr, col, ew, x, ldx, rb, re,
                                                                   w, bias, scale, shift, flags,
                                                                   out, ldo, nullptr, nullptr, st);
-    if (flags & MIGNN_SCHED_DECOUPLED)
+    if ((flags & MIGNN_SCHED_DECOUPLED) && !(flags & MIGNN_SCHED_UNSTAGED))
         return h == 128 ? launch_f16x3<128, false, true, true>(row_ptr, col, ew, x, ldx, rb, re, w,
                                                                bias, scale, shift, flags, out, ldo,
                                                                nullptr, nullptr, st)

@@ -27,9 +27,10 @@ enum {
     MIGNN_SCHED_UNSTAGED = 1048576       /* f16x3 GCN layer: the round-1 form -- 3 image buffers,
                                             stores straight from the 16x16 accumulators (the
                                             default stages whole output rows in LDS) */,
-    MIGNN_SCHED_DECOUPLED = 2097152,     /* f16x3 GCN layer: LDS-counter hand-offs only, no
-                                            block barrier per step (staged form) */
-    MIGNN_SCHED_UB4 = 4194304            /* f16x3 GCN layer: in-tile entries 4 per LDS batch */
+    MIGNN_SCHED_DECOUPLED = 2097152,     /* f16x3 GCN layer, EXPERIMENTAL: LDS-counter hand-offs
+                                            only, no block barrier per step (see gcn_f16x3.hip) */
+    MIGNN_SCHED_UB4 = 4194304,           /* f16x3 GCN layer: in-tile entries 4 per LDS batch */
+    MIGNN_SCHED_UB3 = 8388608            /* f16x3 GCN layer: in-tile entries 3 per LDS batch */
 };
 /* mignn_gcn_layer / mignn_gcn_layer_f16x3 / mignn_linear with the flags above */
 int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,

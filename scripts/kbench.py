@@ -181,7 +181,7 @@ def diag(mode_blocks):
 
 cases = {
     "ring": (ring, 15), "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_interleaved": (gcn16, 15 | 65536), "gcn16_prio_cons": (gcn16, 15 | 131072), "gcn16_prio_prod": (gcn16, 15 | 262144), "gcn16_dma_late": (gcn16, 15 | 524288),
-    "gcn16_dma_late_plain": (gcn16, 15 | 524288 | 32768), "gcn16_unstaged": (gcn16, 15 | 1048576), "gcn16_dec": (gcn16, 15 | 2097152), "gcn16_ub4": (gcn16, 15 | 4194304), "gcn16_no_produce": (gcn16, 15 | 256),
+    "gcn16_dma_late_plain": (gcn16, 15 | 524288 | 32768), "gcn16_unstaged": (gcn16, 15 | 1048576), "gcn16_dec": (gcn16, 15 | 2097152), "gcn16_ub4": (gcn16, 15 | 4194304), "gcn16_ub3": (gcn16, 15 | 8388608), "gcn16_no_produce": (gcn16, 15 | 256),
     "gcn16_no_mfma": (gcn16, 15 | 512), "gcn16_no_ext": (gcn16, 15 | 4096),
     "gcn16_no_tables_ext": (gcn16, 15 | 4096 | 16384),
     "gcn16_plain": (gcn16, 15 | 32768), "gcn16_no_produce_plain": (gcn16, 15 | 256 | 32768),
