@@ -175,3 +175,41 @@ def test_transformer_reassociation_algebra():
     A = torch.cat([agg.reshape(n, -1), sig, x], 1)
     got = A @ wout.T + bout
     assert (got - ref).abs().max().item() < 1e-5
+
+
+def test_attention_layer_entry_points_validate_before_launching():
+    """mignn_gat_layer / mignn_transformer_layer (csrc/attn_layers.hip) reject
+    bad arguments with MIGNN_ERR_ARG and a message before any device work, and
+    report their scratch sizes (host-only paths: no GPU needed)."""
+    L = _lib.lib()
+    buf = (ctypes.c_float * 4096)()
+    p = ctypes.addressof(buf)          # never dereferenced: validation fails first
+    al = (p + 255) & ~255
+    # scratch sizes: [n_x, 2 heads] logits + [rows, heads h] aggregate, 256-B aligned
+    assert L.mignn_gat_layer_scratch_bytes(10, 4, 8, 4) == 512 + 512
+    assert L.mignn_gat_layer_scratch_bytes(0, 4, 8, 4) == 512
+    assert L.mignn_gat_layer_scratch_bytes(-1, 4, 8, 4) == 0
+    # q~ and aggregate [rows, heads h + heads] each
+    assert L.mignn_transformer_layer_scratch_bytes(4, 8, 4) == 2 * 768
+    assert L.mignn_transformer_layer_scratch_bytes(4, 0, 4) == 0
+
+    def gat(flags=0, x=p, rb=0, re=4, scratch=al, nbytes=1024):
+        return L.mignn_gat_layer(p, p, x, 8, 10, rb, re, 8, 4, 0.2, p, None, 8, p, None, None,
+                                 None, None, flags, scratch, nbytes, p, 8, None)
+
+    assert gat(rb=0, re=0) == 0                     # empty range: nothing to do
+    for kw, msg in [({"flags": 1 << 30}, "unknown flags"), ({"x": None}, "null pointer"),
+                    ({"rb": 5, "re": 4}, "bad row range"), ({"re": 11}, "bad row range"),
+                    ({"nbytes": 1023}, "scratch"), ({"scratch": al + 4}, "scratch")]:
+        assert gat(**kw) == 1, kw
+        assert msg in _lib.last_error(), (kw, _lib.last_error())
+
+    def tf(flags=0, bqk=p, rb=0, re=4, nbytes=1536):
+        return L.mignn_transformer_layer(p, p, p, 8, rb, re, 8, 4, 0.35, p, None, bqk, p, None,
+                                         p, None, None, flags, al, nbytes, p, 8, None)
+
+    assert tf(re=0) == 0
+    for kw, msg in [({"flags": 1 << 30}, "unknown flags"), ({"bqk": None}, "null pointer"),
+                    ({"rb": 3, "re": 2}, "bad row range"), ({"nbytes": 1535}, "scratch")]:
+        assert tf(**kw) == 1, kw
+        assert msg in _lib.last_error(), (kw, _lib.last_error())
