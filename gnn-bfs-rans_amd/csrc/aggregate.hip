@@ -190,7 +190,8 @@ template <int LPR, int CPL, int HEADS>
 __global__ __launch_bounds__(256) void transformer_aggregate_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ qt, int64_t ldq, const float* __restrict__ x, int64_t ldx,
-    int64_t row_begin, int64_t row_end, int h, float scale, float* __restrict__ out, int64_t ldo) {
+    int64_t row_begin, int64_t row_end, int h, float scale, float* __restrict__ out, int64_t ldo,
+    bool use_cq) {
     const int h4 = h >> 2;
     RowCursor rc = row_of<LPR>(row_begin);
     const int64_t stride = row_stride<LPR>();
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(256) void transformer_aggregate_kernel(
         float4 acc[HEADS][CPL];
 #pragma unroll
         for (int hd = 0; hd < HEADS; ++hd) {
-            cq[hd] = qt[row * ldq + HEADS * h + hd];
+            cq[hd] = use_cq ? qt[row * ldq + HEADS * h + hd] : 0.f;
             m[hd] = -INFINITY;
             l[hd] = 0.f;
 #pragma unroll
@@ -540,7 +541,7 @@ template <int LPR>
 __global__ __launch_bounds__(256) void tf_rows_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ qt, int64_t ldq, const float* __restrict__ x, int64_t ldx,
-    int64_t rb, int64_t re, int h, float scale, float* __restrict__ out, int64_t ldo) {
+    int64_t rb, int64_t re, int h, float scale, float* __restrict__ out, int64_t ldo, bool use_cq) {
     constexpr int HEADS = 4, RPW = 64 / LPR, NV = LPR == 16 ? 2 : 1;
     // per row group: P[32] | C[4] (rescale) | I[4] (1 / (l + eps))
     __shared__ __attribute__((aligned(16))) float s_w[4][RPW][40];
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(256) void tf_rows_kernel(
             q[hd] = ld4(qt + row * ldq + hd * h + 4 * c);
             acc[hd] = zero;
         }
-        const float cq = qt[row * ldq + HEADS * h + my_hd];
+        const float cq = use_cq ? qt[row * ldq + HEADS * h + my_hd] : 0.f;
         float m = -INFINITY, l = 0.f;      // this lane's head, reduced layout
         for (int e0 = beg; e0 < end; e0 += kB) {
             int j[kB];
@@ -795,13 +796,18 @@ extern "C" int mignn_gat_aggregate(const int32_t* row_ptr, const int32_t* col,
     return launch_status("gat_aggregate");
 }
 
-extern "C" int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t* col,
-                                           const float* qt, int64_t ldq, const float* x,
-                                           int64_t ldx, int64_t rb, int64_t re, int h, int heads,
-                                           float score_scale, float* out, int64_t ldo,
-                                           void* stream) {
+namespace mignn {
+// use_cq = false: the per-head score constant c_i = q_i . b_k is left out
+// (qt's last `heads` columns are not read): it shifts every score of a row's
+// head by the same amount, which the softmax cancels -- the layer entry
+// (attn_layers.hip) does not compute it
+int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const float* qt,
+                               int64_t ldq, const float* x, int64_t ldx, int64_t rb, int64_t re,
+                               int h, int heads, float score_scale, float* out, int64_t ldo,
+                               bool use_cq, void* stream) {
     if (int rc = check_common(row_ptr, col, x, ldx, rb, re, h, out, ldo)) return rc;
-    MIGNN_REQUIRE(qt && aligned16(qt) && ldq % 4 == 0 && ldq >= (int64_t)heads * h + heads,
+    MIGNN_REQUIRE(qt && aligned16(qt) && ldq % 4 == 0 &&
+                      ldq >= (int64_t)heads * h + (use_cq ? heads : 0),
                   "transformer_aggregate: bad qt");
     MIGNN_REQUIRE(ldo >= (int64_t)heads * h + heads, "transformer_aggregate: ldo too small");
     if (re == rb) return MIGNN_OK;
@@ -810,13 +816,23 @@ extern "C" int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t
     // batched: 4 heads, h = 4 LPR (LPR in 16..64)
     if (!g_agg_legacy && heads == 4 && (h == 64 || h == 128 || h == 256)) {
         switch (h) {
-            case 64: tf_rows_kernel<16><<<dim3(batched_grid(re - rb, 16)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo); break;
-            case 128: tf_rows_kernel<32><<<dim3(batched_grid(re - rb, 32)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo); break;
-            default: tf_rows_kernel<64><<<dim3(batched_grid(re - rb, 64)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo); break;
+            case 64: tf_rows_kernel<16><<<dim3(batched_grid(re - rb, 16)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
+            case 128: tf_rows_kernel<32><<<dim3(batched_grid(re - rb, 32)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
+            default: tf_rows_kernel<64><<<dim3(batched_grid(re - rb, 64)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
         }
         return launch_status("transformer_aggregate");
     }
     MIGNN_DISPATCH_HEADS(heads, MIGNN_DISPATCH_LPR(h4, (transformer_aggregate_kernel<LPR, CPL, HEADS><<<dim3(agg_grid(re - rb, LPR)), dim3(256), 0, st>>>( row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale,
-        out, ldo))));
+        out, ldo, use_cq))));
     return launch_status("transformer_aggregate");
+}
+}  // namespace mignn
+
+extern "C" int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t* col,
+                                           const float* qt, int64_t ldq, const float* x,
+                                           int64_t ldx, int64_t rb, int64_t re, int h, int heads,
+                                           float score_scale, float* out, int64_t ldo,
+                                           void* stream) {
+    return transformer_aggregate_rows(row_ptr, col, qt, ldq, x, ldx, rb, re, h, heads, score_scale,
+                                      out, ldo, true, stream);
 }

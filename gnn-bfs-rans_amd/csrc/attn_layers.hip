@@ -7,16 +7,20 @@
 //                                                       skipped if the caller gives them)
 //                 agg    = softmax-weighted sums        (mignn_gat_aggregate, [rows, heads h])
 //                 out    = relu(BN(x + agg . wcat^T + b))
-//   Transformer:  qt     = x . wqk^T + bqk               ([rows, heads h + heads])
+//   Transformer:  qt     = x . wqk^T + bqk               ([rows, heads h])
 //                 agg    = softmax-weighted sums | alpha sums (mignn_transformer_aggregate)
 //                 out    = relu(BN(x + [agg | x] . wout^T + bout))
 //
 // The transforms run in split-fp16 MFMA arithmetic when the caller passes the
 // weight's image (mignn_linear_f16x3_prep), else in exact fp32
 // (mignn_linear).  The re-associated weights (wlog = W_k^T att per head, wcat
-// = head-mean blocks of W; wqk = [W_k^T W_q per head | W_q^T b_k], wout =
+// = head-mean blocks of W; wqk = W_k^T W_q per head, bqk = W_k^T b_q, wout =
 // [W_v / heads | b_v / heads | W_skip]) are built by the host layer once per
-// weight version (mignn/gnn_model.py _gat_weights / _tf_weights).
+// weight version (mignn/gnn_model.py _gat_weights / _tf_weights).  The score's
+// per-head constant q_i . b_k (mignn_transformer_aggregate's c) is not formed:
+// it shifts every score of a row's head alike and the softmax cancels it, so
+// the Q~K transform is heads*h columns wide (four whole 256-column GEMM tiles
+// at h = 256 instead of four and a 4-column fifth).
 #include "common.hpp"
 
 namespace {
@@ -110,18 +114,19 @@ extern "C" int mignn_transformer_layer(const int32_t* row_ptr, const int32_t* co
     const size_t need = mignn_transformer_layer_scratch_bytes(rows, h, heads);
     MIGNN_REQUIRE(scratch && aligned16(scratch) && scratch_bytes >= need,
                   "transformer_layer: scratch %zu < required %zu", scratch_bytes, need);
-    const int k1 = heads * h + heads;
+    const int k1 = heads * h + heads;   // agg: [heads h sums | heads alpha sums]
     // rows of qt / agg padded to 16 B (the aggregation loads qt rows as float4)
     const int64_t ldq = (k1 + 3) / 4 * 4;
     MIGNN_REQUIRE(static_cast<size_t>(rows) * ldq * 4 <= need / 2, "transformer_layer: layout");
     float* qt = static_cast<float*>(scratch);
     float* agg = reinterpret_cast<float*>(static_cast<char*>(scratch) + need / 2);
-    if (int rc = transform(x + row_begin * ldx, ldx, rows, h, nullptr, 0, 0, wqk, wqk_img, k1, bqk,
-                           nullptr, 0, nullptr, nullptr, MIGNN_EPI_BIAS, qt, ldq, stream))
+    if (int rc = transform(x + row_begin * ldx, ldx, rows, h, nullptr, 0, 0, wqk, wqk_img,
+                           heads * h, bqk, nullptr, 0, nullptr, nullptr, MIGNN_EPI_BIAS, qt, ldq,
+                           stream))
         return rc;
-    if (int rc = mignn_transformer_aggregate(row_ptr, col, qt - row_begin * ldq, ldq, x, ldx,
-                                             row_begin, row_end, h, heads, score_scale,
-                                             agg - row_begin * ldq, ldq, stream))
+    if (int rc = transformer_aggregate_rows(row_ptr, col, qt - row_begin * ldq, ldq, x, ldx,
+                                            row_begin, row_end, h, heads, score_scale,
+                                            agg - row_begin * ldq, ldq, false, stream))
         return rc;
     // [agg | x] . wout^T + bout, residual x, BN, ReLU (flags)
     return transform(agg, ldq, rows, k1, x + row_begin * ldx, ldx, h, wout, wout_img, h, bout,

@@ -148,6 +148,12 @@ __device__ __forceinline__ float epilogue(float acc, int flags, float bias, floa
 
 // Register-resident-W persistent row-tile GEMM (tile_gemm.hip) for the
 // FlowGNN layer / head shapes; *handled=false when (k, n) has no instance.
+// mignn_transformer_aggregate with the per-head score constant optional
+// (aggregate.hip; use_cq = false: qt's last `heads` columns are not read)
+int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const float* qt,
+                               int64_t ldq, const float* x, int64_t ldx, int64_t rb, int64_t re,
+                               int h, int heads, float score_scale, float* out, int64_t ldo,
+                               bool use_cq, void* stream);
 int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, int n,
                 const float* bias, const float* residual, int64_t ldr, const float* scale,
                 const float* shift, int flags, float* c, int64_t ldc, hipStream_t st,

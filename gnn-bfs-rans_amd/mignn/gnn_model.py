@@ -824,12 +824,12 @@ class FlowGNN(nn.Module):
         bk = d(layer.lin_key.bias).view(heads, C)
         bv = d(layer.lin_value.bias).view(heads, C)
         Hin = Wq.shape[2]
+        # score_ij = q_i . k_j = (Wk^T q_i) . x_j + q_i . bk; the second term is
+        # the same for every j of row i (per head) and cancels in the softmax
         M = torch.einsum("hck,hcq->hkq", Wk, Wq).reshape(heads * Hin, Hin)   # rows h*H+kk
         mb = torch.einsum("hck,hc->hk", Wk, bq).reshape(heads * Hin)
-        wc = torch.einsum("hcq,hc->hq", Wq, bk)                               # [h, H]
-        cc = (bq * bk).sum(1)                                                 # [h]
-        wqk = torch.cat([M, wc], 0).float().contiguous()                      # [h*H + h, H]
-        bqk = torch.cat([mb, cc], 0).float().contiguous()
+        wqk = M.float().contiguous()                                          # [h*H, H]
+        bqk = mb.float().contiguous()
         wv = Wv.permute(1, 0, 2).reshape(C, heads * Hin) / heads             # [C, h*H]
         wbv = bv.t() / heads                                                  # [C, h]
         wout = torch.cat([wv, wbv, d(layer.lin_skip.weight)], 1).float().contiguous()

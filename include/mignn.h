@@ -187,8 +187,9 @@ int mignn_transformer_aggregate(const int32_t* row_ptr, const int32_t* col, cons
  * GAT: wlog [2*heads, h] = per-head W^T att_src | W^T att_dst (re-associated
  * logit weights), wcat [h, heads*h] = head-mean blocks of W; `logits`
  * ([n_x, 2*heads], ldl = 2*heads) may be given instead of wlog (a sharded
- * caller's exchanged logits).  Transformer: wqk [heads*h + heads, h] and bqk
- * (q~ = Wk^T q per head and c = q . bk, see mignn_transformer_aggregate),
+ * caller's exchanged logits).  Transformer: wqk [heads*h, h] = Wk^T Wq per
+ * head and bqk [heads*h] = Wk^T bq per head (q~ of mignn_transformer_aggregate;
+ * its per-head constant c = q . bk is left out: the softmax cancels it),
  * wout [h, heads*h + heads + h] = [Wv / heads | bv / heads | W_skip], bout =
  * b_skip.  scratch: the *_scratch_bytes sizes, 16-B aligned, device memory. */
 size_t mignn_gat_layer_scratch_bytes(int64_t n_x, int64_t rows, int h, int heads);

@@ -164,11 +164,12 @@ def test_transformer_reassociation_algebra():
                                d(layer.lin_skip.weight), d(layer.lin_skip.bias), HEADS)
     wqk, bqk, wout, bout = (t.double() for t in FlowGNN._tf_weights(layer))
     n = x.shape[0]
-    qt = x @ wqk.T + bqk                                  # [N, heads*H + heads]
+    qt = x @ wqk.T + bqk                                  # [N, heads*H]
+    assert qt.shape[1] == HEADS * H
     src, dst = ei[0], ei[1]
-    q = qt[:, :HEADS * H].view(n, HEADS, H)
-    c = qt[:, HEADS * H:]
-    s = ((q[dst] * x[src].unsqueeze(1)).sum(-1) + c[dst]) / math.sqrt(H)
+    q = qt.view(n, HEADS, H)
+    # no q_i . b_k term: constant over a row's entries, cancelled by the softmax
+    s = (q[dst] * x[src].unsqueeze(1)).sum(-1) / math.sqrt(H)
     a = orc.segment_softmax(s, dst, n)
     agg = torch.zeros(n, HEADS, H, dtype=torch.float64).index_add_(0, dst, a.unsqueeze(-1) * x[src].unsqueeze(1))
     sig = torch.zeros(n, HEADS, dtype=torch.float64).index_add_(0, dst, a)
