@@ -289,20 +289,32 @@ __device__ __forceinline__ XcdRows<LPR> xcd_rows(int64_t rb, int64_t re) {
     const int64_t n = re - rb;
     const int xcd = blockIdx.x & 7;
     const int64_t wpb = blockDim.x >> 6;
-    const int64_t wi = static_cast<int64_t>(blockIdx.x >> 3) * wpb + (threadIdx.x >> 6);
+    // the wave index, made visibly wave-uniform: at LPR = 64 (one row per
+    // wave) the row, its row_ptr pair, column indices and gather bases are
+    // then scalar -- s_load through the constant cache instead of one vector
+    // load per index (half the vector-memory instructions of a 1-KB-row sum)
+    const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int64_t wi = static_cast<int64_t>(blockIdx.x >> 3) * wpb + wv;
     const int64_t r0 = rb + n * xcd / 8, r1 = rb + n * (xcd + 1) / 8;
     return {r0 + wi * RPW + (threadIdx.x & 63) / LPR, static_cast<int64_t>(gridDim.x >> 3) * wpb * RPW,
             r1};
 }
 
 // blocks of 256 threads for `rows` rows at RPW rows per wave: a multiple of 8
-// (one share per XCD), at most 2048 (8 per CU)
-inline unsigned batched_grid(int64_t rows, int lpr) {
+// (one share per XCD), at most `cap`.  The cap sets how many rows an XCD has
+// in flight, i.e. how far its waves spread over the row order -- the L2
+// working set of the neighbour gathers.  Measured in the locality order
+// (scripts/agg_bench.py AGG_LOCAL=1, profiles/r02_agg_grid.json): the 1-KB-row
+// sum is fastest at 1024 blocks (4 per CU: 9.9 vs 11.4 ms at 8 per CU), the
+// TransformerConv aggregation at h = 256 at 512 (2 per CU: 20.0 vs 24.6 ms;
+// at h = 128, 1M rows, the default 2048 stays 7 % faster).
+inline unsigned batched_grid(int64_t rows, int lpr, int cap = 2048) {
     const int64_t waves = (rows + 64 / lpr - 1) / (64 / lpr);
     int64_t g = (waves + 3) / 4;
     g = (g + 7) / 8 * 8;
-    return static_cast<unsigned>(g < 2048 ? (g < 8 ? 8 : g) : 2048);
+    return static_cast<unsigned>(g < cap ? (g < 8 ? 8 : g) : cap);
 }
+constexpr int kSumGrid = 1024, kTfGrid = 512;
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
@@ -436,7 +448,7 @@ __global__ __launch_bounds__(256) void sum_rows_kernel(
                 v.z = v.z + self_scale * xi.z;
                 v.w = v.w + self_scale * xi.w;
             }
-            st4(out + row * ldo + 4 * ch, v);
+            st4_nt(out + row * ldo + 4 * ch, v);
         }
     }
 }
@@ -527,7 +539,7 @@ __global__ __launch_bounds__(256) void gat_rows_kernel(
             }
         }
 #pragma unroll
-        for (int hd = 0; hd < HEADS; ++hd) st4(out + row * ldo + hd * h + 4 * c, acc[hd]);
+        for (int hd = 0; hd < HEADS; ++hd) st4_nt(out + row * ldo + hd * h + 4 * c, acc[hd]);
     }
 }
 
@@ -628,7 +640,7 @@ __global__ __launch_bounds__(256) void tf_rows_kernel(
         const float inv = 1.f / (l + kSoftmaxEps);
         if (head_lead) {
             SW[36 + my_hd] = inv;
-            out[row * ldo + HEADS * h + my_hd] = l * inv;   // sum_j alpha
+            __builtin_nontemporal_store(l * inv, &out[row * ldo + HEADS * h + my_hd]);   // sum_j alpha
         }
         const float4 iv = *reinterpret_cast<const float4*>(SW + 36);
         const float ivs[4] = {iv.x, iv.y, iv.z, iv.w};
@@ -636,7 +648,7 @@ __global__ __launch_bounds__(256) void tf_rows_kernel(
         for (int hd = 0; hd < HEADS; ++hd) {
             float4 a = acc[hd];
             a.x *= ivs[hd]; a.y *= ivs[hd]; a.z *= ivs[hd]; a.w *= ivs[hd];
-            st4(out + row * ldo + hd * h + 4 * c, a);
+            st4_nt(out + row * ldo + hd * h + 4 * c, a);
         }
     }
 }
@@ -750,7 +762,7 @@ extern "C" int mignn_gcn_aggregate(const int32_t* row_ptr, const int32_t* col, c
         MIGNN_DISPATCH_LPR(h4, (weighted_sum_kernel<LPR, CPL, true><<<dim3(agg_grid(re - rb, LPR)), dim3(256), 0, as_stream(stream)>>>( row_ptr, col, dinv, x, ldx, 1.f,
                                                    rb, re, h4, out, ldo)));
     } else {
-        MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, true><<<dim3(batched_grid(re - rb, LPR)), dim3(256), 0, as_stream(stream)>>>(
+        MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, true><<<dim3(batched_grid(re - rb, LPR, kSumGrid)), dim3(256), 0, as_stream(stream)>>>(
                                    row_ptr, col, dinv, x, ldx, 1.f, rb, re, h4, out, ldo)));
     }
     return launch_status("gcn_aggregate");
@@ -766,7 +778,7 @@ extern "C" int mignn_sum_aggregate(const int32_t* row_ptr, const int32_t* col, c
         MIGNN_DISPATCH_LPR(h4, (weighted_sum_kernel<LPR, CPL, false><<<dim3(agg_grid(re - rb, LPR)), dim3(256), 0, as_stream(stream)>>>( row_ptr, col, nullptr, x, ldx,
                                                    self_scale, rb, re, h4, out, ldo)));
     } else {
-        MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, false><<<dim3(batched_grid(re - rb, LPR)), dim3(256), 0, as_stream(stream)>>>(
+        MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, false><<<dim3(batched_grid(re - rb, LPR, kSumGrid)), dim3(256), 0, as_stream(stream)>>>(
                                    row_ptr, col, nullptr, x, ldx, self_scale, rb, re, h4, out, ldo)));
     }
     return launch_status("sum_aggregate");
@@ -818,7 +830,7 @@ int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const
         switch (h) {
             case 64: tf_rows_kernel<16><<<dim3(batched_grid(re - rb, 16)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
             case 128: tf_rows_kernel<32><<<dim3(batched_grid(re - rb, 32)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
-            default: tf_rows_kernel<64><<<dim3(batched_grid(re - rb, 64)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
+            default: tf_rows_kernel<64><<<dim3(batched_grid(re - rb, 64, kTfGrid)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
         }
         return launch_status("transformer_aggregate");
     }

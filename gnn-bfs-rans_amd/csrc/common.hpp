@@ -63,6 +63,12 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+// streaming store (non-temporal): the written rows do not displace gathered
+// rows from L2
+__device__ __forceinline__ void st4_nt(float* p, float4 v) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f*>(p));
+}
 
 // Raw buffer loads through a hand-built 128-bit descriptor (the clang
 // __builtin_amdgcn_raw_buffer_load_b64 of this toolchain lowers to a 4-byte

@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(HERE, "gnn-bfs-rans_amd"))
 import torch  # noqa: E402
 
 from mignn import _lib  # noqa: E402
-from mignn.gnn_model import build_csr  # noqa: E402
+from mignn.gnn_model import build_csr, locality_order  # noqa: E402
 from mignn.synthetic import grid_graph  # noqa: E402
 
 dev = torch.device("cuda", 0)
@@ -19,7 +19,7 @@ L, P = _lib.lib(), _lib.ptr
 res = {}
 
 
-def timeit(fn, reps=5):
+def timeit(fn, reps=int(os.environ.get("AGG_REPS", "5"))):
     fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -43,15 +43,22 @@ def ab(name, fn, nbytes):
     print(name, out, file=sys.stderr, flush=True)
 
 
-for name, dims, h, kind in [("transformer_h256_10M", (250, 200, 200), 256, "tf"),
-                            ("gin_sum_h256_12.6M", (500, 400, 63), 256, "sum"),
-                            ("gat_h128_1M", (100, 100, 100), 128, "gat"),
-                            ("transformer_h128_1M", (100, 100, 100), 128, "tf")]:
+CASES = [("transformer_h256_10M", (250, 200, 200), 256, "tf"),
+         ("gin_sum_h256_12.6M", (500, 400, 63), 256, "sum"),
+         ("gat_h128_1M", (100, 100, 100), 128, "gat"),
+         ("transformer_h128_1M", (100, 100, 100), 128, "tf")]
+# AGG_LOCAL=1: the 10M-class cases again in the engine's locality order (the
+# order the model runs them in)
+if os.environ.get("AGG_LOCAL"):
+    CASES = [(n + "_local", d, h, k) for n, d, h, k in CASES[:2]]
+for name, dims, h, kind in CASES:
     x0, ei = grid_graph(*dims, device=dev)
     n = x0.shape[0]
     E = ei.shape[1]
     mode = _lib.CSR_ONE_SELF_LOOP if kind == "gat" else _lib.CSR_VERBATIM
-    csr = build_csr(ei, n, mode)
+    inv = locality_order(x0, ei)[1] if name.endswith("_local") else None
+    csr = build_csr(ei, n, mode, relabel=inv)
+    del inv
     del ei
     nnz = E + (n if kind == "gat" else 0)
     g = torch.Generator(device=dev).manual_seed(0)
