@@ -11,6 +11,9 @@ sys.path.insert(0, os.path.join(HERE, "gnn-bfs-rans_amd"))
 import torch  # noqa: E402
 
 from mignn import _lib  # noqa: E402
+
+if os.environ.get("AGG_LIB"):       # an alternative build of the library (experiments)
+    _lib.LIB_PATH = os.path.abspath(os.environ["AGG_LIB"])
 from mignn.gnn_model import build_csr, locality_order  # noqa: E402
 from mignn.synthetic import grid_graph  # noqa: E402
 
