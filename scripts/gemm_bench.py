@@ -19,7 +19,7 @@ M = int(os.environ.get("GB_M", 2_000_000))
 SHAPES = [  # (name, k1, k2, n, residual)
     ("gin_nn0 256->256", 256, 0, 256, False),
     ("gin_nn2 256->256 +res", 256, 0, 256, True),
-    ("tf_qt 256->1028", 256, 0, 1028, False),
+    ("tf_qt 256->1024", 256, 0, 1024, False),
     ("tf_out [1028|256]->256 +res", 1028, 256, 256, True),
     ("gat_out 1024->256 +res", 1024, 0, 256, True),
 ]
