@@ -206,7 +206,12 @@ __global__ __launch_bounds__(GNT, RPW == 1 ? 2 : 1) void gemm_f16x3_kernel(
         unsigned char* dst = lds + (kc & 1) * CHUNK_BYTES;
 #pragma unroll
         for (int pc = 0; pc < CHUNK_BYTES / 1024 / GW; ++pc) {
-            const int piece = wave + pc * GW;
+            const int piece = wave + pc * GW;   // fragment (column block piece / 2, hi | lo)
+            // column blocks past N (zero padding of a narrow tile, e.g. GAT's
+            // N = 128 head-mean GEMM): not copied, their MFMAs are skipped.
+            // (Uniform per wave; fewer DMA pieces only make the counted
+            // vmcnt waits below more conservative.)
+            if ((piece >> 1) >= ncb) continue;
             glds16_g(src + piece * 1024 + lane * 16, lds_addr_g(dst + piece * 1024));
         }
     };
@@ -324,6 +329,7 @@ __global__ __launch_bounds__(GNT, RPW == 1 ? 2 : 1) void gemm_f16x3_kernel(
         const int64_t rbase = tm * GBM + 16 * wave;         // first row of this wave
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
+            if (8 * hf >= ncb) break;          // a half tile past N: nothing to store
 #pragma unroll
             for (int c8 = 0; c8 < 8; ++c8) {
                 const int cb = 8 * hf + c8;

@@ -22,6 +22,7 @@ SHAPES = [  # (name, k1, k2, n, residual)
     ("tf_qt 256->1024", 256, 0, 1024, False),
     ("tf_out [1028|256]->256 +res", 1028, 256, 256, True),
     ("gat_out 1024->256 +res", 1024, 0, 256, True),
+    ("gat_out 512->128 +res", 512, 0, 128, True),
 ]
 
 
