@@ -23,55 +23,9 @@
 // at h = 256 instead of four and a 4-column fifth).
 #include "common.hpp"
 
-#include <algorithm>
-
 namespace {
 
-using mignn::f32x4;
-using mignn::as_stream;
-using mignn::launch_status;
-using mignn::aligned16;
-
 inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
-
-// GAT logits [n, 8] = x [n, h] . wlog^T (4 heads: src | dst) in exact fp32:
-// a row group of LPR = h / 4 lanes holds one row (a float4 per lane) and the
-// lanes' float4 slices of the 8 logit weights (registers), 8 partial dots
-// reduced over the group by xor-shuffles.  A pure stream over x (the generic
-// fp32 MFMA GEMM wastes its 16-column tiles on N = 8: 0.23 ms at 1M x 128).
-template <int LPR>
-__global__ __launch_bounds__(256) void gat_logits8_kernel(const float* __restrict__ x, int64_t ldx,
-                                                          int64_t n, const float* __restrict__ w,
-                                                          int h, float* __restrict__ out) {
-    constexpr int RPW = 64 / LPR;
-    const int lane = static_cast<int>(threadIdx.x & 63);
-    const int c = lane % LPR, grp = lane / LPR;
-    f32x4 wv[8];
-#pragma unroll
-    for (int o = 0; o < 8; ++o) wv[o] = *reinterpret_cast<const f32x4*>(w + o * h + 4 * c);
-    const int64_t wave = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * 4 * RPW;
-    for (int64_t row = wave * RPW + grp; row < n; row += stride) {
-        const f32x4 xv = *reinterpret_cast<const f32x4*>(x + row * ldx + 4 * c);
-        float v[8];
-#pragma unroll
-        for (int o = 0; o < 8; ++o) {
-            float d = xv[0] * wv[o][0];
-            d = fmaf(xv[1], wv[o][1], d);
-            d = fmaf(xv[2], wv[o][2], d);
-            d = fmaf(xv[3], wv[o][3], d);
-            v[o] = d;
-        }
-#pragma unroll
-        for (int off = LPR / 2; off > 0; off >>= 1)
-#pragma unroll
-            for (int o = 0; o < 8; ++o) v[o] += __shfl_xor(v[o], off);
-        if (c == 0) {
-            *reinterpret_cast<f32x4*>(out + row * 8) = f32x4{v[0], v[1], v[2], v[3]};
-            *reinterpret_cast<f32x4*>(out + row * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        }
-    }
-}
 
 // the transform of either arithmetic: img != NULL -> split fp16, else fp32 w
 int transform(const float* a, int64_t lda, int64_t m, int k1, const float* a2, int64_t lda2,
@@ -119,22 +73,9 @@ extern "C" int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const
     if (lg == nullptr) {   // logits of every row the CSR references
         float* l = reinterpret_cast<float*>(base);
         base += align256(static_cast<size_t>(n_x) * 2 * heads * 4);
-        const bool vec = heads == 4 && (h == 64 || h == 128 || h == 256) && ldx % 4 == 0 &&
-                         aligned16(x) && aligned16(wlog);
-        if (vec && n_x > 0) {
-            const int64_t waves = (n_x * (h / 4) + 63) / 64;
-            const unsigned grid = static_cast<unsigned>(std::min<int64_t>((waves + 3) / 4, 4096));
-            hipStream_t st = as_stream(stream);
-            switch (h) {
-                case 64: gat_logits8_kernel<16><<<grid, 256, 0, st>>>(x, ldx, n_x, wlog, h, l); break;
-                case 128: gat_logits8_kernel<32><<<grid, 256, 0, st>>>(x, ldx, n_x, wlog, h, l); break;
-                default: gat_logits8_kernel<64><<<grid, 256, 0, st>>>(x, ldx, n_x, wlog, h, l); break;
-            }
-            if (int rc = launch_status("gat_logits8_kernel")) return rc;
-        } else if (int rc = mignn_linear(x, ldx, n_x, h, nullptr, 0, 0, wlog, 2 * heads, nullptr,
-                                         nullptr, 0, nullptr, nullptr, 0, l, 2 * heads, stream)) {
+        if (int rc = mignn_linear(x, ldx, n_x, h, nullptr, 0, 0, wlog, 2 * heads, nullptr, nullptr,
+                                  0, nullptr, nullptr, 0, l, 2 * heads, stream))
             return rc;
-        }
         lg = l;
         ld_lg = 2 * heads;
     }

@@ -18,6 +18,8 @@
 // persistent kernel in tile_gemm.hip; this kernel covers everything else.
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace mignn {
 namespace {
 
@@ -129,6 +131,55 @@ __global__ __launch_bounds__(256) void input_proj_kernel(
     }
 }
 
+// Narrow transform (n <= 8 output columns, k in {64, 128, 256}, bias / ReLU
+// epilogue): GAT's logits [N, 8], the head's last layer.  A row group of
+// LPR = k / 4 lanes holds one row (a float4 per lane) and its lanes' float4
+// slices of the n weight rows (registers); n partial dots are reduced over
+// the group by xor-shuffles.  A pure stream over A -- the tiled MFMA kernel
+// spends a whole 16-column tile on n <= 8 (0.23 ms vs ~0.1 ms at 1M x 128).
+template <int LPR>
+__global__ __launch_bounds__(256) void narrow_linear_kernel(const float* __restrict__ a, int64_t lda,
+                                                            int64_t m, int k,
+                                                            const float* __restrict__ w, int n,
+                                                            const float* __restrict__ bias, int flags,
+                                                            float* __restrict__ c, int64_t ldc) {
+    constexpr int RPW = 64 / LPR;
+    const int lane = static_cast<int>(threadIdx.x & 63);
+    const int cl = lane % LPR, grp = lane / LPR;
+    f32x4 wv[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o)
+        wv[o] = o < n ? *reinterpret_cast<const f32x4*>(w + o * k + 4 * cl) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int64_t wave = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * 4 * RPW;
+    for (int64_t row = wave * RPW + grp; row < m; row += stride) {
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(a + row * lda + 4 * cl);
+        float v[8];
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+            float d = xv[0] * wv[o][0];
+            d = fmaf(xv[1], wv[o][1], d);
+            d = fmaf(xv[2], wv[o][2], d);
+            d = fmaf(xv[3], wv[o][3], d);
+            v[o] = d;
+        }
+#pragma unroll
+        for (int off = LPR / 2; off > 0; off >>= 1)
+#pragma unroll
+            for (int o = 0; o < 8; ++o) v[o] += __shfl_xor(v[o], off);
+        if (cl == 0) {
+#pragma unroll
+            for (int o = 0; o < 8; ++o)
+                if (o < n) {
+                    float y = v[o];
+                    if (flags & MIGNN_EPI_BIAS) y += bias[o];
+                    if (flags & MIGNN_EPI_RELU) y = y < 0.f ? 0.f : y;
+                    c[row * ldc + o] = y;
+                }
+        }
+    }
+}
+
 }  // namespace
 }  // namespace mignn
 
@@ -158,6 +209,18 @@ extern "C" int mignn_diag_linear(const float* a, int64_t lda, int64_t m, int k, 
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_RESIDUAL) || residual, "linear: residual flag without R");
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "linear: affine w/o params");
     if (m == 0) return MIGNN_OK;
+    if (k2 == 0 && n <= 8 && (k == 64 || k == 128 || k == 256) &&
+        !(flags & (MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE))) {
+        const int64_t waves = (m * (k / 4) + 63) / 64;
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>((waves + 3) / 4, 4096));
+        hipStream_t st = as_stream(stream);
+        switch (k) {
+            case 64: narrow_linear_kernel<16><<<grid, 256, 0, st>>>(a, lda, m, k, w, n, bias, flags, c, ldc); break;
+            case 128: narrow_linear_kernel<32><<<grid, 256, 0, st>>>(a, lda, m, k, w, n, bias, flags, c, ldc); break;
+            default: narrow_linear_kernel<64><<<grid, 256, 0, st>>>(a, lda, m, k, w, n, bias, flags, c, ldc); break;
+        }
+        return launch_status("narrow_linear_kernel");
+    }
     if (k2 == 0) {
         bool handled = false;
         const int rc = tile_linear(a, lda, m, k, w, n, bias, residual, ldr, scale, shift, flags,

@@ -135,6 +135,30 @@ def test_linear_vs_fp64(M, K, K2, N):
     assert (plain.cpu().double() - A.double() @ W[:, :K].double().T).abs().max().item() < 1e-5
 
 
+@pytest.mark.parametrize("M,K,N", [(1, 64, 1), (1000, 128, 8), (777, 64, 7), (513, 256, 3),
+                                   (4099, 128, 8)])
+def test_narrow_linear_vs_fp64(M, K, N):
+    """n <= 8 outputs at k in {64, 128, 256}: the streaming row-dot kernel of
+    mignn_linear (bias + ReLU epilogue; a residual falls back to the tiles)."""
+    g = torch.Generator().manual_seed(7 * M + K + N)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * 0.1
+    b = torch.randn(N, generator=g)
+    got = linear(A.to(DEV), W.to(DEV), b.to(DEV), relu=True).cpu().double()
+    ref = torch.relu(A.double() @ W.double().T + b.double())
+    assert (got - ref).abs().max().item() < 1e-5
+    plain = linear(A.to(DEV), W.to(DEV)).cpu().double()
+    assert (plain - A.double() @ W.double().T).abs().max().item() < 1e-5
+    # strided rows and a strided output
+    Ab = torch.randn(M, K + 8, generator=g)
+    out = torch.full((M, 12), float("nan"))
+    o = out.to(DEV)
+    linear(Ab.to(DEV)[:, :K], W.to(DEV), b.to(DEV), out=o[:, :N])
+    o = o.cpu()
+    assert (o[:, :N].double() - (Ab[:, :K].double() @ W.double().T + b.double())).abs().max() < 1e-5
+    assert torch.isnan(o[:, N:]).all()
+
+
 def test_linear_identity_asymmetric():
     # A = I with an asymmetric W catches a transposed C-write
     n = 48
