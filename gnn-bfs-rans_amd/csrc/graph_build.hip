@@ -81,32 +81,52 @@ __global__ void csr_count_kernel(const int64_t* __restrict__ ei, int64_t E, int6
     const int lane = threadIdx.x & 63;
     unsigned kept = 0, bad = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < E; base += stride) {
-        const int64_t e = base + threadIdx.x;           // uniform trip count: whole waves
-        const bool in = e < E;
-        int64_t s = -1, d = -1;
-        if (in) {
-            // transposed: rows keyed by the source (backward of the aggregation)
-            s = ei[transpose ? E + e : e];
-            d = ei[transpose ? e : E + e];
+    // kU edges per lane per trip, their loads (edge ends, then relabels)
+    // issued together: the per-edge chain load -> relabel -> atomic is
+    // latency-bound at one edge in flight per lane
+    constexpr int kU = 4;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < E; base += kU * stride) {
+        int64_t s[kU], d[kU];
+        bool in[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t e = base + u * stride + threadIdx.x;   // uniform trip count: whole waves
+            in[u] = e < E;
+            s[u] = -1;
+            d[u] = -1;
+            if (in[u]) {
+                // transposed: rows keyed by the source (backward of the aggregation)
+                s[u] = ei[transpose ? E + e : e];
+                d[u] = ei[transpose ? e : E + e];
+            }
         }
-        const bool valid = in & (s >= 0) & (s < N) & (d >= 0) & (d < N);
-        bool keep = valid;
-        if (mode == MIGNN_CSR_ONE_SELF_LOOP && s == d) keep = false;
-        int64_t sn = s, dn = d;
-        if (relabel != nullptr && valid) {   // node ids in the internal (relabelled) order
-            sn = relabel[s];
-            dn = relabel[d];
+        bool valid[kU];
+        int64_t sn[kU], dn[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            valid[u] = in[u] & (s[u] >= 0) & (s[u] < N) & (d[u] >= 0) & (d[u] < N);
+            sn[u] = s[u];
+            dn[u] = d[u];
+            if (relabel != nullptr && valid[u]) {   // node ids in the internal (relabelled) order
+                sn[u] = relabel[s[u]];
+                dn[u] = relabel[d[u]];
+            }
         }
-        const uint32_t key = keep ? static_cast<uint32_t>(dn) : static_cast<uint32_t>(N);
-        if (in) {
-            keys[e] = key;
-            vals[e] = valid ? static_cast<int32_t>(sn) : 0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t e = base + u * stride + threadIdx.x;
+            bool keep = valid[u];
+            if (mode == MIGNN_CSR_ONE_SELF_LOOP && s[u] == d[u]) keep = false;
+            const uint32_t key = keep ? static_cast<uint32_t>(dn[u]) : static_cast<uint32_t>(N);
+            if (in[u]) {
+                keys[e] = key;
+                vals[e] = valid[u] ? static_cast<int32_t>(sn[u]) : 0;
+            }
+            int hl, rl;
+            if (wave_run(key, keep, lane, hl, rl)) atomicAdd(&deg[key], rl);
+            kept += keep ? 1u : 0u;
+            bad += (in[u] && !valid[u]) ? 1u : 0u;
         }
-        int hl, rl;
-        if (wave_run(key, keep, lane, hl, rl)) atomicAdd(&deg[key], rl);
-        kept += keep ? 1u : 0u;
-        bad += (in && !valid) ? 1u : 0u;
     }
     if (kept) atomicAdd(&s_kept, kept);
     if (bad) atomicAdd(&s_bad, bad);
@@ -129,23 +149,40 @@ __global__ void csr_scatter_kernel(const uint32_t* __restrict__ keys,
                                    int32_t* __restrict__ col, uint8_t* __restrict__ unsorted) {
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < E; base += stride) {
-        const int64_t e = base + threadIdx.x;
-        const bool in = e < E;
-        const uint32_t k = in ? keys[e] : static_cast<uint32_t>(N);
-        const bool keep = k < static_cast<uint32_t>(N);
-        int hl, rl;
-        int32_t pos0 = 0;
-        if (wave_run(k, keep, lane, hl, rl)) {
-            const int32_t b = row_ptr0[k];
-            pos0 = b + atomicAdd(&fill[k], rl);
-            if (rl != row_ptr0[k + 1] - b) unsorted[k] = 1;
+    constexpr int kU = 4;   // edges per lane per trip, loads issued together (as csr_count)
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < E; base += kU * stride) {
+        uint32_t kk[kU];
+        int32_t vv[kU], b0[kU], b1[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t e = base + u * stride + threadIdx.x;
+            const bool in = e < E;
+            kk[u] = in ? keys[e] : static_cast<uint32_t>(N);
+            vv[u] = in ? vals[e] : 0;
         }
-        pos0 = __shfl(pos0, hl);
-        if (keep) {
-            const int32_t pos = pos0 + (lane - hl);
-            slot_eid[pos] = static_cast<int32_t>(e);
-            col[pos + (one_loop ? static_cast<int32_t>(k) : 0)] = vals[e];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {   // the rows' bounds (every kept lane: L1 hits)
+            const bool keep = kk[u] < static_cast<uint32_t>(N);
+            b0[u] = keep ? row_ptr0[kk[u]] : 0;
+            b1[u] = keep ? row_ptr0[kk[u] + 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t e = base + u * stride + threadIdx.x;
+            const uint32_t k = kk[u];
+            const bool keep = k < static_cast<uint32_t>(N);
+            int hl, rl;
+            int32_t pos0 = 0;
+            if (wave_run(k, keep, lane, hl, rl)) {
+                pos0 = b0[u] + atomicAdd(&fill[k], rl);
+                if (rl != b1[u] - b0[u]) unsorted[k] = 1;
+            }
+            pos0 = __shfl(pos0, hl);
+            if (keep) {
+                const int32_t pos = pos0 + (lane - hl);
+                slot_eid[pos] = static_cast<int32_t>(e);
+                col[pos + (one_loop ? static_cast<int32_t>(k) : 0)] = vv[u];
+            }
         }
     }
 }
