@@ -124,6 +124,8 @@ def parse():
     p.add_argument("--no-legs", action="store_true", help="skip the other-config legs")
     p.add_argument("--legs", default="gcn_h64,shuffled,gat,transformer,gin",
                    help="comma list of legs (see the docstring)")
+    p.add_argument("--oversubscribe", action="store_true",
+                   help="rehearsal only: every rank on GPU 0, gloo + host-staged halo")
     return p.parse_args()
 
 
@@ -143,10 +145,19 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    # --oversubscribe (rehearsal of the N > 1 path on a one-GPU box only):
+    # every rank on device 0, gloo with the halo staged through host memory
+    # (mignn.dist.DistExchange); the driver's multi-GPU runs use one GPU per
+    # rank and RCCL
+    if args.oversubscribe:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.oversubscribe:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from mignn import FlowGNN
     from mignn.dist import DistExchange, DistRequests, FlowGNNShard, RangeLayout, sharded_forward
@@ -171,27 +182,26 @@ def main():
             return model(x, ei)
     else:
         # contiguous node ranges of the 250 x 200 x (200 N) mesh (natural order:
-        # k-slabs), this rank's in-edges with global ids, RCCL halo exchange
+        # k-slabs), this rank's in-edges with global ids, RCCL halo exchange.
+        # The partition layout (ghost lists, interior-first locality order,
+        # send lists) is built once, outside the timed loop; each timed step
+        # rebuilds the rank-local CSR + GCN weights (with the ghost-degree
+        # exchange) as the N = 1 step rebuilds its CSR from edge_index
         x, ei = grid_graph(nx, ny, nz * world, device=dev, z_begin=rank * nz, z_count=nz)
         E_local = ei.shape[1]
         N_local = x.shape[0]
         bounds = [r * N_local for r in range(world + 1)]
         exch = DistExchange()
         order = (lambda p, e: locality_order(p, e)[0]) if model._use_reorder(x) else None
-        shard_box = []
-
-        def setup():
-            lay = RangeLayout(ei, bounds, rank, DistRequests(device=dev), pos=x, order_fn=order)
-            sh = FlowGNNShard(model, lay, x)
-            sh.setup(exch, [sh])
-            shard_box[:] = [sh]
-
-        setup()
+        lay = RangeLayout(ei, bounds, rank, DistRequests(), pos=x, order_fn=order)
+        shard = FlowGNNShard(model, lay, x)
+        shard.setup(exch, [shard])
+        del ei
 
         def step():
             if model._csr.capacity <= 0:      # graph setup inside the step (see timed_loop)
-                setup()
-            return sharded_forward(shard_box, exch, [x])[0]
+                shard.setup_graph(exch, [shard])
+            return sharded_forward([shard], exch, [x])[0]
 
     # ---- live per-launch timing of the dominant (GCN layer) kernel
     launches = []   # (start_event, end_event, n_rows) of the headline loop
@@ -284,9 +294,12 @@ def main():
                      "seeded random weights",
             "nodes_per_gpu": N_local, "edges_per_gpu": E_local, "global_batch": 1,
             "parallelism": "single" if world == 1 else f"node_range{world}+rccl_halo",
-            "internal_node_order": ("locality (4x4-cell pencils, mignn_locality_order; part of "
-                                    "the per-step graph setup)" + ("" if world == 1 else
-                                    ", inside each rank's range, interior rows first"))
+            "internal_node_order": ("locality (4x4x4-cell blocks in panels of 4x4 block "
+                                    "columns, mignn_locality_order; part of the per-step graph "
+                                    "setup)" if world == 1 else
+                                    "locality order inside each rank's range, interior rows "
+                                    "first (built once per partition; the rank-local CSR is "
+                                    "rebuilt every step)")
                                    if model._use_reorder(x) else "as given",
         },
         "roofline": roofline,
@@ -295,8 +308,12 @@ def main():
     if world > 1:
         dist.barrier()
 
+    cpu_threads = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu_threads = cpu_thread_sweep(dev)
+        progress(f"cpu thread sweep: {cpu_threads}")
     if rank == 0 and not args.no_bfs:
-        line["bfs_mesh"] = bfs_leg(dev)
+        line["bfs_mesh"] = bfs_leg(dev, cpu_threads)
     if rank == 0 and world == 1 and not args.no_legs:
         model._csr.entries.clear()
         del x
@@ -307,7 +324,7 @@ def main():
             heavy = name in ("transformer", "gin")
             line["legs"][name] = eval_leg(name, dev, args.precision,
                                           steps=max(1, min(args.steps, 3 if heavy else 10)),
-                                          warmup=1 if heavy else 2)
+                                          warmup=1 if heavy else 2, cpu_threads=cpu_threads)
             progress(f"leg {name}: {line['legs'][name]['ms_per_forward']} ms per forward")
     if rank == 0 and world == 1 and not args.no_graph:
         line["graph_build"] = graph_build_leg(dev, nx, ny, nz, not args.no_cpu)
@@ -316,7 +333,7 @@ def main():
         line["train_step"] = train_leg(dev, args)
         progress("train_step leg done")
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_leg(model, sd, cfg, args, dev)
+        line["cpu_baseline"] = cpu_leg(model, sd, cfg, args, dev, cpu_threads)
         progress("cpu_baseline leg done")
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -402,9 +419,50 @@ LEGS = {
 LEG_CONFIG = {"gcn_h64": "SURVEY 8d H=64 HBM-target layer", "shuffled": "configs[1] model, shuffled order",
               "gat": "configs[2]", "transformer": "configs[3]",
               "gin": "configs[4] model, one GPU's shard of the 100M mesh"}
+# bounded CPU samples of each leg's model (a few seconds of oracle work each;
+# the CPU path is O(L E H + L N H^2) with no cache effects at these sizes, so
+# its edges/s is taken as size-independent and stated as such)
+LEG_CPU_SAMPLE = {"gcn_h64": (100, 100, 100), "shuffled": (80, 80, 80), "gat": (60, 60, 60),
+                  "transformer": (40, 40, 32), "gin": (50, 50, 40)}
 
 
-def eval_leg(name, dev, precision, steps, warmup):
+def cpu_thread_sweep(dev):
+    """The torch-CPU thread count used for every CPU baseline: the fastest of
+    a sweep up to this process's CPU affinity (torch's CPU kernels ran 3.6x
+    slower on all 256 hardware threads of the 2-socket host than on 32)."""
+    from oracle import flowgnn_oracle as orc
+    from mignn import FlowGNN
+    from mignn.synthetic import grid_graph, seeded_state_dict
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    avail = max(1, avail or 1)
+    cfg = dict(hidden_dim=128, num_layers=4, layer_type="GCN")
+    sd = seeded_state_dict(FlowGNN(input_dim=3, output_dim=7, **cfg).state_dict(), seed=0)
+    xs, eis = (t.cpu() for t in grid_graph(40, 40, 40, device=dev))
+    sweep = {}
+    for nt in sorted({c for c in (8, 16, 32, 64, 128, avail) if c <= avail}):
+        torch.set_num_threads(nt)
+        orc.flowgnn_forward(sd, cfg, xs, eis, None, dtype=torch.float32)
+        t0 = time.perf_counter()
+        orc.flowgnn_forward(sd, cfg, xs, eis, None, dtype=torch.float32)
+        sweep[nt] = round(time.perf_counter() - t0, 4)
+    threads = min(sweep, key=sweep.get)
+    return {"threads": threads, "cpus_available": avail, "os_cpu_count": os.cpu_count(),
+            "sweep_s_40x40x40": sweep}
+
+
+def cpu_time_model(sd, cfg, x, ei, cpu_threads, reps=1):
+    """Median seconds of the torch-CPU oracle forward (fp32) on (x, ei)."""
+    from oracle import flowgnn_oracle as orc
+    torch.set_num_threads(cpu_threads["threads"])
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        orc.flowgnn_forward(sd, cfg, x, ei, None, dtype=torch.float32)
+        times.append(time.perf_counter() - t0)
+    return statistics.median(times)
+
+
+def eval_leg(name, dev, precision, steps, warmup, cpu_threads=None):
     """One other-config forward (see the docstring): ms per forward, edges/s,
     per-layer roofline."""
     from mignn import FlowGNN
@@ -412,7 +470,8 @@ def eval_leg(name, dev, precision, steps, warmup):
     lt, H, L, dims, shuffle, setup_in_step = LEGS[name]
     cfg = dict(hidden_dim=H, num_layers=L, layer_type=lt)
     model = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
-    model.load_state_dict(seeded_state_dict(model.state_dict(), seed=0))
+    sd = seeded_state_dict(model.state_dict(), seed=0)
+    model.load_state_dict(sd)
     model = model.to(dev).eval()
     model.precision = precision
     x, ei = grid_graph(*dims, device=dev, permute_seed=shuffle)
@@ -481,10 +540,23 @@ def eval_leg(name, dev, precision, steps, warmup):
         }
     del model, x, ei
     torch.cuda.empty_cache()
+    if cpu_threads is not None:
+        cdims = LEG_CPU_SAMPLE[name]
+        xc, eic = (t.cpu() for t in grid_graph(*cdims, device=dev, permute_seed=shuffle))
+        tc = cpu_time_model(sd, cfg, xc, eic, cpu_threads)
+        out["cpu_baseline"] = {
+            "value": L * eic.shape[1] / tc, "unit": "edges/s", "cores": cpu_threads["threads"],
+            "kind": "port", "s_per_forward": round(tc, 3),
+            "sample": f"{lt} L{L} H{H} forward on the {cdims[0]}x{cdims[1]}x{cdims[2]} periodic "
+                      f"mesh ({xc.shape[0]} nodes, {eic.shape[1]} edges"
+                      + (", shuffled" if shuffle is not None else "") + "), torch-CPU oracle "
+                      "fp32, one timed run; edges/s taken as size-independent (not timed at "
+                      "the leg's full size)",
+            "gpu_over_cpu": round(out["edges_per_s"] / (L * eic.shape[1] / tc), 1)}
     return out
 
 
-def bfs_leg(dev):
+def bfs_leg(dev, cpu_threads=None):
     """configs[1]: 4-layer GCN H=128 on the reference-built BFS mesh vs the
     committed reference-CPU output."""
     import numpy as np
@@ -542,7 +614,15 @@ def bfs_leg(dev):
         fields[k] = {"mae": float(d.mean()), "max_abs": float(d.max()),
                      "field_std": float(np.std(refs[k])),
                      "max_abs_over_field_std": float(d.max() / max(np.std(refs[k]), 1e-300))}
+    cpu = None
+    if cpu_threads is not None:
+        # the reference's own inference size (inference.py:73): the whole mesh
+        tc = cpu_time_model(sd, cfg, x.cpu(), ei.cpu(), cpu_threads, reps=3)
+        cpu = {"value": cfg["num_layers"] * ei.shape[1] / tc, "unit": "edges/s",
+               "cores": cpu_threads["threads"], "kind": "port", "s_per_forward": round(tc, 4),
+               "sample": "the whole train-path BFS mesh, torch-CPU oracle fp32, median of 3"}
     return {"config": "configs[1]: GCN L4 H128, train-path BFS mesh",
+            "cpu_baseline": cpu,
             "nodes": int(x.shape[0]), "edges": int(ei.shape[1]),
             "ms_per_forward": round(t * 1e3, 4),
             "edges_per_s": cfg["num_layers"] * ei.shape[1] / t,
@@ -641,27 +721,14 @@ def graph_build_leg(dev, nx, ny, nz, with_cpu):
     return out
 
 
-def cpu_leg(model, sd, cfg, args, dev):
+def cpu_leg(model, sd, cfg, args, dev, cpu_threads):
     """The CPU oracle on a bounded sample of the same workload (1M-node mesh)."""
     from oracle import flowgnn_oracle as orc
     from mignn.synthetic import grid_graph
 
-    # every CPU this process may run on (its cpuset / affinity: the box's share
-    # of the host when the pool restricts it, else the whole machine); torch's
-    # CPU kernels do not scale to all hardware threads of a 2-socket host (256
-    # threads ran 3.6x slower than 16 in round 2), so the thread count is the
-    # fastest of a sweep up to that limit, timed on a small mesh
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    avail = max(1, avail or 1)
-    xs, eis = (t.cpu() for t in grid_graph(40, 40, 40, device=dev))
-    sweep = {}
-    for nt in sorted({c for c in (8, 16, 32, 64, 128, avail) if c <= avail}):
-        torch.set_num_threads(nt)
-        orc.flowgnn_forward(sd, cfg, xs, eis, None, dtype=torch.float32)
-        t0 = time.perf_counter()
-        orc.flowgnn_forward(sd, cfg, xs, eis, None, dtype=torch.float32)
-        sweep[nt] = round(time.perf_counter() - t0, 4)
-    threads = min(sweep, key=sweep.get)
+    threads = cpu_threads["threads"]
+    avail = cpu_threads["cpus_available"]
+    sweep = cpu_threads["sweep_s_40x40x40"]
     torch.set_num_threads(threads)
     cx, cy, cz = (int(v) for v in args.cpu_grid.split(","))
     xg, eig = grid_graph(cx, cy, cz, device=dev)

@@ -7,12 +7,14 @@
 // Edges are visited in CSR order == edge_index order (stable CSR), which is
 // also the order PyG's scatter-add visits them on the CPU.
 //
-//  gcn_aggregate_kernel   GCNConv message/aggregate with gcn_norm weights
-//  sum_aggregate_kernel   GINConv: sum_j x_j + (1+eps) x_i
-//  gat_aggregate_kernel   GATConv: LeakyReLU logits, per-row max / sum-exp
-//                         (+1e-16), alpha-weighted sums of x_j for every head
-//  transformer_aggregate  TransformerConv: online softmax of (q~_i . x_j + c_i)
-//                         * 1/sqrt(C) with alpha-weighted sums of x_j per head
+//  sum_rows_kernel        GCNConv (gcn_norm weights) / GINConv (sum_j x_j +
+//                         (1+eps) x_i), CSR entries 8 at a time
+//  gat_rows_kernel        GATConv, 4 heads (h 32..256): LeakyReLU logits,
+//                         per-row max / sum-exp (+1e-16), alpha-weighted sums
+//  tf_rows_kernel         TransformerConv, 4 heads (h 64..256): online softmax
+//                         of (q~_i . x_j + c_i) / sqrt(C), alpha-weighted sums
+//  gat_aggregate_kernel / transformer_aggregate_kernel: the same for any other
+//                         head count / width, one CSR entry at a time
 // The per-head transforms are applied afterwards by one MFMA GEMM
 // (`mignn_linear`) with the weights re-associated on the host side
 // (see mignn/gnn_model.py), so the [N, heads*C] projected tensors of the
@@ -52,62 +54,6 @@ __device__ __forceinline__ RowCursor row_of(int64_t row_begin) {
 template <int LPR>
 __device__ __forceinline__ int64_t row_stride() {
     return ((int64_t)gridDim.x * blockDim.x >> 6) * (64 / LPR);
-}
-
-// ---------------------------------------------------------------- GCN / GIN
-template <int LPR, int CPL, bool GCN>
-__global__ __launch_bounds__(256) void weighted_sum_kernel(
-    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ dinv, const float* __restrict__ x, int64_t ldx, float self_scale,
-    int64_t row_begin, int64_t row_end, int h4, float* __restrict__ out, int64_t ldo) {
-    RowCursor rc = row_of<LPR>(row_begin);
-    const int64_t stride = row_stride<LPR>();
-    for (int64_t row = rc.row; row < row_end; row += stride) {
-        const int beg = row_ptr[row], end = row_ptr[row + 1];
-        const float di = GCN ? dinv[row] : 1.f;
-        float4 acc[CPL];
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        int e = beg;
-        for (; e + 4 <= end; e += 4) {
-            int j[4];
-            float w[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) j[u] = col[e + u];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) w[u] = GCN ? dinv[j[u]] * di : 1.f;
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int q = 0; q < CPL; ++q) {
-                    const int ch = rc.c + q * LPR;
-                    if (ch < h4) acc[q] = fma4(w[u], ld4(x + (int64_t)j[u] * ldx + 4 * ch), acc[q]);
-                }
-        }
-        for (; e < end; ++e) {
-            const int j = col[e];
-            const float w = GCN ? dinv[j] * di : 1.f;
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                const int ch = rc.c + q * LPR;
-                if (ch < h4) acc[q] = fma4(w, ld4(x + (int64_t)j * ldx + 4 * ch), acc[q]);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            const int ch = rc.c + q * LPR;
-            if (ch >= h4) continue;
-            float4 v = acc[q];
-            if (!GCN) {  // GINConv: out + (1 + eps) * x_i
-                const float4 xi = ld4(x + row * ldx + 4 * ch);
-                v.x = v.x + self_scale * xi.x;
-                v.y = v.y + self_scale * xi.y;
-                v.z = v.z + self_scale * xi.z;
-                v.w = v.w + self_scale * xi.w;
-            }
-            st4(out + row * ldo + 4 * ch, v);
-        }
-    }
 }
 
 // ---------------------------------------------------------------- GAT
@@ -717,15 +663,6 @@ static int check_common(const int32_t* row_ptr, const int32_t* col, const float*
     return MIGNN_OK;
 }
 
-// mignn_diag_set_agg_legacy: route the eval aggregations to the
-// entry-at-a-time kernels above (A/B timing; same results up to fp32
-// summation order)
-static bool g_agg_legacy = false;
-extern "C" int mignn_diag_set_agg_legacy(int on) {
-    g_agg_legacy = on != 0;
-    return MIGNN_OK;
-}
-
 // batched kernels: h a multiple of 4 with LPR = pow2 >= h/4 (<= 64), any CPL
 #define MIGNN_DISPATCH_SUM(h4, BODY)                                      \
     do {                                                                  \
@@ -758,13 +695,8 @@ extern "C" int mignn_gcn_aggregate(const int32_t* row_ptr, const int32_t* col, c
     MIGNN_REQUIRE(dinv, "gcn_aggregate: null dinv");
     if (re == rb) return MIGNN_OK;
     const int h4 = h / 4;
-    if (g_agg_legacy) {
-        MIGNN_DISPATCH_LPR(h4, (weighted_sum_kernel<LPR, CPL, true><<<dim3(agg_grid(re - rb, LPR)), dim3(256), 0, as_stream(stream)>>>( row_ptr, col, dinv, x, ldx, 1.f,
-                                                   rb, re, h4, out, ldo)));
-    } else {
-        MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, true><<<dim3(batched_grid(re - rb, LPR, kSumGrid)), dim3(256), 0, as_stream(stream)>>>(
-                                   row_ptr, col, dinv, x, ldx, 1.f, rb, re, h4, out, ldo)));
-    }
+    MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, true><<<dim3(batched_grid(re - rb, LPR, kSumGrid)), dim3(256), 0, as_stream(stream)>>>(
+                               row_ptr, col, dinv, x, ldx, 1.f, rb, re, h4, out, ldo)));
     return launch_status("gcn_aggregate");
 }
 
@@ -774,13 +706,8 @@ extern "C" int mignn_sum_aggregate(const int32_t* row_ptr, const int32_t* col, c
     if (int rc = check_common(row_ptr, col, x, ldx, rb, re, h, out, ldo)) return rc;
     if (re == rb) return MIGNN_OK;
     const int h4 = h / 4;
-    if (g_agg_legacy) {
-        MIGNN_DISPATCH_LPR(h4, (weighted_sum_kernel<LPR, CPL, false><<<dim3(agg_grid(re - rb, LPR)), dim3(256), 0, as_stream(stream)>>>( row_ptr, col, nullptr, x, ldx,
-                                                   self_scale, rb, re, h4, out, ldo)));
-    } else {
-        MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, false><<<dim3(batched_grid(re - rb, LPR, kSumGrid)), dim3(256), 0, as_stream(stream)>>>(
-                                   row_ptr, col, nullptr, x, ldx, self_scale, rb, re, h4, out, ldo)));
-    }
+    MIGNN_DISPATCH_SUM(h4, (sum_rows_kernel<LPR, CPL, false><<<dim3(batched_grid(re - rb, LPR, kSumGrid)), dim3(256), 0, as_stream(stream)>>>(
+                               row_ptr, col, nullptr, x, ldx, self_scale, rb, re, h4, out, ldo)));
     return launch_status("sum_aggregate");
 }
 
@@ -795,7 +722,7 @@ extern "C" int mignn_gat_aggregate(const int32_t* row_ptr, const int32_t* col,
     const int h4 = h / 4;
     hipStream_t st = as_stream(stream);
     // batched: 4 heads, h = 4 LPR (LPR in 8..64)
-    if (!g_agg_legacy && heads == 4 && (h == 32 || h == 64 || h == 128 || h == 256)) {
+    if (heads == 4 && (h == 32 || h == 64 || h == 128 || h == 256)) {
         switch (h) {
             case 32: gat_rows_kernel<8><<<dim3(batched_grid(re - rb, 8)), dim3(256), 0, st>>>(row_ptr, col, logits, x, ldx, rb, re, h, slope, out, ldo); break;
             case 64: gat_rows_kernel<16><<<dim3(batched_grid(re - rb, 16)), dim3(256), 0, st>>>(row_ptr, col, logits, x, ldx, rb, re, h, slope, out, ldo); break;
@@ -826,7 +753,7 @@ int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const
     const int h4 = h / 4;
     hipStream_t st = as_stream(stream);
     // batched: 4 heads, h = 4 LPR (LPR in 16..64)
-    if (!g_agg_legacy && heads == 4 && (h == 64 || h == 128 || h == 256)) {
+    if (heads == 4 && (h == 64 || h == 128 || h == 256)) {
         switch (h) {
             case 64: tf_rows_kernel<16><<<dim3(batched_grid(re - rb, 16)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;
             case 128: tf_rows_kernel<32><<<dim3(batched_grid(re - rb, 32)), dim3(256), 0, st>>>(row_ptr, col, qt, ldq, x, ldx, rb, re, h, score_scale, out, ldo, use_cq); break;

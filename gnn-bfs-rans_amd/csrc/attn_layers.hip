@@ -93,8 +93,10 @@ extern "C" int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const
 
 extern "C" size_t mignn_transformer_layer_scratch_bytes(int64_t rows, int h, int heads) {
     if (rows < 0 || h <= 0 || heads <= 0) return 0;
+    // rows of qt / agg: heads h sums | heads alpha sums, padded to 16 B
     const size_t k1 = static_cast<size_t>(heads) * h + heads;
-    return 2 * align256(static_cast<size_t>(rows) * k1 * 4);
+    const size_t ldq = (k1 + 3) / 4 * 4;
+    return 2 * align256(static_cast<size_t>(rows) * ldq * 4);
 }
 
 extern "C" int mignn_transformer_layer(const int32_t* row_ptr, const int32_t* col, const float* x,

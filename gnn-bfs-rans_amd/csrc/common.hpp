@@ -160,6 +160,11 @@ int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const
                                int64_t ldq, const float* x, int64_t ldx, int64_t rb, int64_t re,
                                int h, int heads, float score_scale, float* out, int64_t ldo,
                                bool use_cq, void* stream);
+// the fused split-fp16 GCN layer (gcn_fused.hip), arguments checked by the caller
+int gcn_fused_layer(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
+                    int64_t ldx, int64_t rb, int64_t re, int h, const float* w, const float* bias,
+                    const float* scale, const float* shift, int flags, float* out, int64_t ldo,
+                    void* stream);
 int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, int n,
                 const float* bias, const float* residual, int64_t ldr, const float* scale,
                 const float* shift, int flags, float* c, int64_t ldc, hipStream_t st,

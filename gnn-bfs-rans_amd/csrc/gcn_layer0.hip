@@ -11,10 +11,10 @@
 // never materialised: the kernel reads 12-32 B per neighbour instead of a
 // 512-B row and writes y once -- an HBM-write-bound pass (N*H*4 bytes).
 //
-// Layout: a wave takes 64 consecutive rows; pass 1, lane = row: gather and
-// aggregate (c_i, C_i, s_i) in CSR order into LDS; pass 2, 32 lanes x 16 B
-// per row: each lane owns 4 output columns (their 4 x (2D+2) coefficients in
-// registers) and writes two rows per store instruction (non-temporal).
+// Layout: a workgroup of 4 gather waves + 4 store waves (below); gather
+// lane = row: aggregate (c_i, C_i, s_i) in CSR order into LDS; store role: 32
+// lanes x 16 B per row, each lane owning 4 output columns (their 4 x (2D+2)
+// coefficients in registers), two rows per store instruction (non-temporal).
 #include "common.hpp"
 
 namespace mignn {
@@ -22,129 +22,14 @@ namespace {
 
 constexpr int kWaves = 4;
 
-template <int D, int DIAG = 0>   // DIAG (timing ablations): 1 = no gathers, 2 = no stores;
-                                 // 4 = records mode: write each row's aggregates (8 floats)
-__global__ __launch_bounds__(kWaves * 64) void gcn_layer0_kernel(
-    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
-    int64_t row_end, const float* __restrict__ coef, int h, float* __restrict__ out,
-    int64_t ldo) {
-    constexpr int K = 2 * D + 2;                  // coefficients per column
-    __shared__ float agg[kWaves][64][2 * D + 2];   // c_i | C_i | s_i | pad
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    float (*ag)[2 * D + 2] = agg[wave];
-    const int cpl = h / 4;                         // lanes per row (<= 64)
-    const int rps = 64 / cpl;                      // rows per store instruction
-    const int sub = lane / cpl, cq = (lane % cpl) * 4;
-    const bool active = sub < rps;
-    float cf[4][K];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            cf[q][k] = (active && (DIAG & 4) == 0) ? coef[(int64_t)(cq + q) * K + k] : 0.f;
-
-    const int64_t nrows = row_end - row_begin;
-    const int64_t stride = (int64_t)gridDim.x * kWaves * 64;
-    for (int64_t base = ((int64_t)blockIdx.x * kWaves + wave) * 64; base < nrows; base += stride) {
-        // pass 1: lane = row
-        const int64_t r = base + lane;
-        if constexpr ((DIAG & 1) != 0) {
-            ag[lane][0] = static_cast<float>(r);
-        } else if (r < nrows) {
-            const int64_t i = row_begin + r;
-            float c[D], C[D], s = 0.f;
-#pragma unroll
-            for (int a = 0; a < D; ++a) { c[a] = pos[i * ldp + a]; C[a] = 0.f; }
-            const int32_t e0 = row_ptr[i], e1 = row_ptr[i + 1];
-            // first kU entries: all index loads, then all coordinate loads (two
-            // memory round trips instead of one per entry); CSR order kept
-            constexpr int kU = 8;
-            int32_t jj[kU];
-            float ww[kU];
-#pragma unroll
-            for (int k = 0; k < kU; ++k) {
-                jj[k] = e0 + k < e1 ? col[e0 + k] : 0;
-                ww[k] = e0 + k < e1 ? ew[e0 + k] : 0.f;
-            }
-            float pv[kU][D];
-#pragma unroll
-            for (int k = 0; k < kU; ++k)
-#pragma unroll
-                for (int a = 0; a < D; ++a)
-                    pv[k][a] = e0 + k < e1 ? pos[(int64_t)jj[k] * ldp + a] : 0.f;
-#pragma unroll
-            for (int k = 0; k < kU; ++k) {
-                if (e0 + k < e1) {
-                    s += ww[k];
-#pragma unroll
-                    for (int a = 0; a < D; ++a) C[a] = fmaf(ww[k], pv[k][a], C[a]);
-                }
-            }
-            for (int32_t e = e0 + kU; e < e1; ++e) {   // rows of > kU entries
-                const int64_t j = col[e];
-                const float w = ew[e];
-                s += w;
-#pragma unroll
-                for (int a = 0; a < D; ++a) C[a] = fmaf(w, pos[j * ldp + a], C[a]);
-            }
-#pragma unroll
-            for (int a = 0; a < D; ++a) { ag[lane][a] = c[a]; ag[lane][D + a] = C[a]; }
-            ag[lane][2 * D] = s;
-        }
-        if constexpr ((DIAG & 4) != 0) {
-            // records: rec[i] = {c_i, C_i, s_i} padded to 8 floats (the REC layer
-            // kernel expands x0_i = relu(coef8 . rec_i) itself)
-            if (r < nrows) {
-                f32x4 ra = f32x4{0.f, 0.f, 0.f, 0.f}, rb = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < 2 * D + 1; ++k) {
-                    if (k < 4) ra[k] = ag[lane][k];
-                    else rb[k - 4] = ag[lane][k];
-                }
-                f32x4* const dst = reinterpret_cast<f32x4*>(out + (row_begin + r) * 8);
-                dst[0] = ra;
-                dst[1] = rb;
-            }
-            continue;
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes landed
-        __builtin_amdgcn_wave_barrier();
-        // pass 2: rps rows per instruction, lane owns columns cq .. cq + 3
-        const int64_t nblk = nrows - base < 64 ? nrows - base : 64;
-        for (int rr = 0; rr < nblk; rr += rps) {
-            const int rl = rr + sub;
-            if (active && rl < nblk) {
-                float v[K - 1];
-#pragma unroll
-                for (int k = 0; k < K - 1; ++k) v[k] = ag[rl][k];
-                float o[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    float t = cf[q][K - 1];
-#pragma unroll
-                    for (int k = 0; k < K - 1; ++k) t = fmaf(cf[q][k], v[k], t);
-                    o[q] = t < 0.f ? 0.f : t;
-                }
-                f32x4* const dst = reinterpret_cast<f32x4*>(out + (row_begin + base + rl) * ldo + cq);
-                if constexpr ((DIAG & 2) == 0)
-                    __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, dst);
-                else if (o[0] == 1234.5f) *dst = f32x4{o[0], o[1], o[2], o[3]};
-            }
-        }
-        __builtin_amdgcn_wave_barrier();   // pass 1 of the next block overwrites ag
-    }
-}
-
-// Split-role form (the default for mignn_gcn_layer0_coords): a workgroup of
-// 4 gather waves + 4 store waves walks 256-row blocks.  At iteration i the
+// Split roles: a workgroup of 4 gather waves + 4 store waves walks 256-row
+// blocks.  At iteration i the
 // gather waves (lane = row, as pass 1 above) aggregate block i into LDS
 // buffer i % 2 while the store waves expand and write block i - 1 from the
 // other buffer; one barrier per block.  The write stream (N*H*4 bytes, the
 // bound) no longer waits behind each wave's three dependent gather round
-// trips (row_ptr -> col / ew -> pos).  Same fma order as gcn_layer0_kernel:
-// bit-identical output.
+// trips (row_ptr -> col / ew -> pos) -- 1.52 -> 1.09 ms at 10M nodes against
+// the one-role form of round 1.
 constexpr int kSplitRows = kWaves * 64;   // rows per block
 
 template <int D>
@@ -277,48 +162,3 @@ extern "C" int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* co
     return launch_status("gcn_layer0_split_kernel");
 }
 
-extern "C" int mignn_gcn_layer0_records(const int32_t* row_ptr, const int32_t* col,
-                                        const float* ew, const float* pos, int64_t ldp, int in_dim,
-                                        int64_t row_begin, int64_t row_end, float* rec,
-                                        void* stream) {
-    MIGNN_REQUIRE(row_ptr && col && ew && pos && rec, "gcn_layer0_records: null pointer");
-    MIGNN_REQUIRE(in_dim >= 1 && in_dim <= 3, "gcn_layer0_records: in_dim must be 1..3 (got %d)",
-                  in_dim);
-    MIGNN_REQUIRE(ldp >= in_dim, "gcn_layer0_records: ldp < in_dim");
-    MIGNN_REQUIRE(aligned16(rec), "gcn_layer0_records: rec must be 16-B aligned");
-    MIGNN_REQUIRE(row_begin >= 0 && row_end >= row_begin, "gcn_layer0_records: bad row range");
-    if (row_end == row_begin) return MIGNN_OK;
-    hipStream_t st = as_stream(stream);
-    const int64_t blocks = (row_end - row_begin + kWaves * 64 - 1) / (kWaves * 64);
-    const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);
-    // (coef / h / ldo unused in records mode)
-    switch (in_dim) {
-    case 1: hipLaunchKernelGGL((gcn_layer0_kernel<1, 4>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, nullptr, 4, rec, 8); break;
-    case 2: hipLaunchKernelGGL((gcn_layer0_kernel<2, 4>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, nullptr, 4, rec, 8); break;
-    default: hipLaunchKernelGGL((gcn_layer0_kernel<3, 4>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, nullptr, 4, rec, 8); break;
-    }
-    return launch_status("gcn_layer0_kernel(records)");
-}
-
-extern "C" int mignn_diag_gcn_layer0(int mode, const int32_t* row_ptr, const int32_t* col,
-                                     const float* ew, const float* pos, int64_t n,
-                                     const float* coef, float* out, void* stream) {
-    MIGNN_REQUIRE(mode >= 0 && mode <= 4 && n > 0, "diag_gcn_layer0: bad args");
-    if (mode == 4) {   // the round-1 one-role kernel (exact results), for A/B timing
-        const int64_t b1 = (n + kWaves * 64 - 1) / (kWaves * 64);
-        hipLaunchKernelGGL((gcn_layer0_kernel<3, 0>), dim3(static_cast<unsigned>(b1 < 8192 ? b1 : 8192)),
-                           dim3(kWaves * 64), 0, as_stream(stream), row_ptr, col, ew, pos, 3, 0, n,
-                           coef, 128, out, 128);
-        return launch_status("gcn_layer0_kernel(diag)");
-    }
-    hipStream_t st = as_stream(stream);
-    const int64_t blocks = (n + kWaves * 64 - 1) / (kWaves * 64);
-    const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);
-    switch (mode) {
-    case 0: hipLaunchKernelGGL((gcn_layer0_kernel<3, 0>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
-    case 1: hipLaunchKernelGGL((gcn_layer0_kernel<3, 1>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
-    case 2: hipLaunchKernelGGL((gcn_layer0_kernel<3, 2>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
-    default: hipLaunchKernelGGL((gcn_layer0_kernel<3, 3>), dim3(grid), dim3(kWaves * 64), 0, st, row_ptr, col, ew, pos, 3, 0, n, coef, 128, out, 128); break;
-    }
-    return launch_status("gcn_layer0_kernel(diag)");
-}

@@ -54,9 +54,6 @@ SIGNATURES = {
                                             c_int, c_int, c_float, _P, c_int64, _P]),
     "mignn_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P, _P,
                                 c_int, _P, c_int64, _P]),
-    "mignn_gcn_layer_f16x3_rec": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P,
-                                          _P, c_int, _P, c_int64, _P]),
-    "mignn_gcn_layer0_records": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P, _P]),
     "mignn_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                       _P, _P, c_int, _P, c_int64, _P]),
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
@@ -135,17 +132,14 @@ DIAG_SIGNATURES = {
                                   _P]),
     "mignn_diag_set_trace": (c_int, [_P]),
     "mignn_diag_set_trace_f16x3": (c_int, [_P]),
-    "mignn_diag_gcn_layer0": (c_int, [c_int, _P, _P, _P, _P, c_int64, _P, _P, _P]),
     "mignn_diag_clock": (c_int, [c_int, c_int, _P, _P]),
     "mignn_diag_mlp_head": (c_int, [c_int, _P, c_int64, _P, _P, _P]),
-    "mignn_gcn_layer_ring": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
-                                     _P, _P, c_int, _P, c_int64, c_int64, _P]),
-    "mignn_diag_set_trace_ring": (c_int, [_P]),
-    "mignn_diag_set_agg_legacy": (c_int, [c_int]),
     "mignn_diag_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P,
                                      _P, c_int, _P, c_int64, _P]),
     "mignn_diag_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                            _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_layer_wave": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P,
+                                     _P, c_int, _P, c_int64, c_int, _P]),
     "mignn_diag_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,
                                   _P, c_int64, _P, _P, c_int, _P, c_int64, _P]),
 }

@@ -48,6 +48,15 @@ def range_bounds(num_nodes: int, world: int) -> List[int]:
     return [(r * num_nodes) // world for r in range(world + 1)]
 
 
+def _nonzero_known(t: torch.Tensor, count: int) -> torch.Tensor:
+    """Indices of the nonzero entries of a 1-D tensor whose count is already
+    known on the host (no second device->host sync)."""
+    try:
+        return torch.nonzero_static(t, size=count).flatten()
+    except (RuntimeError, NotImplementedError):
+        return torch.nonzero(t).flatten()
+
+
 class RangeLayout:
     """One rank's part of a contiguous node-range partition (see the module
     docstring).  `edge_index` [2, E_r] holds global ids of the edges whose
@@ -63,30 +72,50 @@ class RangeLayout:
         self.rank, self.world = rank, len(bounds) - 1
         self.bounds = [int(b) for b in bounds]
         lo, hi = self.bounds[rank], self.bounds[rank + 1]
+        N = self.bounds[-1]
         self.lo, self.hi, self.n_own = lo, hi, hi - lo
         src, dst = edge_index[0].long(), edge_index[1].long()
-        if bool(((dst < lo) | (dst >= hi)).any()):
-            raise ValueError("edge_index holds an edge whose destination this rank does not own")
-        if src.numel() and bool(((src < 0) | (src >= self.bounds[-1])).any()):
-            raise ValueError("edge_index holds a source outside [0, N)")
+        E = int(src.numel())
         own_src = (src >= lo) & (src < hi)
-        # ghosts: sorted global ids == grouped by owner rank (contiguous ranges)
-        ghost = torch.unique(src[~own_src])
-        self.ghost_gid = ghost
-        self.n_ghost = int(ghost.numel())
-        self.n_total = self.n_own + self.n_ghost
+        # ghost marks over the global ids (+1 dummy slot for owned sources)
+        mark = torch.zeros(N + 1, dtype=torch.int32, device=dev)
+        if E:
+            mark.index_fill_(0, torch.where(own_src, torch.full_like(src, N), src.clamp(0, N)), 1)
+        mark[N] = 0
+        csum = torch.cumsum(mark, 0)
         b = torch.tensor(self.bounds, dtype=torch.int64, device=dev)
-        owner = torch.searchsorted(b, ghost, right=True) - 1
-        counts = torch.bincount(owner, minlength=self.world).cpu().tolist()
+        ends = torch.where(b > 0, csum[(b - 1).clamp(min=0)], torch.zeros_like(b))
+        counts = ends[1:] - ends[:-1]                        # ghosts per owner rank
+        # boundary rows: owned destinations with a ghost source
+        boundary = torch.zeros(self.n_own, dtype=torch.int32, device=dev)
+        if E:
+            boundary.index_add_(0, (dst - lo).clamp(0, max(self.n_own - 1, 0)), (~own_src).int())
+        boundary = boundary > 0
+        # every host-side size in ONE device->host transfer
+        bad_dst = ((dst < lo) | (dst >= hi)).any() if E else torch.zeros((), dtype=torch.bool, device=dev)
+        bad_src = ((src < 0) | (src >= N)).any() if E else torch.zeros((), dtype=torch.bool, device=dev)
+        host = torch.cat([torch.stack([bad_dst.long(), bad_src.long(), (~boundary).sum(),
+                                       own_src.sum()]), counts]).cpu().tolist()
+        if host[0]:
+            raise ValueError("edge_index holds an edge whose destination this rank does not own")
+        if host[1]:
+            raise ValueError("edge_index holds a source outside [0, N)")
+        self.n_int, n_own_edges = int(host[2]), int(host[3])
+        counts = [int(c) for c in host[4:]]
         self.ghost_ptr = [0]
         for c in counts:
-            self.ghost_ptr.append(self.ghost_ptr[-1] + int(c))
+            self.ghost_ptr.append(self.ghost_ptr[-1] + c)
+        self.n_ghost = self.ghost_ptr[-1]
+        self.n_total = self.n_own + self.n_ghost
+        # ghosts: sorted global ids == grouped by owner rank (contiguous ranges)
+        ghost = _nonzero_known(mark[:N], self.n_ghost)
+        self.ghost_gid = ghost
         # local order of the owned rows: interior first, boundary last
-        boundary = torch.zeros(self.n_own, dtype=torch.bool, device=dev)
-        boundary[dst[~own_src] - lo] = True
         if order_fn is not None and pos is not None and self.n_own > 0:
-            keep = own_src
-            base = order_fn(pos, torch.stack([src[keep] - lo, dst[keep] - lo])).long()
+            # the locality order sees the edges among owned rows (own sources
+            # first by a stable sort: no host sync for the count)
+            sel = torch.sort((~own_src).to(torch.int8), stable=True).indices[:n_own_edges]
+            base = order_fn(pos, torch.stack([src[sel] - lo, dst[sel] - lo])).long()
         else:
             base = torch.arange(self.n_own, device=dev)
         key = boundary[base].to(torch.int64)
@@ -94,7 +123,6 @@ class RangeLayout:
         self.perm = perm
         self.inv = torch.empty_like(perm)
         self.inv[perm] = torch.arange(self.n_own, device=dev)
-        self.n_int = int((~boundary).sum())
         # local edge list: owned -> local position, ghost -> n_own + ghost index
         lsrc = torch.where(own_src, self.inv[(src - lo).clamp(0, max(self.n_own - 1, 0))],
                            self.n_own + torch.searchsorted(ghost, src))
@@ -122,15 +150,26 @@ class RequestExchange:
         raise NotImplementedError
 
 
+def _comm_device(group=None, device=None) -> torch.device:
+    """Where a process group's tensors must live: the given device, else the
+    current ROCm device for nccl (RCCL), else the CPU (gloo)."""
+    if device is not None:
+        return torch.device(device)
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 class DistRequests(RequestExchange):
-    """torch.distributed: counts by all_gather, id lists by P2P."""
+    """torch.distributed: counts by all_gather, id lists by P2P (on the
+    group's device: the current ROCm device under nccl, the CPU under gloo)."""
 
     def __init__(self, group=None, device=None):
         self.group, self.device = group, device
 
     def exchange(self, rank, req):
         world = dist.get_world_size(self.group)
-        dev = self.device or torch.device("cpu")
+        dev = _comm_device(self.group, self.device)
         mine = torch.zeros(world, dtype=torch.int64, device=dev)
         for q, ids in req.items():
             mine[q] = ids.numel()
@@ -196,29 +235,49 @@ def _gather_rows(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor):
 
 class DistExchange:
     """This rank's halo over torch.distributed P2P: pack each peer's rows,
-    isend; irecv straight into the peer's ghost slice."""
+    isend; irecv straight into the peer's ghost slice.  Under a backend
+    whose P2P takes host tensors only (gloo) with device activations, the
+    packed rows and the ghost slices are staged through host memory (the
+    multi-process GPU test on a one-GPU box); under nccl (RCCL) the device
+    tensors go straight to the transport."""
 
     def __init__(self, group=None):
         self.group = group
+        self._staged = None
+
+    def _stage(self, buf) -> bool:
+        if self._staged is None:
+            self._staged = dist.get_backend(self.group) != "nccl"
+        return self._staged and buf.is_cuda
 
     def start(self, shards, bufs):
         (sh,), (buf,) = shards, bufs
         lay = sh.layout
-        ops = []
+        stage = self._stage(buf)
+        ops, unstage = [], []
         for q in lay.peers():
             if q in lay.send_idx:
                 idx = lay.send_idx[q]
                 pk = torch.empty((idx.numel(), buf.shape[1]), dtype=buf.dtype, device=buf.device)
                 _gather_rows(buf, idx, pk)
-                ops.append(dist.P2POp(dist.isend, pk, q, self.group, TAG_HALO))
+                ops.append(dist.P2POp(dist.isend, pk.cpu() if stage else pk, q, self.group,
+                                      TAG_HALO))
             sl = lay.ghost_slice(q)
             if sl.stop > sl.start:
-                ops.append(dist.P2POp(dist.irecv, buf[sl], q, self.group, TAG_HALO))
-        return dist.batch_isend_irecv(ops) if ops else []
+                dst = buf[sl]
+                if stage:
+                    host = torch.empty(dst.shape, dtype=dst.dtype)
+                    unstage.append((dst, host))
+                    dst = host
+                ops.append(dist.P2POp(dist.irecv, dst, q, self.group, TAG_HALO))
+        return (dist.batch_isend_irecv(ops) if ops else [], unstage)
 
     def wait(self, handle):
-        for w in handle:
+        works, unstage = handle
+        for w in works:
             w.wait()
+        for dst, host in unstage:
+            dst.copy_(host)
 
 
 class LocalExchange:
@@ -311,7 +370,16 @@ class FlowGNNShard(Shard):
 
     def setup(self, exchange, shards: List["FlowGNNShard"]):
         """Per-graph setup of every shard in `shards` (collective over them):
-        local CSRs, GCN ghost degrees + edge weights, ghost cell centres."""
+        setup_graph (local CSRs, GCN ghost degrees + edge weights) and
+        setup_static (ghost cell centres for the fused GCN layer 0)."""
+        self.setup_graph(exchange, shards)
+        self.setup_static(exchange, shards)
+
+    def setup_graph(self, exchange, shards: List["FlowGNNShard"]):
+        """The rank-local CSRs on the device, GCN's ghost deg^-1/2 from their
+        owners and the gcn_norm edge weights -- what FlowGNN.forward rebuilds
+        from edge_index when its CSR cache is off (the bench's per-step graph
+        setup)."""
         from ._lib import CSR_ONE_SELF_LOOP, CSR_VERBATIM
         from .gnn_model import build_csr
         m = self.model
@@ -324,6 +392,12 @@ class FlowGNNShard(Shard):
                                                for sh in shards])
             for sh in shards:
                 sh.csr.compute_gcn_weights(0, sh.layout.n_own)
+
+    def setup_static(self, exchange, shards: List["FlowGNNShard"]):
+        """Static per-layout data: the ghost rows' cell centres (the fused
+        input_proj + GCN layer 0 reads coordinates, so layer 0 needs no
+        feature exchange)."""
+        m = self.model
         if m._fuse_layer0():
             D = m.input_dim
             poss = []
@@ -350,6 +424,7 @@ class FlowGNNShard(Shard):
         return 0
 
     def before_halo(self, i, x):
+        """GAT: the owned rows' logits, computed while the features move."""
         if self.model.layer_type == "GAT":
             from .gnn_model import linear
             layer = self.model.gnn_layers[i]
@@ -360,6 +435,7 @@ class FlowGNNShard(Shard):
             linear(x[:self.layout.n_own], wlog, out=self.logits[:self.layout.n_own])
 
     def after_halo(self, i, x):
+        """GAT: the ghost rows' logits, from their rows that just landed."""
         if self.model.layer_type == "GAT" and self.layout.n_ghost:
             from .gnn_model import linear
             layer = self.model.gnn_layers[i]

@@ -149,8 +149,10 @@ class Csr:
 
 
 def locality_order(pos: torch.Tensor, edge_index: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(perm, inv) of mignn_locality_order: 4x4-cell pencils of the mesh given
-    by the cell centres `pos` [N, >=3]; perm[new] = old id, inv[old] = new."""
+    """(perm, inv) of mignn_locality_order: 4x4x4-cell blocks (one 64-row tile
+    of the fused layer each) in panels of 4x4 block columns swept along the
+    third axis, from the cell centres `pos` [N, >=3]; perm[new] = old id,
+    inv[old] = new."""
     dev = pos.device
     n = int(pos.shape[0])
     p = pos if (pos.dtype == torch.float32 and pos.stride(1) == 1) else pos.float().contiguous()
@@ -378,6 +380,13 @@ class FlowGNN(nn.Module):
         self.reorder = os.environ.get("MIGNN_REORDER", "auto")
         self._csr = _CsrCache()
         self._prep: Dict[Tuple, object] = {}
+        self._dtypes_checked = False
+
+    def _apply(self, fn, *args, **kwargs):
+        # every parameter conversion / move passes here: re-check the dtypes
+        # at the next forward
+        self._dtypes_checked = False
+        return super()._apply(fn, *args, **kwargs)
 
     # ------------------------------------------------------------------ API
     def predict_fields(self, output: torch.Tensor) -> dict:
@@ -414,20 +423,7 @@ class FlowGNN(nn.Module):
         csr = self._csr.get(edge_index, num_nodes, mode, pos)
         cur, nxt = buf_a, buf_b
         first = 0
-        if self._records_layer1():
-            # layer 0 as per-node records (c_i, C_i, s_i: 32 B) and GCN layer 1
-            # expanding x0 = relu(coef8 . rec) on the fly: the [N, H] layer-0
-            # activations never reach HBM (mignn_gcn_layer_f16x3_rec)
-            try:
-                rec = self._gcn_layer0_records(xin, csr)
-            except RuntimeError as e:
-                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
-            try:
-                self._gcn_layer1_rec(csr, rec, cur)
-            except RuntimeError as e:
-                raise self._layer_error(1, e, num_nodes, edge_index, xin, edge_attr) from e
-            first = 2
-        elif self._fuse_layer0():
+        if self._fuse_layer0():
             # input_proj + GCN layer 0 from the coordinates (mignn_gcn_layer0_coords)
             try:
                 self._gcn_layer0(xin, csr, cur)
@@ -460,9 +456,13 @@ class FlowGNN(nn.Module):
                 "graph to 'cuda' (HIP).")
         if self.input_proj.weight.device != x.device:
             raise RuntimeError(f"model is on {self.input_proj.weight.device}, input on {x.device}")
-        for p in self.parameters():
-            if p.dtype != torch.float32:
-                raise RuntimeError("mignn FlowGNN computes in fp32; parameters must be float32")
+        if not self._dtypes_checked:
+            # once per .to() / .float() / .half() ... (nn.Module._apply below),
+            # not per forward
+            for p in self.parameters():
+                if p.dtype != torch.float32:
+                    raise RuntimeError("mignn FlowGNN computes in fp32; parameters must be float32")
+            self._dtypes_checked = True
         if self.hidden_dim % 8 != 0:
             raise RuntimeError("mignn FlowGNN requires hidden_dim % 8 == 0")
         if self.precision not in ("f32", "f16x3"):
@@ -609,15 +609,6 @@ class FlowGNN(nn.Module):
             return torch.cat([A, B, d[:, None], e[:, None]], 1).float().contiguous()
         return self._cached("layer0", 0, ts, make)
 
-    def _records_layer1(self) -> bool:
-        """Layer 0 as records + records-input GCN layer 1: f16x3 precision, the
-        fused layer-0 conditions with <= 3 input features, H in {64, 128}, at
-        least two layers; opt-in ($MIGNN_REC=1) until it beats the
-        materialised pair (layer0 kernel + fused layer 1) on the bench mesh."""
-        return (os.environ.get("MIGNN_REC", "0") == "1" and self.precision == "f16x3"
-                and self._fuse_layer0() and self.input_dim <= 3
-                and self.hidden_dim in (64, 128) and self.num_layers >= 2)
-
     def _coords(self, x, csr: Csr):
         """The node features (coordinates) in the CSR's node order."""
         if csr.perm is None:
@@ -628,36 +619,6 @@ class FlowGNN(nn.Module):
             _lib.ptr(x), x.stride(0), _lib.ptr(csr.perm), x.shape[0], D, _lib.ptr(pos), D,
             _stream(x)), "mignn_rows_gather")
         return pos
-
-    def _gcn_layer0_records(self, x, csr: Csr) -> torch.Tensor:
-        pos = self._coords(x, csr)
-        rec = torch.empty((x.shape[0], 8), dtype=torch.float32, device=x.device)
-        _lib.check(_lib.lib().mignn_gcn_layer0_records(
-            _lib.ptr(csr.row_ptr), _lib.ptr(csr.col), _lib.ptr(csr.ew), _lib.ptr(pos),
-            pos.stride(0), self.input_dim, 0, x.shape[0], _lib.ptr(rec), _stream(x)),
-            "mignn_gcn_layer0_records")
-        return rec
-
-    def _layer0_coef8(self):
-        """_layer0_coef padded to 8 per column: [A | B | d | 0.. | e] against
-        the record [c | C | s | 0..] (gcn_layer0.hip records mode)."""
-        c = self._layer0_coef()
-        K = c.shape[1]
-        if K == 8:
-            return c
-        return self._cached("layer0_8", 0, (c,), lambda: torch.cat(
-            [c[:, :K - 1], torch.zeros((c.shape[0], 8 - K), dtype=c.dtype, device=c.device),
-             c[:, K - 1:]], 1).contiguous())
-
-    def _gcn_layer1_rec(self, csr: Csr, rec, out):
-        layer = self.gnn_layers[1]
-        scale, shift = self._bn(1)
-        epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
-        P = _lib.ptr
-        _lib.check(_lib.lib().mignn_gcn_layer_f16x3_rec(
-            P(csr.row_ptr), P(csr.col), P(csr.ew), P(rec), P(self._layer0_coef8()), 0,
-            rec.shape[0], self.hidden_dim, P(layer.lin.weight), P(layer.bias), P(scale), P(shift),
-            epi, P(out), out.stride(0), _stream(rec)), "mignn_gcn_layer_f16x3_rec")
 
     def _gcn_layer0(self, x, csr: Csr, out):
         D = self.input_dim

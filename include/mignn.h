@@ -273,25 +273,6 @@ int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* col, const fl
                             int64_t row_end, const float* coef, int h, float* out, int64_t ldo,
                             void* stream);
 
-/* Layer 0 as records (in_dim 1..3): rec[i] = {pos_i, C_i, s_i, 0...} (8 floats,
- * 16-B aligned rows) -- the aggregates of mignn_gcn_layer0_coords before its
- * per-column expansion; 32 B per node instead of an h-wide row. */
-int mignn_gcn_layer0_records(const int32_t* row_ptr, const int32_t* col, const float* ew,
-                             const float* pos, int64_t ldp, int in_dim, int64_t row_begin,
-                             int64_t row_end, float* rec, void* stream);
-/* GCN layer 1 straight from layer-0 records: mignn_gcn_layer_f16x3 with every
- * x row (own and neighbour) expanded on the fly as
- *   x_j[n] = relu( coef8[n][7] + sum_{k<7} coef8[n][k] rec_j[k] )
- * (bit-identical to mignn_gcn_layer0_coords' output with coef8 = coef padded
- * to [A | B | d | 0... | e]).  The [N, h] layer-0 activations are never
- * written or read: ~32 B of HBM per node instead of 2 h floats.  h in
- * {64, 128}; flags / epilogue as mignn_gcn_layer. */
-int mignn_gcn_layer_f16x3_rec(const int32_t* row_ptr, const int32_t* col, const float* ew,
-                              const float* rec, const float* coef8, int64_t row_begin,
-                              int64_t row_end, int h, const float* w, const float* bias,
-                              const float* scale, const float* shift, int flags, float* out,
-                              int64_t ldo, void* stream);
-
 /* Fused GIN layer (gnn_model.py:70-75, :166, :184-191), h in {64, 128}:
  *   tmp_i = relu(nn.0( sum_{j in row i} x_j + (1 + eps) x_i ))      (rows rb..re -> tmp[0..])
  *   out_i = epi( nn.2(tmp_i) ) with residual x_i, BN affine, ReLU   (flags as above)

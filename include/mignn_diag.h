@@ -76,35 +76,17 @@ int mignn_diag_set_trace_f16x3(void* buf);
  * out[2b] = s_memtime delta, out[2b+1] = s_memrealtime delta (100 MHz). */
 int mignn_diag_clock(int blocks, int iters, int64_t* out, void* stream);
 
-/* input_proj + GCN layer 0 (H = 128, D = 3) timing ablations (mode 4: the
- * one-role round-1 kernel, exact): bit 1 = no
- * neighbour gathers, bit 2 = no stores (results wrong by design). */
-int mignn_diag_gcn_layer0(int mode, const int32_t* row_ptr, const int32_t* col, const float* ew,
-                          const float* pos, int64_t n, const float* coef, float* out,
-                          void* stream);
-
 int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img, float* out,
                         void* stream);
 
-/* EXPERIMENTAL (not used by FlowGNN): the fused GCN layer of
- * mignn_gcn_layer_f16x3 as a "tile ring" kernel (csrc/gcn_ring.hip): one
- * 4-wave workgroup per CU walks consecutive 64-row tiles with the previous /
- * current / next tile images in an LDS ring and the whole split W in AGPRs.
- * Same arguments and results contract as mignn_gcn_layer_f16x3, plus
- * seg_tiles (tiles per contiguous segment, 0 = one segment per workgroup).
- * Measured slower than the producer/consumer kernel. */
-int mignn_gcn_layer_ring(const int32_t* row_ptr, const int32_t* col, const float* ew,
+/* EXPERIMENTAL (round 3): the wave-independent split-fp16 GCN layer
+ * (csrc/gcn_wave.hip), same contract as mignn_gcn_layer_f16x3; variant selects
+ * the occupancy / gather-group / residual-timing instance (timing study). */
+int mignn_gcn_layer_wave(const int32_t* row_ptr, const int32_t* col, const float* ew,
                          const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
                          const float* w, const float* bias, const float* scale,
-                         const float* shift, int flags, float* out, int64_t ldo,
-                         int64_t seg_tiles, void* stream);
-/* Timeline buffer (uint64 [8 * 64 * 16]) for mignn_gcn_layer_ring: s_memtime
- * of wave 0 of workgroups 0..7 at the 10 phase boundaries of steps 0..63. */
-int mignn_diag_set_trace_ring(void* buf);
-/* on != 0: the eval aggregations (mignn_gcn/sum/gat/transformer_aggregate)
- * use the entry-at-a-time kernels instead of the batched ones (A/B timing;
- * results equal up to fp32 summation order).  Process-wide. */
-int mignn_diag_set_agg_legacy(int on);
+                         const float* shift, int flags, float* out, int64_t ldo, int variant,
+                         void* stream);
 #ifdef __cplusplus
 }
 #endif

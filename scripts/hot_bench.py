@@ -1,0 +1,121 @@
+"""Hot-kernel study (round 3): the fused split-fp16 GCN layer variants on the
+bench mesh (250x200x200 periodic hex, 10M nodes, the model's locality order),
+timed with HIP events in interleaved rounds, each checked against an fp64
+reference on sampled rows and against the producer/consumer kernel.
+Env: HB_H (128), HB_GRID, HB_VARIANTS (comma list of wave variants), HB_REPS."""
+import json
+import os
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "gnn-bfs-rans_amd"))
+import torch  # noqa: E402
+
+from mignn import _lib  # noqa: E402
+from mignn.gnn_model import build_csr, locality_order  # noqa: E402
+from mignn.synthetic import grid_graph  # noqa: E402
+
+dev = torch.device("cuda", 0)
+H = int(os.environ.get("HB_H", "128"))
+nx, ny, nz = (int(v) for v in os.environ.get("HB_GRID", "250,200,200").split(","))
+pos, ei = grid_graph(nx, ny, nz, device=dev, permute_seed=int(os.environ["HB_SHUFFLE"]) if os.environ.get("HB_SHUFFLE") else None)
+n = pos.shape[0]
+if os.environ.get("HB_ORDER", "1") == "1":
+    perm, inv = locality_order(pos, ei)
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv)
+else:
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
+del ei
+g = torch.Generator(device=dev).manual_seed(0)
+X = torch.randn(n, H, device=dev, generator=g)
+W = torch.randn(H, H, device=dev, generator=g) * 0.05
+b = torch.randn(H, device=dev, generator=g) * 0.05
+sc = torch.rand(H, device=dev, generator=g) + 0.5
+sh = torch.randn(H, device=dev, generator=g) * 0.1
+L = _lib.lib()
+P = _lib.ptr
+st = _lib.stream()
+FL = 15
+
+
+def old(Y):
+    _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                       P(W), P(b), P(sc), P(sh), FL, P(Y), H, st), "old")
+
+
+def wave(v):
+    def f(Y):
+        _lib.check(L.mignn_gcn_layer_wave(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                          P(W), P(b), P(sc), P(sh), FL, P(Y), H, v, st), "wave")
+    return f
+
+
+def copy(Y):
+    _lib.check(L.mignn_diag_gather(2, P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), n, nx, ny, nz, 0,
+                                   P(Y), st), "copy")
+
+
+variants = [int(v) for v in os.environ.get("HB_VARIANTS", "0,1,2,3").split(",") if v]
+cases = {"old_f16x3": old}
+if H == 128:          # mignn_diag_gather's copy is written for 128-float rows
+    cases["diag_copy"] = copy
+for v in variants:
+    cases[f"wave_v{v}"] = wave(v)
+res = {"grid": [nx, ny, nz], "H": H, "n": n}
+PMC = os.environ.get("HB_PMC") == "1"
+if PMC:                      # profiled passes: each case twice, nothing else
+    Y = torch.empty_like(X)
+    for _ in range(2):
+        for k, f in cases.items():
+            f(Y)
+    torch.cuda.synchronize()
+    print(json.dumps(res), flush=True)
+    sys.exit(0)
+outs = {k: torch.full_like(X, float("nan")) for k in cases}
+# ---- correctness: fp64 on sampled rows + cross-check vs the old kernel
+for k, f in cases.items():
+    f(outs[k])
+torch.cuda.synchronize()
+rows = torch.randint(0, n, (4096,), generator=torch.Generator().manual_seed(5))
+rp = csr.row_ptr.cpu().long()
+colc = csr.col.cpu().long()
+ewc = csr.ew.cpu().double()
+Xd = X.double()
+A = []
+for r in rows.tolist():
+    e = slice(int(rp[r]), int(rp[r + 1]))
+    A.append((ewc[e].to(dev)[:, None] * Xd[colc[e].to(dev)]).sum(0))
+A = torch.stack(A)
+rr = rows.to(dev)
+Yr = ((Xd[rr] + b.double() + A @ W.double().t()) * sc.double() + sh.double()).clamp_min(0)
+chk = {}
+for k in cases:
+    if k == "diag_copy":
+        continue
+    Y = outs[k]
+    chk[k] = {"vs_fp64_max": (Y[rr].double() - Yr).abs().max().item(),
+              "vs_old_max": (Y - outs["old_f16x3"]).abs().max().item(),
+              "nan_rows": int(torch.isnan(Y).any(1).sum().item())}
+res["check"] = chk
+res["ref_max"] = Yr.abs().max().item()
+del outs
+Y = torch.empty_like(X)
+reps = int(os.environ.get("HB_REPS", "5"))
+times = {k: [] for k in cases}
+for rnd in range(reps + 1):
+    for k, f in cases.items():
+        f(Y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            f(Y)
+        e1.record()
+        e1.synchronize()
+        if rnd > 0:
+            times[k].append(e0.elapsed_time(e1) / 3)
+res["ms"] = {k: round(statistics.median(v), 4) for k, v in times.items()}
+by = 4 * (2 * n * H + (n + 1) + int(csr.row_ptr[-1].item()) + n)
+res["frac_of_8TBps"] = {k: round(by / (v * 1e-3) / 8e12, 4) for k, v in res["ms"].items()}
+print(json.dumps(res), flush=True)

@@ -4,9 +4,10 @@ float64 torch restatement of the PyG message/aggregate steps on the same CSR.
 Graphs: random destination-major edge lists with degrees 0..20 and hub rows
 of 40-90 entries (several 8-entry batches per row, the batched kernels'
 online-softmax path), both CSR modes, and a row sub-range [rb, re) written at
-out + rb * ldo.  The batched kernels (default) and the entry-at-a-time
-kernels (mignn_diag_set_agg_legacy) are held to the same bound: fp32
-accumulation error relative to the sum of |terms| of each output.
+out + rb * ldo.  The batched kernels (4 heads, the FlowGNN widths) and the
+entry-at-a-time kernels (any other head count / width: h = 20 / 48 / 40
+below) are held to the same bound: fp32 accumulation error relative to the
+sum of |terms| of each output.
 """
 
 import math
@@ -27,8 +28,6 @@ def _gpu():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm GPU")
     _lib.lib()
-    yield
-    _lib.lib().mignn_diag_set_agg_legacy(0)
 
 
 def _graph(n, seed, hubs=True):
@@ -70,19 +69,14 @@ def _check(got, ref, mag, what, deg=None):
     assert not bool(bad.any()), (what, float(err.max()), float((err / bound).max()))
 
 
-def _run(legacy, fn):
-    _lib.lib().mignn_diag_set_agg_legacy(1 if legacy else 0)
-    try:
-        out = fn()
-        torch.cuda.synchronize()
-        return out
-    finally:
-        _lib.lib().mignn_diag_set_agg_legacy(0)
+def _run(fn):
+    out = fn()
+    torch.cuda.synchronize()
+    return out
 
 
-@pytest.mark.parametrize("legacy", [False, True])
 @pytest.mark.parametrize("h", [32, 64, 128, 256, 20])
-def test_sum_and_gcn_aggregate(h, legacy):
+def test_sum_and_gcn_aggregate(h):
     n = 3000
     ei = _graph(n, 11 + h)
     g = torch.Generator().manual_seed(h)
@@ -94,7 +88,7 @@ def test_sum_and_gcn_aggregate(h, legacy):
     csr = build_csr(ei, n, _lib.CSR_VERBATIM)
     col, dst = _edges(csr, n)
     out = torch.full((n, h), float("nan"), device=DEV)
-    _run(legacy, lambda: _lib.check(L.mignn_sum_aggregate(
+    _run(lambda: _lib.check(L.mignn_sum_aggregate(
         P(csr.row_ptr), P(csr.col), P(xd), h, 1.25, rb, re, h, P(out), h, _lib.stream(xd.device)), "sum"))
     xr = xd.double().cpu()
     ref = torch.zeros((n, h), dtype=torch.float64).index_add_(0, dst, xr[col]) + 1.25 * xr
@@ -106,7 +100,7 @@ def test_sum_and_gcn_aggregate(h, legacy):
     col, dst = _edges(csr, n)
     dinv = csr.dinv.cpu().double()
     out = torch.full((n, h), float("nan"), device=DEV)
-    _run(legacy, lambda: _lib.check(L.mignn_gcn_aggregate(
+    _run(lambda: _lib.check(L.mignn_gcn_aggregate(
         P(csr.row_ptr), P(csr.col), P(csr.dinv), P(xd), h, rb, re, h, P(out), h,
         _lib.stream(xd.device)), "gcn"))
     w = (dinv[col] * dinv[dst])[:, None]
@@ -115,9 +109,8 @@ def test_sum_and_gcn_aggregate(h, legacy):
     _check(out[rb:re].cpu(), ref[rb:re], mag[rb:re], f"gcn h={h}")
 
 
-@pytest.mark.parametrize("legacy", [False, True])
 @pytest.mark.parametrize("h", [32, 64, 128, 256, 48])
-def test_gat_aggregate(h, legacy):
+def test_gat_aggregate(h):
     n = 2500
     ei = _graph(n, 23 + h)
     csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
@@ -128,7 +121,7 @@ def test_gat_aggregate(h, legacy):
     L, P = _lib.lib(), _lib.ptr
     rb, re = 9, n - 100
     out = torch.full((n, HEADS * h), float("nan"), device=DEV)
-    _run(legacy, lambda: _lib.check(L.mignn_gat_aggregate(
+    _run(lambda: _lib.check(L.mignn_gat_aggregate(
         P(csr.row_ptr), P(csr.col), P(logits), P(x), h, rb, re, h, HEADS, 0.2, P(out), HEADS * h,
         _lib.stream(x.device)), "gat"))
     lg = logits.cpu().double()
@@ -144,9 +137,8 @@ def test_gat_aggregate(h, legacy):
            deg[rb:re])
 
 
-@pytest.mark.parametrize("legacy", [False, True])
 @pytest.mark.parametrize("h", [64, 128, 256, 40])
-def test_transformer_aggregate(h, legacy):
+def test_transformer_aggregate(h):
     n = 2500
     ei = _graph(n, 37 + h)
     csr = build_csr(ei, n, _lib.CSR_VERBATIM)
@@ -159,7 +151,7 @@ def test_transformer_aggregate(h, legacy):
     L, P = _lib.lib(), _lib.ptr
     rb, re = 33, n
     out = torch.full((n, K1), float("nan"), device=DEV)
-    _run(legacy, lambda: _lib.check(L.mignn_transformer_aggregate(
+    _run(lambda: _lib.check(L.mignn_transformer_aggregate(
         P(csr.row_ptr), P(csr.col), P(qt), K1, P(x), h, rb, re, h, HEADS, scale, P(out), K1,
         _lib.stream(x.device)), "tf"))
     q = qt.cpu().double()

@@ -10,6 +10,7 @@ arbitrary node ranges (shuffled order)."""
 import pytest
 import torch
 
+from helpers import khop_subgraph
 from mignn import FlowGNN
 from mignn.dist import FlowGNNShard, LocalExchange, build_local_layouts, range_bounds, sharded_forward
 from mignn.gnn_model import locality_order
@@ -85,3 +86,46 @@ def test_sharded_single_shard_is_plain_forward():
     ys, lays = _sharded(m, x, ei, 1, ordered=False)
     assert lays[0].n_ghost == 0 and lays[0].n_int == x.shape[0]
     assert torch.equal(ys, y)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_config4_gin_h256_l8_partitioned(P):
+    """configs[4]'s model (GIN, hidden 256, 8 layers) as the bench runs it at
+    N GPUs -- k-slab node ranges with a halo exchange per layer -- here as P
+    in-process FlowGNNShards of a 500 x 400 x 16 mesh (3.2M nodes; P = 8
+    gives each shard two k-planes and two ghost planes).  Must equal the
+    unsharded forward up to fp32 summation order, and the fp64 oracle on the
+    receptive field of a seeded row sample (helpers.khop_subgraph)."""
+    cfg = dict(hidden_dim=256, num_layers=8, layer_type="GIN")
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    sd = seeded_state_dict(m.state_dict(), seed=6)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    x, ei = grid_graph(500, 400, 16, device=DEV)
+    n = x.shape[0]
+    with torch.no_grad():
+        y = m(x, ei)
+    ys, lays = _sharded(m, x, ei, P)
+    plane = 500 * 400
+    assert all(l.n_ghost == 2 * plane for l in lays)
+    scale = max(1.0, y.abs().max().item())
+    err = (ys - y).abs().max().item()
+    g = torch.Generator().manual_seed(77 + P)
+    # seeds on the shard boundaries (first / last plane of each shard) and inside
+    b = range_bounds(n, P)
+    seeds = torch.cat([torch.tensor([b[r], b[r + 1] - 1]) for r in range(P)]
+                      + [torch.randint(0, n, (8,), generator=g)]).unique().to(DEV)
+    nodes, sub = khop_subgraph(ei, n, seeds, cfg["num_layers"])
+    xs, subc = x[nodes].cpu(), sub.cpu()
+    got = ys[seeds].cpu().double()
+    del y, ys
+    torch.cuda.empty_cache()
+    r64 = orc.flowgnn_forward(sd, cfg, xs, subc, None, dtype=torch.float64)[:seeds.numel()]
+    r32 = orc.flowgnn_forward(sd, cfg, xs, subc, None, dtype=torch.float32)[:seeds.numel()]
+    e64 = (got - r64).abs().max().item()
+    ref = (r32.double() - r64).abs().max().item()
+    print(f"GIN H256 L8 P={P}: {n} nodes, interior {[l.n_int for l in lays]}, "
+          f"max|sharded-unsharded| {err:.2e} (|y| <= {scale:.2f}), max|sharded-fp64| {e64:.2e} "
+          f"on {seeds.numel()} rows ({nodes.numel()}-node field), fp32 oracle {ref:.2e}")
+    assert err <= 2e-6 * scale
+    assert e64 <= max(1e-5, 2.0 * ref)

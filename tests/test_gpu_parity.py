@@ -323,7 +323,7 @@ def test_mlp_head_rejects_bad_shapes():
 
 
 # ------------------------------------------------------------------ locality order
-def _pencil_order_np(nx, ny, nz):
+def _block_panel_order_np(nx, ny, nz):
     """numpy restatement of the locality key on the natural grid labels:
     4x4x4-cell blocks in panels of 4x4 block columns swept along z
     (csrc/reorder.hip order_keys_kernel)."""
@@ -346,7 +346,7 @@ def test_locality_order_grid(dims):
     p = perm.cpu().numpy()
     assert np.array_equal(np.sort(p), np.arange(n))
     assert np.array_equal(inv.cpu().numpy()[p], np.arange(n))
-    assert np.array_equal(p, _pencil_order_np(*dims))
+    assert np.array_equal(p, _block_panel_order_np(*dims))
 
 
 def test_locality_order_shuffled_and_degenerate():
