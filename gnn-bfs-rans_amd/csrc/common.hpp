@@ -164,7 +164,7 @@ int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const
 int gcn_fused_layer(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                     int64_t ldx, int64_t rb, int64_t re, int h, const float* w, const float* bias,
                     const float* scale, const float* shift, int flags, float* out, int64_t ldo,
-                    void* stream);
+                    void* stream, int xm = 0);
 int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, int n,
                 const float* bias, const float* residual, int64_t ldr, const float* scale,
                 const float* shift, int flags, float* c, int64_t ldc, hipStream_t st,

@@ -100,6 +100,84 @@ __global__ __launch_bounds__(256) void diag_gather_kernel(
     }
 }
 
+// mode 16 | D: the fused layer's streaming skeleton -- one 4-wave block per
+// CU, persistent over 64-row tiles (XCD-contiguous order), own rows LDS-DMA'd
+// D-1 steps ahead into a ring of D images, each wave copies its 16 rows out
+// of the image in the accumulator store pattern (16 rows x 64 B, non-temporal)
+__device__ __forceinline__ void dma16_diag(const void* src, uint32_t dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(__builtin_amdgcn_readfirstlane(static_cast<int>(dst)))
+        : "memory");
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void diag_stream_kernel(const float* __restrict__ x, int64_t n,
+                                                             float* __restrict__ out) {
+    constexpr int H = 128, BM = 64, ROWB = 512, XB = BM * ROWB, NPIECE = XB / 1024 / 4;
+    constexpr int NST = 8;
+    // vmcnt(N) lgkmcnt(0) at the end of step s: ops younger than step s+1's
+    // DMA = the stores of steps s-D+2 .. s and the DMAs of steps s+2 .. s+D-1
+    constexpr int N = (D - 1) * NST + (D - 2) * NPIECE;
+    constexpr int WAIT = (N & 15) | ((N >> 4) << 14) | (7 << 4);
+    __shared__ __attribute__((aligned(16))) unsigned char lds[D * XB];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t ntiles = n / BM;                   // host: n % 64 == 0
+    const int G = gridDim.x;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = G >> 3;
+    const int64_t nsteps = (ntiles + G - 1) / G;
+    const int64_t chunk = nsteps * per_xcd;
+    auto tile_of = [&](int64_t s) -> int64_t { return (int64_t)xcd * chunk + s * per_xcd + slot; };
+    auto issue = [&](int64_t s) {
+        int64_t t = tile_of(s);
+        if (s >= nsteps || t >= ntiles) t = 0;        // keep the op count uniform
+        unsigned char* const X = lds + (s % D) * XB;
+#pragma unroll
+        for (int pc = 0; pc < NPIECE; ++pc) {
+            const int piece = wave * NPIECE + pc;
+            const int lr = piece * 2 + lane / 32;
+            const int pos = lane % 32;
+            dma16_diag(x + (t * BM + lr) * H + 4 * (pos ^ (lr & 15)), static_cast<uint32_t>(
+                reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) void*)(X + piece * 1024))));
+        }
+    };
+    for (int d = 0; d < D - 1; ++d) issue(d);
+    __builtin_amdgcn_s_waitcnt(0x70);
+    __builtin_amdgcn_s_barrier();
+    for (int64_t s = 0; s < nsteps; ++s) {
+        issue(s + D - 1);
+        const int64_t t = tile_of(s);
+        const unsigned char* const X = lds + (s % D) * XB;
+        const int lr = 16 * wave + r;
+        f32x4 v[8];
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb)
+            v[nb] = *reinterpret_cast<const f32x4*>(X + lr * ROWB + 16 * ((4 * nb + g) ^ (lr & 15)));
+        if (t < ntiles) {
+#pragma unroll
+            for (int nb = 0; nb < 8; ++nb)
+                __builtin_nontemporal_store(v[nb], reinterpret_cast<f32x4*>(out + (t * BM + lr) * H + 16 * nb + 4 * g));
+        } else {
+#pragma unroll
+            for (int nb = 0; nb < 8; ++nb)
+                __builtin_nontemporal_store(v[nb], reinterpret_cast<f32x4*>(out + lr * H + 16 * nb + 4 * g));
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(WAIT);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_s_waitcnt(0x70);
+}
+
 }  // namespace
 }  // namespace mignn
 
@@ -112,6 +190,15 @@ extern "C" int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t
     const int g = blocks > 0 ? blocks : static_cast<int>(grid_for(n * 32, 256, 1 << 20));
 #define MIGNN_DIAG(M, R, T) \
     hipLaunchKernelGGL((diag_gather_kernel<M, R, T>), dim3(g), dim3(256), 0, st, row_ptr, col, ew, x, n, nx, ny, nz, out)
+    if (mode >= 16) {
+        MIGNN_REQUIRE(n % 64 == 0 && blocks > 0 && blocks % 8 == 0, "diag stream: n % 64, blocks % 8");
+        const int d = mode & 15;
+        if (d == 2) hipLaunchKernelGGL((diag_stream_kernel<2>), dim3(blocks), dim3(256), 0, st, x, n, out);
+        else if (d == 3) hipLaunchKernelGGL((diag_stream_kernel<3>), dim3(blocks), dim3(256), 0, st, x, n, out);
+        else if (d == 4) hipLaunchKernelGGL((diag_stream_kernel<4>), dim3(blocks), dim3(256), 0, st, x, n, out);
+        else { set_error("diag stream: depth 2..4"); return MIGNN_ERR_ARG; }
+        return launch_status("diag_stream_kernel");
+    }
     const int base = mode & 3;
     const bool remap = mode & 4, nt = mode & 8;
     if (remap && blocks > 0) { set_error("diag: remap needs a full grid"); return MIGNN_ERR_ARG; }

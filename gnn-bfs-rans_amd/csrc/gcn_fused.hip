@@ -23,11 +23,11 @@
 //   4. split: the row's 4 lanes agree on 2^p (row max in [2^13, 2^14)),
 //      a 2^p = hi + lo in fp16 -- already the MFMA B fragments;
 //   5. transform: D[n][row] = W'.agg^T, three 16x16x32 MFMAs per block
-//      (hi.hi + hi.lo + lo.hi); W' = diag(BN scale) W split once per launch:
-//      the hi fragments in registers, the lo fragments in LDS;
+//      (hi.hi + hi.lo + lo.hi); W' = diag(BN scale) W split once per launch
+//      into fragments held in LDS;
 //   6. epilogue from the accumulators (row r, columns 16 nb + 4 g + i):
 //      out = relu(acc 2^-(p+q) + x sc + (b sc + shift)), residual x from the
-//      image, staged through the wave's LDS tile and stored as whole rows.
+//      image, 16-B stores (16 rows x 64 B per instruction).
 // One block barrier per step (the image buffers change hands); everything
 // else is per wave.
 //
@@ -62,9 +62,8 @@ struct FCfg {
     static constexpr int EX = 3;                      // out-of-tile rows per row in registers
     static constexpr int OFF_X = 0;                   // two images
     static constexpr int OFF_ZERO = 2 * X_BYTES;      // a zero row
-    static constexpr int OFF_WLO = OFF_ZERO + ROWB;   // W' lo fragments [kc][nb]
-    static constexpr int OFF_STG = OFF_WLO + KC * NB * FRAG;   // per-wave output staging
-    static constexpr int OFF_TA = OFF_STG + NW * RW * ROWB;    // residual multiplier per column
+    static constexpr int OFF_W = OFF_ZERO + ROWB;     // W' fragments [kc][nb][hi, lo]
+    static constexpr int OFF_TA = OFF_W + KC * NB * 2 * FRAG;  // residual multiplier per column
     static constexpr int OFF_TB = OFF_TA + H * 4;              // additive term per column
     static constexpr int OFF_Q = OFF_TB + H * 4;               // exponent per column block
     // CSR tables of a wave's 16 rows (two steps: the one summed, the next):
@@ -76,7 +75,7 @@ struct FCfg {
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     static constexpr int NPIECE = X_BYTES / 1024 / NW;   // LDS-DMA pieces per wave per tile
     static constexpr int RPP = 1024 / ROWB;              // rows per 1-KB piece
-    static constexpr int NST = RW * ROWB / 1024;         // row stores per wave per tile
+    static constexpr int NST = NB;                       // row stores per wave per tile
 };
 
 __device__ __attribute__((aligned(16))) float g_zero_row_f[256];
@@ -122,7 +121,8 @@ __device__ __forceinline__ void step_barrier() {
     asm volatile("" ::: "memory");
 }
 
-template <int H>
+// XM (experiments): 1 no table build, 2 no out-of-tile gather, 4 no in-tile sum
+template <int H, int XM = 0>
 __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t rb,
@@ -179,7 +179,6 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
         atomicMax(&QM[nb], m);
     }
     __syncthreads();
-    // hi fragments -> the (still free) image area, lo fragments -> OFF_WLO
     for (int task = tid; task < NTASK; task += C::NT) {
         float v[8];
         const int nb = wvals(task, v);
@@ -193,18 +192,10 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
             lv[j] = static_cast<_Float16>(s - static_cast<float>(hh));
         }
         const int fb = task >> 6, ln = task & 63;
-        *reinterpret_cast<f16x8*>(lds + C::OFF_X + fb * C::FRAG + ln * 16) = hv;
-        *reinterpret_cast<f16x8*>(lds + C::OFF_WLO + fb * C::FRAG + ln * 16) = lv;
+        *reinterpret_cast<f16x8*>(lds + C::OFF_W + (2 * fb) * C::FRAG + ln * 16) = hv;
+        *reinterpret_cast<f16x8*>(lds + C::OFF_W + (2 * fb + 1) * C::FRAG + ln * 16) = lv;
     }
     __syncthreads();
-    f16x8 wh[C::KC][C::NB];          // W' hi fragments, in registers for the launch
-#pragma unroll
-    for (int kc = 0; kc < C::KC; ++kc)
-#pragma unroll
-        for (int nb = 0; nb < C::NB; ++nb)
-            wh[kc][nb] = *reinterpret_cast<const f16x8*>(lds + C::OFF_X +
-                                                          (kc * C::NB + nb) * C::FRAG + lane * 16);
-    __syncthreads();                 // the image area is the images' from here on
     if (tid < C::NB) QM[tid] = static_cast<uint32_t>(fexp(QM[tid]));
 
     // ---------------------------------------------------------------- schedule
@@ -363,7 +354,6 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
 
     const bool relu = (flags & MIGNN_EPI_RELU) != 0;
     const bool res_on = (flags & MIGNN_EPI_RESIDUAL) != 0;
-    unsigned char* const stg = lds + C::OFF_STG + wave * C::RW * C::ROWB;
     for (int64_t s = 0; s < nsteps; ++s) {
         const bool vs = valid(s);
         const int64_t t0 = rb + tile_of(s) * C::BM;
@@ -387,14 +377,15 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
                     for (int i = 0; i < 4; ++i) agg[h][i] = fmaf(xw[k], xe[k][h][i], agg[h][i]);
         }
         // ---- 2. step s+1: tables and out-of-tile rows; CSR of s+2, s+3
-        build(s + 1, rpv1, en1, maxd_n, slow_n);
-        gather_ext(s + 1, xe);
+        if constexpr (!(XM & 1)) build(s + 1, rpv1, en1, maxd_n, slow_n);
+        else { maxd_n = 7; slow_n = false; }
+        if constexpr (!(XM & 2)) gather_ext(s + 1, xe);
         load_ent(rpv2, en1);
         rpv1 = rpv2;
         rpv2 = load_rpv(s + 3);
         // ---- 3. in-tile entries of step s from the image (CSR order)
         unsigned char* const X = lds + C::OFF_X + (s & 1) * C::X_BYTES;
-        if (!slow_c) {
+        if (!slow_c && !(XM & 4)) {
             const int xoff = C::OFF_X + static_cast<int>(s & 1) * C::X_BYTES;
 #pragma unroll
             for (int e = 0; e < S; ++e) {
@@ -417,7 +408,8 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
 #pragma unroll
                     for (int i = 0; i < 4; ++i) agg[h][i] = fmaf(w, v[h][i], agg[h][i]);
             }
-        } else if (vs) {
+        }
+        else if (vs && !(XM & 4)) {
             // general path (rows with > S entries or > EX out-of-tile ones):
             // every entry of the lane's row, one at a time, CSR order
             const int64_t row = t0 + 16 * wave + r;
@@ -473,8 +465,8 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
 #pragma unroll
         for (int nb = 0; nb < C::NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
         int wofs = lane * 16;
-        asm volatile("" : "+v"(wofs));            // lo fragments re-read per step
-        const unsigned char* const wlo = lds + C::OFF_WLO + wofs;
+        asm volatile("" : "+v"(wofs));            // fragments re-read per step
+        const unsigned char* const wf = lds + C::OFF_W + wofs;
 #pragma unroll
         for (int kc = 0; kc < C::KC; ++kc) {
             f16x8 bh, bl;
@@ -487,16 +479,19 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
             }
 #pragma unroll
             for (int nb = 0; nb < C::NB; ++nb) {
-                const f16x8 wl = *reinterpret_cast<const f16x8*>(wlo + (kc * C::NB + nb) * C::FRAG);
-                acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc][nb], bh, acc[nb], 0, 0, 0);
-                acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc][nb], bl, acc[nb], 0, 0, 0);
+                const int fb = kc * C::NB + nb;
+                const f16x8 wh = *reinterpret_cast<const f16x8*>(wf + (2 * fb) * C::FRAG);
+                const f16x8 wl = *reinterpret_cast<const f16x8*>(wf + (2 * fb + 1) * C::FRAG);
+                acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[nb], 0, 0, 0);
+                acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, acc[nb], 0, 0, 0);
                 acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, acc[nb], 0, 0, 0);
             }
         }
         // ---- 6. epilogue: residual from the image (own row 16 w + r), BN,
-        // ReLU -> the wave's staging tile (row r, chunk c at c ^ r) -> rows out
+        // ReLU, 16-B stores
         {
             const int lr = 16 * wave + r;
+            const int64_t grow = t0 + lr;
             int eofs = 16 * g;
             asm volatile("" : "+v"(eofs));
 #pragma unroll
@@ -514,19 +509,8 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
                     if (relu) v = v < 0.0f ? 0.0f : v;
                     o[i] = v;
                 }
-                *reinterpret_cast<f32x4*>(stg + r * C::ROWB + 16 * (ch ^ r)) = o;
-            }
-            // whole rows: instruction i stores rows RPP i .. (a wave's LDS
-            // operations execute in order: its staged writes are visible)
-            constexpr int LPR = C::NCH;              // lanes per row
-#pragma unroll
-            for (int i = 0; i < C::NST; ++i) {
-                const int rr = C::RPP * i + lane / LPR;
-                const int chn = lane % LPR;
-                const f32x4 v = *reinterpret_cast<const f32x4*>(stg + rr * C::ROWB + 16 * (chn ^ rr));
-                const int64_t grow = t0 + 16 * wave + rr;
                 if (vs && grow < re)
-                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + grow * ldo + 4 * chn));
+                    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + grow * ldo + 4 * ch));
             }
         }
         // the next image (DMA'd this step), the out-of-tile rows and CSR
@@ -540,7 +524,7 @@ __global__ __launch_bounds__(FCfg<H>::NT, 1) void gcn_fused_kernel(
     }
 }
 
-template <int H>
+template <int H, int XM>
 int launch_fused(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                  int64_t ldx, int64_t rb, int64_t re, const float* w, const float* bias,
                  const float* scale, const float* shift, int flags, float* out, int64_t ldo,
@@ -559,7 +543,7 @@ int launch_fused(const int32_t* row_ptr, const int32_t* col, const float* ew, co
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL((gcn_fused_kernel<H>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x,
+    hipLaunchKernelGGL((gcn_fused_kernel<H, XM>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x,
                        ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
     return launch_status("gcn_fused_kernel");
 }
@@ -569,12 +553,17 @@ int launch_fused(const int32_t* row_ptr, const int32_t* col, const float* ew, co
 int gcn_fused_layer(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                     int64_t ldx, int64_t rb, int64_t re, int h, const float* w, const float* bias,
                     const float* scale, const float* shift, int flags, float* out, int64_t ldo,
-                    void* stream) {
+                    void* stream, int xm) {
     hipStream_t st = as_stream(stream);
-    return h == 128 ? launch_fused<128>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
-                                        flags, out, ldo, st)
-                    : launch_fused<64>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
-                                       flags, out, ldo, st);
+#define MIGNN_FUSED(XM) \
+    return h == 128 ? launch_fused<128, XM>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, \
+                                            flags, out, ldo, st) \
+                    : launch_fused<64, XM>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, \
+                                           flags, out, ldo, st)
+    if (xm == 7) MIGNN_FUSED(7);
+    if (xm == 3) MIGNN_FUSED(3);
+    MIGNN_FUSED(0);
+#undef MIGNN_FUSED
 }
 
 }  // namespace mignn

@@ -430,9 +430,9 @@ extern "C" int mignn_gcn_layer_wave(const int32_t* row_ptr, const int32_t* col, 
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gcn_layer_wave: affine");
     MIGNN_REQUIRE(x != out, "gcn_layer_wave: in-place not supported (neighbours read x)");
     if (re == rb) return MIGNN_OK;
-    if (variant == 10)    // the fused tile kernel (gcn_fused.hip)
+    if (variant >= 10 && variant < 20)    // the fused tile kernel (gcn_fused.hip)
         return gcn_fused_layer(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift, flags,
-                               out, ldo, stream);
+                               out, ldo, stream, variant - 10);
     hipStream_t st = as_stream(stream);
 #define MIGNN_WAVE(HH, WPS, GRP, LR, ...) \
     return launch_wave<HH, WPS, GRP, LR, ##__VA_ARGS__>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, \

@@ -59,8 +59,17 @@ def copy(Y):
 
 variants = [int(v) for v in os.environ.get("HB_VARIANTS", "0,1,2,3").split(",") if v]
 cases = {"old_f16x3": old}
+def stream(d, blocks):
+    def f(Y):
+        _lib.check(L.mignn_diag_gather(16 | d, P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), n, nx, ny,
+                                       nz, blocks, P(Y), st), "stream")
+    return f
+
+
 if H == 128:          # mignn_diag_gather's copy is written for 128-float rows
     cases["diag_copy"] = copy
+    for d in [int(v) for v in os.environ.get("HB_STREAM", "").split(",") if v]:
+        cases[f"stream_d{d}"] = stream(d, 256)
 for v in variants:
     cases[f"wave_v{v}"] = wave(v)
 res = {"grid": [nx, ny, nz], "H": H, "n": n}
@@ -92,7 +101,8 @@ rr = rows.to(dev)
 Yr = ((Xd[rr] + b.double() + A @ W.double().t()) * sc.double() + sh.double()).clamp_min(0)
 chk = {}
 for k in cases:
-    if k == "diag_copy":
+    if k == "diag_copy" or k.startswith("stream"):
+        chk[k] = {"copy_exact": bool(torch.equal(outs[k], X))}
         continue
     Y = outs[k]
     chk[k] = {"vs_fp64_max": (Y[rr].double() - Yr).abs().max().item(),
