@@ -21,12 +21,12 @@
 //
 // Structure: one 12-wave workgroup per CU, persistent over 64-row tiles,
 // XCD-aware tile order (as tile_gemm.hip), one barrier per tile step.
-//   * Own-row image (2 buffers; 3 in the records mode and the diagnostic
-//     MIGNN_SCHED_UNSTAGED form): a tile's rows x[t0, t0+64) are copied
+//   * Own-row image (2 buffers): a tile's rows x[t0, t0+64) are copied
 //     HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) issued by the consumer
-//     waves one step ahead (two with 3 buffers), unpadded, 16-B chunks
-//     XOR-swizzled by (row & 7) on the SOURCE address.  With a locality order (mignn_locality_order:
-//     Morton curve) ~70 % of a mesh's CSR entries point inside their tile.
+//     waves one step ahead, unpadded, 16-B chunks XOR-swizzled by (row & 7)
+//     on the SOURCE address.  In the locality order (mignn_locality_order:
+//     4x4x4-cell blocks, one per 64-row tile, in panels of 4x4 block columns)
+//     ~75 % of a mesh's CSR entries point inside their tile.
 //   * 8 producer waves, 8 rows each (two quads of 4 rows; a row = 16 lanes x
 //     32 B).  Per tile, vectorised over the wave's CSR entries (lane = entry),
 //     two lookup tables are built in LDS: in-tile entries -> {image address,
@@ -40,17 +40,19 @@
 //   * 4 consumer waves (one per SIMD), 32 output columns each, split W held in
 //     registers for the whole launch.  (residual + bias) * 2^(p_row + q_w)
 //     seeds the accumulator, 3 MFMAs per 16x16x32 block, epilogue (unscale,
-//     BN affine, ReLU) from the accumulators into an LDS staging tile (the
-//     third image buffer's space), then whole rows out: a half-wave stores
+//     BN affine, ReLU) from the accumulators into an LDS staging tile, then
+//     whole rows out: a half-wave stores
 //     one 512-B row (H = 128) -- the accumulator layout would store 16 rows x
 //     64 B per instruction, measured 1.5x slower as a plain copy
 //     (profiles/r02_kbench_store_patterns.json) and 2 % (H = 128) / 9 %
 //     (H = 64) slower in this kernel.
 //   * Hand-offs (LDS counters, relaxed: a wave's LDS operations execute in
 //     order): consumers bump cntX once they hold their residual -- then the
-//     own-row buffer takes the tile three steps on; they bump cntA once their
+//     own-row buffer takes the tile two steps on; they bump cntA once their
 //     MFMAs have read the (single) A image -- then producers may write the
-//     next tile's rows into it.
+//     next tile's rows into it; cntS once their blocks are staged.  Every
+//     spin is bounded: one that runs out sets the device error word
+//     (mignn_device_errors) instead of falling through silently.
 #include <type_traits>
 
 #include "common.hpp"
@@ -62,11 +64,11 @@ using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 using f16x4 = __attribute__((ext_vector_type(4))) _Float16;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-// STG: two own-row image buffers (the own rows DMA'd one step ahead) and an
-// output staging tile in the LDS they free: the consumers write their
-// accumulator blocks there and store whole rows (512 B per half-wave at
-// H = 128) instead of 16 rows x 64 B per instruction
-template <int H, bool STG = false>
+// two own-row image buffers (the own rows DMA'd one step ahead) and an output
+// staging tile: the consumers write their accumulator blocks there and store
+// whole rows (512 B per half-wave at H = 128) instead of 16 rows x 64 B per
+// instruction
+template <int H>
 struct SCfg {
     static_assert(H == 64 || H == 128, "f16x3 GCN layer: H in {64, 128}");
     static constexpr int BM = 64;                  // rows per tile
@@ -97,12 +99,12 @@ struct SCfg {
     static constexpr int LPR = 64 / RPP;           // lanes per row in a piece
     static constexpr int NPIECE = BM / RPP;        // pieces per tile
     static constexpr int NPC = NPIECE / NCW;       // DMA pieces per consumer per tile
-    static constexpr int XBUF = STG ? 2 : 3;       // own-row image buffers
+    static constexpr int XBUF = 2;                 // own-row image buffers
     static constexpr int X_BYTES = BM * ROWB;
     static constexpr int A_BYTES = BM * AS * 2;
-    // Xs[3] | zero row | Ah | Al | rexp[BM] | tables[2][NPW] | epi | counters
-    // (own-image rows and the zero row sit at ROWB multiples: an image address
-    // is P ^ chunk offset, see the producer)
+    // Xs[2] | zero row | Ah | Al | rexp[BM] | tables[2][NPW] | epi | counters |
+    // staging tile (own-image rows and the zero row sit at ROWB multiples: an
+    // image address is P ^ chunk offset, see the producer)
     static constexpr int OFF_ZERO = XBUF * X_BYTES;
     static constexpr int OFF_AH = OFF_ZERO + ROWB;
     static constexpr int OFF_AL = OFF_AH + A_BYTES;
@@ -110,19 +112,10 @@ struct SCfg {
     static constexpr int OFF_TAB = OFF_REXP + BM * 4;
     static constexpr int OFF_EPI = OFF_TAB + 2 * NPW * TAB_BYTES;   // bias | scale | shift [H]
     static constexpr int OFF_CNT = OFF_EPI + 3 * H * 4;             // cntX, cntA, cntS
-    static constexpr int OFF_CNT2 = OFF_CNT + 16;                    // cntP, cntD, cntR
-    static constexpr int OFF_STG = OFF_CNT2 + 16;                    // STG: [BM][ROWB]
-    static constexpr int LDS_BYTES = OFF_STG + (STG ? BM * ROWB : 0);
-    static constexpr int NSTG = BM * ROWB / 1024 / NCW;             // STG row stores per consumer
+    static constexpr int OFF_STG = OFF_CNT + 16;                     // [BM][ROWB]
+    static constexpr int LDS_BYTES = OFF_STG + BM * ROWB;
+    static constexpr int NSTG = BM * ROWB / 1024 / NCW;             // row stores per consumer
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-    // records mode (layer 1 from layer-0 records, gcn_layer0.hip): the
-    // expansion coefficients [H][8] after everything else
-    static constexpr int OFF_COEF = LDS_BYTES;
-    static constexpr int LDS_BYTES_REC = OFF_COEF + H * 32;
-    static_assert(LDS_BYTES_REC <= 160 * 1024, "LDS budget (records mode)");
-    static constexpr int CPL = H / 4;              // consumer expansion: lanes per row (16-B chunk each)
-    static constexpr int RG = 64 / CPL;            // rows per expansion instruction
-    static constexpr int RPL = 16 / RG;            // rows per lane (a consumer expands 16 rows)
     static_assert(NPIECE % NCW == 0, "DMA pieces per consumer");
     static_assert(NQD == 2, "two row quads per producer wave");
     static_assert(PROWS * LTS % 2 == 0 && PROWS * LTS / 2 <= 64 && PROWS * ETS <= 64, "tables");
@@ -182,33 +175,6 @@ __device__ __forceinline__ f32x4 mfma16x16x32h(f16x8 a, f16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// Records mode: a layer-0 output element from its row's record r[0..6] (the
-// layer-0 aggregates c_i | C_i | s_i, gcn_layer0.hip) and its column's
-// coefficients ca | cb (cb[3] = the bias e): relu(e + sum_k coef_k r_k) in
-// gcn_layer0_kernel's fma order -- bit-identical to the materialised row.
-__device__ __forceinline__ float expand1(const f32x4& ca, const f32x4& cb, const f32x4& ra,
-                                         const f32x4& rb) {
-    float t = cb[3];
-    t = fmaf(ca[0], ra[0], t);
-    t = fmaf(ca[1], ra[1], t);
-    t = fmaf(ca[2], ra[2], t);
-    t = fmaf(ca[3], ra[3], t);
-    t = fmaf(cb[0], rb[0], t);
-    t = fmaf(cb[1], rb[1], t);
-    t = fmaf(cb[2], rb[2], t);
-    return t < 0.f ? 0.f : t;
-}
-
-// lanes B .. B + 6 of each 16-lane row broadcast to the whole row (DPP
-// row_newbcast, VALU): a record held one element per lane
-template <int B>
-__device__ __forceinline__ void row_bcast7(int v, f32x4& ra, f32x4& rb) {
-#define MIGNN_BC(e) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(v, 0x150 + B + (e), 0xf, 0xf, false))
-    ra = f32x4{MIGNN_BC(0), MIGNN_BC(1), MIGNN_BC(2), MIGNN_BC(3)};
-    rb = f32x4{MIGNN_BC(4), MIGNN_BC(5), MIGNN_BC(6), 0.f};
-#undef MIGNN_BC
-}
-
 // 32-bit LDS address of a pointer into the kernel's LDS array
 __device__ __forceinline__ uint32_t lds_addr(const unsigned char* p) {
     return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)(p)));
@@ -243,7 +209,22 @@ __device__ __forceinline__ void block_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// relaxed LDS counter: bump / bounded spin until >= target
+}  // namespace
+
+// the device error word (mignn_device_errors)
+__device__ unsigned int g_device_errors = 0u;
+
+namespace {
+
+__device__ __forceinline__ void device_error(unsigned int code) {
+    __hip_atomic_fetch_or(&g_device_errors, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// relaxed LDS counter: bump / bounded spin until >= target.  A spin that runs
+// out (2^22 polls, ~0.1 s: a hand-off that never came) records
+// MIGNN_DEVERR_SPIN in the device error word -- the launch still drains (every
+// wave reaches every barrier), its output is flagged wrong by
+// mignn_device_errors() instead of passing silently
 __device__ __forceinline__ void lds_bump(int* c) {
     asm volatile("" ::: "memory");
     __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -251,10 +232,15 @@ __device__ __forceinline__ void lds_bump(int* c) {
 }
 __device__ __forceinline__ void lds_wait(int* c, int target) {
     asm volatile("" ::: "memory");
+    bool ok = false;
     for (int it = 0; it < (1 << 22); ++it) {
-        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+        if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
+            ok = true;
+            break;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
+    if (!ok) device_error(MIGNN_DEVERR_SPIN);
     asm volatile("" ::: "memory");
 }
 
@@ -292,39 +278,19 @@ __device__ __forceinline__ void p_load_entries(PIdx& t, const int32_t* __restric
     t.ew = lane < ne ? ew[e0 + lane] : 0.f;
 }
 
-// REC: layer 1 from layer-0 records -- x rows are not read from HBM but
-// expanded from rec (8 floats per node) with coef8 ([H][8], copied to LDS)
-// on the fly, all by the producers: the own rows of tile s+2 into the image
-// at the end of step s (their records gathered at its start), the
-// out-of-tile rows in registers next to their gathered records.
-// DEC (with STG; EXPERIMENTAL, diagnostic flag MIGNN_SCHED_DECOUPLED): no
-// block barrier per step -- the hand-offs are LDS counters only (cntP:
-// producers finished a tile's A image / own-row reads; cntD: a consumer's
-// own-row DMA landed; cntR: staging tile read), so the producers' table /
-// gather phase of the next tile overlaps the consumers' epilogue.  1-2 %
-// faster on the 10M locality-ordered mesh and correct there, but it gave
-// wrong rows in a 1M natural-order model test (slow-path tiles): not the
-// default until that hand-off is found.  Every wait is a bounded spin.
-// UBT: in-tile entries per LDS batch of the producers' finish pass (0: SCfg::UB)
-template <int H, bool REC, bool STG, bool DEC = false, int UBT = 0>
+template <int H>
 __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t row_begin,
     int64_t row_end, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift, int flags,
-    float* __restrict__ out, int64_t ldo, const float* __restrict__ rec,
-    const float* __restrict__ coef8, unsigned long long* trace) {
-    static_assert(!(REC && STG), "records mode keeps three image buffers");
-    static_assert(!DEC || STG, "counter hand-offs need the staged form");
-    using C = SCfg<H, STG>;
-    constexpr int UBE = UBT ? UBT : C::UB;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[REC ? C::LDS_BYTES_REC : C::LDS_BYTES];
+    float* __restrict__ out, int64_t ldo, unsigned long long* trace) {
+    using C = SCfg<H>;
+    constexpr int UBE = C::UB;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
     int* const cntX = reinterpret_cast<int*>(lds + C::OFF_CNT);
     int* const cntA = cntX + 1;
     int* const cntS = cntX + 2;
-    int* const cntP = reinterpret_cast<int*>(lds + C::OFF_CNT2);
-    int* const cntD = cntP + 1;
-    int* const cntR = cntP + 2;
     _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
     _Float16* const AL = reinterpret_cast<_Float16*>(lds + C::OFF_AL);
     int* const REXP = reinterpret_cast<int*>(lds + C::OFF_REXP);
@@ -350,7 +316,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     const int64_t chunk = chunks ? nsteps * per_xcd : per_xcd;
     const int64_t sstride = chunks ? per_xcd : G;
     auto tile_of = [&](int64_t s) -> int64_t { return (int64_t)xcd * chunk + s * sstride + slot; };
-    // own-row image buffer of a tile of this workgroup: (its step index) mod 3
+    // own-row image buffer of a tile of this workgroup: (its step index) mod 2
     auto xbuf_of = [&](int64_t tile) -> int {
         return static_cast<int>(((tile - (int64_t)xcd * chunk) / sstride) % C::XBUF);
     };
@@ -359,9 +325,6 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         cntX[0] = 0;
         cntA[0] = 0;
         cntS[0] = 0;
-        cntP[0] = 0;
-        cntD[0] = 0;
-        cntR[0] = 0;
     }
 
     // static wave priority (diagnostic schedules): consumers or producers
@@ -378,9 +341,6 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         // zero row (read by the empty slots of the in-tile pass)
         for (int i = lane_ + pw * 64; i < C::ROWB / 4; i += C::NPW * 64)
             reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
-        if constexpr (REC)   // the expansion coefficients -> LDS (read after the first barrier)
-            for (int i = lane_ + pw * 64; i < H * 8; i += C::NPW * 64)
-                reinterpret_cast<float*>(lds + C::OFF_COEF)[i] = coef8[i];
         // lookup tables of tile parity tb: LT [PROWS][LTS] {P, w}, ET [PROWS][ETS] {col, w}
         auto LTb = [&](int tb) { return lds + C::OFF_TAB + (tb * C::NPW + pw) * C::TAB_BYTES; };
         auto ETb = [&](int tb) { return LTb(tb) + C::PROWS * C::LTS * 8; };
@@ -395,62 +355,6 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         uint32_t coff[C::CH];                         // byte offset of my chunks in a row
 #pragma unroll
         for (int j = 0; j < C::CH; ++j) coff[j] = static_cast<uint32_t>((c0 + 16 * j) << 4);
-        // REC: coefficients of columns 4 ch .. 4 ch + 3 from the LDS table
-        // (re-read per use: 64 registers for all of a lane's columns would
-        // spill; a global load issued after the out-of-tile gathers would make
-        // every wait for it drain them)
-        auto load_pc = [&](int ch, f32x4 (&ca)[4], f32x4 (&cb)[4]) {
-            const unsigned char* cp = lds + C::OFF_COEF + ch * 4 * 32;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                ca[r] = *reinterpret_cast<const f32x4*>(cp + r * 32);
-                cb[r] = *reinterpret_cast<const f32x4*>(cp + r * 32 + 16);
-            }
-        };
-        // ---- REC: the wave's rows [PROWS pw, +PROWS) of a tile.  Expansion
-        // lane (erg, ecl) = columns 4 ecl .. 4 ecl + 3 of rows erg + RG k (k <
-        // NK) of them; every 16-lane DPP row holds the records of its erg
-        // group's NK rows: register t, lane m of the DPP row = element m % 8
-        // of row erg + RG (2 t + m / 8) -- broadcast by row_newbcast.  Loaded
-        // at the start of a step (before the out-of-tile gathers, so waiting
-        // for them does not drain those) ...
-        constexpr int NK = C::PROWS / C::RG, NOWN = NK / 2;
-        static_assert(NK % 2 == 0, "own-record layout");
-        using OWN = float[NOWN];
-        auto load_own = [&](int64_t step, OWN& own) {    // always NOWN loads (never a
-            const int64_t tile = tile_of(step);             // conditional one: the
-            const int erg = lane_ / C::CPL, m = lane_ & 15; // merge would wait)
-#pragma unroll
-            for (int t = 0; t < NOWN; ++t) {
-                int64_t row = row_begin + tile * C::BM + C::PROWS * pw + erg + C::RG * (2 * t + (m >> 3));
-                if (tile >= ntiles || row >= row_end) row = row_end - 1;
-                own[t] = rec[row * 8 + (m & 7)];
-            }
-        };
-        // ... and expanded into the own-row image at its end: lane (erg, ecl)
-        // = columns 4 ecl .. 4 ecl + 3 of rows PROWS pw + erg + RG k (chunk ecl
-        // of row lr at position ecl ^ (lr & 7)); a row's record broadcast
-        // from its 8 lanes
-        auto expand_tile = [&](int64_t step, const OWN& own) {
-            if (tile_of(step) >= ntiles) return;
-            const int sb = static_cast<int>(step % C::XBUF); // its image buffer (xbuf_of)
-            const int erg = lane_ / C::CPL, ecl = lane_ % C::CPL;
-            f32x4 ca[4], cb[4];
-            load_pc(ecl, ca, cb);
-            unsigned char* X = lds + sb * C::X_BYTES;
-#pragma unroll
-            for (int k = 0; k < NK; ++k) {
-                const int lr = C::PROWS * pw + erg + C::RG * k;
-                const int vo = __builtin_bit_cast(int, own[k >> 1]);
-                f32x4 ra, rb;
-                if (k & 1) row_bcast7<8>(vo, ra, rb);
-                else row_bcast7<0>(vo, ra, rb);
-                f32x4 v;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = expand1(ca[r], cb[r], ra, rb);
-                *reinterpret_cast<f32x4*>(X + lr * C::ROWB + ((ecl ^ (lr & 7)) << 4)) = v;
-            }
-        };
         // out-of-tile row c (empty slot: c = ~0u -> the zero row)
         auto xrow = [&](uint32_t c) -> const unsigned char* {
             return c != 0xffffffffu ? reinterpret_cast<const unsigned char*>(x + (int64_t)c * ldx)
@@ -493,15 +397,6 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                         const uint32_t a = (xb + off * C::ROWB) +
                                            (static_cast<uint32_t>(loff) ^ ((off & 7u) << 4));
                         ldv<C::VPL>(reinterpret_cast<const float*>(lds + a), vv);
-                    } else if constexpr (REC) {
-                        const f32x4 ra = *reinterpret_cast<const f32x4*>(rec + (int64_t)c * 8);
-                        const f32x4 rb = *reinterpret_cast<const f32x4*>(rec + (int64_t)c * 8 + 4);
-#pragma unroll
-                        for (int k = 0; k < C::VPL; ++k) {
-                            const float* cp = coef8 + (C::VPL * lane_ + k) * 8;
-                            vv[k] = expand1(*reinterpret_cast<const f32x4*>(cp),
-                                            *reinterpret_cast<const f32x4*>(cp + 4), ra, rb);
-                        }
                     } else {
                         const i32x4 rs = buffer_rsrc(xbase + (uint64_t)static_cast<uint32_t>(c) * ldxb, H * 4);
                         if constexpr (C::VPL == 2) {
@@ -594,9 +489,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         };
 
         // ---- out-of-tile rows of a tile (tables tb) -> registers, EX per row
-        // REC: one float of the record per lane (lane i & 7 of the row's 16),
-        // broadcast within the row at expansion time
-        using XV = std::conditional_t<REC, float[C::NQD][C::EX], f32x4[C::NQD][C::EX][C::CH]>;
+        using XV = f32x4[C::NQD][C::EX][C::CH];
         auto issue_ext = [&](int tb, XV& xv) {
             asm volatile("" ::: "memory");   // after the table writes
             const unsigned char* const ET = ETb(tb);
@@ -612,17 +505,6 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                     if (e + 1 < C::EX) cc[qd][e + 1] = t.z;
                 }
             }
-            if constexpr (REC) {
-#pragma unroll
-                for (int qd = 0; qd < C::NQD; ++qd)
-#pragma unroll
-                    for (int e = 0; e < C::EX; ++e) {
-                        xv[qd][e] = 0.f;
-                        if (cc[qd][e] != 0xffffffffu)
-                            xv[qd][e] = rec[static_cast<uint64_t>(cc[qd][e]) * 8 + (iq & 7)];
-                    }
-                return;
-            } else {
 #pragma unroll
             for (int qd = 0; qd < C::NQD; ++qd)
 #pragma unroll
@@ -641,70 +523,12 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                             xv[qd][e][j] = *reinterpret_cast<const f32x4*>(rowp + coff[j]);
                     }
                 }
-            }
         };
         // their weighted sum, CSR order (empty slots: zeros, w 0), + the rest
         // beyond the register slots (rare; synchronous loads)
         using ACC = f32x4[C::NQD][C::CH];
         auto sum_ext = [&](int tb, const XV& xv, const TInfo& info, ACC& acc) {
             const unsigned char* const ET = ETb(tb);
-            if constexpr (REC) {
-#pragma unroll
-                for (int qd = 0; qd < C::NQD; ++qd)
-#pragma unroll
-                    for (int j = 0; j < C::CH; ++j) acc[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-                // chunk by chunk (its coefficients: 32 registers, read once per
-                // step), slot by slot: the slot's record broadcast from the row's
-                // lanes 0..7 (DPP row_newbcast: VALU, no LDS crossbar)
-#pragma unroll
-                for (int j = 0; j < C::CH; ++j) {
-                    // (scheduling fence: keeps the next chunk's coefficient reads
-                    // from being hoisted over this one -- registers)
-                    __builtin_amdgcn_sched_barrier(0);
-                    f32x4 ca[4], cb[4];
-                    load_pc(c0 + 16 * j, ca, cb);
-#pragma unroll
-                    for (int qd = 0; qd < C::NQD; ++qd) {
-                        const int row = 4 * qd + gq;
-#pragma unroll
-                        for (int e = 0; e < C::EX; ++e) {
-                            // slots past every row's last entry: nothing to add
-                            // (an empty slot adds 0 * relu(e_n): skipping is exact)
-                            if (e >= info.maxext) break;
-                            const float w = __builtin_bit_cast(
-                                float, *reinterpret_cast<const uint32_t*>(ET + (row * C::ETS + e) * 8 + 4));
-                            f32x4 ra, rb;
-                            row_bcast7<0>(__builtin_bit_cast(int, xv[qd][e]), ra, rb);
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                acc[qd][j][r] = fmaf(w, expand1(ca[r], cb[r], ra, rb), acc[qd][j][r]);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int qd = 0; qd < C::NQD; ++qd) {
-                    const int row = 4 * qd + gq;
-#pragma unroll 1
-                    for (int e = C::EX; e < info.maxext; ++e) {
-                        const uint2 cw = *reinterpret_cast<const uint2*>(ET + (row * C::ETS + e) * 8);
-                        const float w = __builtin_bit_cast(float, cw.y);
-                        const float* rp = cw.x != 0xffffffffu ? rec + static_cast<uint64_t>(cw.x) * 8
-                                                              : g_zero_row;
-                        const f32x4 ra = *reinterpret_cast<const f32x4*>(rp);
-                        const f32x4 rb = *reinterpret_cast<const f32x4*>(rp + 4);
-#pragma unroll
-                        for (int j = 0; j < C::CH; ++j) {
-                            f32x4 ca[4], cb[4];
-                            load_pc(c0 + 16 * j, ca, cb);
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                acc[qd][j][r] = fmaf(w, expand1(ca[r], cb[r], ra, rb), acc[qd][j][r]);
-                        }
-                    }
-                }
-                return;
-            }
-            else {
 #pragma unroll
             for (int qd = 0; qd < C::NQD; ++qd) {
                 const int row = 4 * qd + gq;
@@ -732,20 +556,15 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                     }
                 }
             }
-            }
         };
 
         // ---- in-tile entries of a tile (tables tb) on top of acc, then scale,
         //      split and write the wave's rows to the A image
         auto finish_tile = [&](int tb, const TInfo& info, ACC& acc, int64_t s) {
             const unsigned char* const LT = LTb(tb);
-            // REC: lane-derived values laundered per call, so their address
-            // arithmetic is redone per step instead of pinned in registers
-            int gqs = gq, c0s = c0;
-            if constexpr (REC) asm volatile("" : "+v"(gqs), "+v"(c0s));
 #pragma unroll
             for (int qd = 0; qd < C::NQD; ++qd) {
-                const int row = 4 * qd + gqs;
+                const int row = 4 * qd + gq;
                 const int ndeg = (flags & MIGNN_DIAG_NO_LOCAL) ? 0 : info.maxdeg;
                 for (int u0 = 0; u0 < ndeg; u0 += UBE) {
                     uint2 pw_[UBE];
@@ -791,7 +610,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                 wait_a(s);
 #pragma unroll
                 for (int j = 0; j < C::CH; ++j) {
-                    const int hc = 4 * (c0s + 16 * j);  // first half of my chunk in the row
+                    const int hc = 4 * (c0 + 16 * j);  // first half of my chunk in the row
                     *reinterpret_cast<f16x4*>(&AH[lrow * C::AS + hc]) = h[j];
                     *reinterpret_cast<f16x4*>(&AL[lrow * C::AS + hc]) = l[j];
                 }
@@ -816,14 +635,7 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
         issue_ext(0, xv);
         sum_ext(0, xv, ia, acc);
         int rpa = pa.rpv;
-        if constexpr (REC) {
-            block_barrier<0xC07F>();   // the coefficient table (written before the tables)
-            OWN own0;
-            load_own(0, own0);
-            expand_tile(0, own0);
-        }
-        OWN own_next;                   // REC: records of tile s+2's own rows
-        block_barrier<0xC07F>();   // zero row, counters, own rows of tiles 0, 1 (lgkmcnt(0))
+        block_barrier<0xC07F>();   // zero row, counters, own rows of tile 0 (lgkmcnt(0))
         for (int64_t s = -1; s < nsteps; ++s) {
             const int ta = static_cast<int>((s + 1) & 1), tbb = ta ^ 1;
             PIdx pc{};
@@ -831,7 +643,6 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             p_load_entries<C::PROWS>(pc, col, ew, lane_);                      // tile s+3
             const int rpd = p_load_rpv<C::PROWS>(row_ptr, first_row(tile_of(s + 4)), row_end, lane_);
             if (pw == 0) stamp(trace, lane_, s, 0);
-            if constexpr (REC) load_own(s + 2, own_next);   // expanded at the end of the step
             // (re)built every step: past the last tile this only resets the
             // tables to empty slots, so the gathers never see stale columns
             const bool prod = !(flags & MIGNN_DIAG_NO_PRODUCE);
@@ -841,29 +652,18 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             if (dext) issue_ext(tbb, xv);
             if (pw == 0) stamp(trace, lane_, s, 1);
             a_free = s < 0;
-            // DEC: tile s+1's own rows (DMA'd at consumer step s-1) landed
-            if constexpr (DEC) lds_wait(cntD, C::NCW * static_cast<int>(s + 1));
             const int64_t t1 = tile_of(s + 1);
             if (s + 1 < nsteps && t1 < ntiles && prod) {
                 if (ia.slow) slow_rows(t1, rpa, s);
                 else finish_tile(ta, ia, acc, s);
             }
-            // DEC: tile s+1's A image / exponents written, its own rows read
-            if constexpr (DEC)
-                if (lane_ == 0) lds_bump(cntP);
             if (pw == 0) stamp(trace, lane_, s, 3);
             if (dext) sum_ext(tbb, xv, ib, acc);
             rpa = pb.rpv;
             pb = pc;
             rpc = rpd;
             ia = ib;
-            // REC: tile s+2's rows (records DMA'd at step s-2, landed a step
-            // ago), read by the producers next step.  Placed at the END of the
-            // step: at its start the same expansion produced sporadic wrong
-            // chunks (a few rows per 10^5, run to run; scripts/rec_debug.py)
-            if constexpr (REC)
-                if (s + 2 < nsteps) expand_tile(s + 2, own_next);
-            if constexpr (!DEC) block_barrier<0xC07F>();   // this step's LDS writes done (lgkmcnt(0))
+            block_barrier<0xC07F>();   // this step's LDS writes done (lgkmcnt(0))
         }
         return;
     }
@@ -939,24 +739,14 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     }
     const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
 
-    if constexpr (REC) {
-        // (the producers fill the coefficient table before the first barrier
-        // and expand tile 0 between the two, tile s+2 at the end of step s)
-        block_barrier<0x70>();
-    } else {
-        x_dma(tile_of(0));
-        if constexpr (!STG) x_dma(tile_of(1));   // (STG: tile 1 at step -1)
-    }
-    block_barrier<0x70>();   // own rows of tiles 0 and 1 landed: vmcnt(0) lgkmcnt(0)
+    x_dma(tile_of(0));             // (tile 1 at step -1)
+    block_barrier<0x70>();   // own rows of tile 0 landed: vmcnt(0) lgkmcnt(0)
     for (int64_t s = -1; s < nsteps; ++s) {
         const int64_t tile = tile_of(s);
         const bool work = s >= 0 && tile < ntiles;
         const bool mm = work && !(flags & MIGNN_DIAG_NO_MFMA);
         f32x4 acc[C::IB][C::JB];
         int pr[C::IB];
-        // DEC: the producers finished tile s (A image, exponents, own-row reads)
-        if constexpr (DEC)
-            if (s >= 0) lds_wait(cntP, C::NPW * static_cast<int>(s + 1));
         if (work) {
             // seed: (residual + bias) * 2^(p_row + q_w)
             const unsigned char* const X = lds + xbuf_of(tile) * C::X_BYTES;
@@ -979,17 +769,15 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
             }
         }
         // residual taken (or nothing to take): once every consumer has, the
-        // buffer takes the own rows of tile s+3
+        // buffer takes the own rows of tile s+2
         if (s >= 0 && lane_ == 0) lds_bump(cntX);
         lds_wait(cntX, C::NCW * static_cast<int>(s + 1));
         if (wave == 0) stamp(trace, lane_, s, 4);
-        // own rows of tile s+3 into the buffer just freed: before the MFMAs, or
+        // own rows of tile s+2 into the buffer just freed: before the MFMAs, or
         // (MIGNN_SCHED_DMA_LATE) after the epilogue stores, away from the
         // producers' gather burst at the start of the step
         const bool dma_late = (flags & MIGNN_SCHED_DMA_LATE) != 0;
-        bool dma = false;
-        if constexpr (!REC)
-            if (!dma_late) dma = (s + C::XBUF < nsteps) && x_dma(tile_of(s + C::XBUF));
+        if (!dma_late && s + C::XBUF < nsteps) x_dma(tile_of(s + C::XBUF));
         if (wave == 0) stamp(trace, lane_, s, 5);
         if (mm) {
             // fragments of block (kc, ib) = step t = kc * IB + ib; the next
@@ -1020,22 +808,18 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        // A image read (the MFMA operands are in registers once issued... the
-        // last fragment pair is consumed by the MFMAs above): producers may
-        // overwrite it with the next tile
+        // A image read (the last fragment pair is consumed by the MFMAs
+        // above): producers may overwrite it with the next tile
         if (s >= 0 && lane_ == 0) lds_bump(cntA);
         if (wave == 0) stamp(trace, lane_, s, 6);
         bool stored = false;
-        // DEC: every consumer has read the staging tile of step s-1
-        if constexpr (DEC)
-            if (mm) lds_wait(cntR, C::NCW * static_cast<int>(s));
         if (mm) {
-            // epilogue: unscale, BN affine, ReLU; lane (r, g) stores 16 B of row r
+            // epilogue: unscale, BN affine, ReLU -> the staging tile (row lr,
+            // 16-B chunk ch at position ch ^ (lr & 15))
             const int64_t t0 = row_begin + tile * C::BM;
             stored = t0 + C::BM <= row_end;    // every row of the tile stored below
 #pragma unroll
             for (int ib = 0; ib < C::IB; ++ib) {
-                const int64_t row = t0 + (wm * C::IB + ib) * 16 + rr;
 #pragma unroll
                 for (int jb = 0; jb < C::JB; ++jb) {
                     const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 16 * jb + 4 * gg]);
@@ -1048,77 +832,47 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
                         if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
                         o[r] = v;
                     }
-                    if constexpr (STG) {
-                        // staging tile: row lr, 16-B chunk ch at position ch ^ (lr & 15)
-                        const int lr = (wm * C::IB + ib) * 16 + rr;
-                        const int ch = ((n0 + 16 * jb) >> 2) + gg;
-                        *reinterpret_cast<f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4)) =
-                            f32x4{o[0], o[1], o[2], o[3]};
-                    } else if (row < row_end) {
-                        f32x4* const dst = reinterpret_cast<f32x4*>(out + row * ldo + n0 + 16 * jb + 4 * gg);
-                        if (flags & MIGNN_DIAG_PLAIN_STORE) *dst = f32x4{o[0], o[1], o[2], o[3]};
-                        else __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, dst);
-                    }
+                    const int lr = (wm * C::IB + ib) * 16 + rr;
+                    const int ch = ((n0 + 16 * jb) >> 2) + gg;
+                    *reinterpret_cast<f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4)) =
+                        f32x4{o[0], o[1], o[2], o[3]};
                 }
             }
         }
-        if constexpr (STG) {
-            // every consumer's blocks staged -> whole rows: consumer w stores
-            // rows 16 w .. 16 w + 15, two per instruction (a half-wave per row)
-            if (s >= 0 && lane_ == 0) lds_bump(cntS);
-            if (mm) {
-                lds_wait(cntS, C::NCW * static_cast<int>(s + 1));
-                const int64_t t0 = row_begin + tile * C::BM;
-                constexpr int LPRW = C::ROWB / 16;          // lanes per row (32 at H = 128)
-                constexpr int RPI = 64 / LPRW;              // rows per store instruction
-                const int ch = lane_ % LPRW;
+        // every consumer's blocks staged -> whole rows: consumer w stores
+        // rows 16 w .. 16 w + 15, two per instruction (a half-wave per row)
+        if (s >= 0 && lane_ == 0) lds_bump(cntS);
+        if (mm) {
+            lds_wait(cntS, C::NCW * static_cast<int>(s + 1));
+            const int64_t t0 = row_begin + tile * C::BM;
+            constexpr int LPRW = C::ROWB / 16;          // lanes per row (32 at H = 128)
+            constexpr int RPI = 64 / LPRW;              // rows per store instruction
+            const int ch = lane_ % LPRW;
 #pragma unroll
-                for (int i = 0; i < C::NSTG; ++i) {
-                    const int lr = wave * (C::BM / C::NCW) + i * RPI + lane_ / LPRW;
-                    const f32x4 v = *reinterpret_cast<const f32x4*>(
-                        lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4));
-                    if (t0 + lr < row_end)
-                        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + 4 * ch));
-                }
+            for (int i = 0; i < C::NSTG; ++i) {
+                const int lr = wave * (C::BM / C::NCW) + i * RPI + lane_ / LPRW;
+                const f32x4 v = *reinterpret_cast<const f32x4*>(
+                    lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4));
+                if (t0 + lr < row_end)
+                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + 4 * ch));
             }
-            if constexpr (DEC)
-                if (s >= 0 && lane_ == 0) lds_bump(cntR);
         }
-        if constexpr (!REC)
-            if (dma_late) dma = (s + C::XBUF < nsteps) && x_dma(tile_of(s + C::XBUF));
+        if (dma_late && s + C::XBUF < nsteps) x_dma(tile_of(s + C::XBUF));
         if (wave == 0) stamp(trace, lane_, s, 7);
-        // the own rows DMA'd a step ago must have landed (producers read them
-        // next step); this step's DMA (NPC) and row stores (NST), the youngest
-        // vector-memory operations, may stay in flight
-        constexpr int npc = C::NPC;
-        if constexpr (DEC) {
-            // this step's DMA (tile s+2, read by the producers' next step)
-            // landed -- the row stores may fly -- then tell the producers
-            asm volatile("" ::: "memory");
-            if (stored) __builtin_amdgcn_s_waitcnt(0x70 | C::NSTG);
-            else __builtin_amdgcn_s_waitcnt(0x70);
-            asm volatile("" ::: "memory");
-            if (lane_ == 0) lds_bump(cntD);
-        } else if constexpr (STG) {
-            // two image buffers: this step's DMA (tile s+2) is read by the
-            // producers next step -- it must land now; the row stores may fly
-            if (stored) block_barrier<0x70 | C::NSTG>();
-            else block_barrier<0x70>();
-        } else {
-            if (dma && stored) block_barrier<0x70 | (npc + C::NST)>();
-            else if (dma) block_barrier<0x70 | npc>();
-            else if (stored) block_barrier<0x70 | C::NST>();
-            else block_barrier<0x70>();
-        }
+        // this step's DMA (tile s+2) is read by the producers next step -- it
+        // must land now; the row stores (the youngest vector-memory
+        // operations) may fly
+        if (stored) block_barrier<0x70 | C::NSTG>();
+        else block_barrier<0x70>();
     }
 }
 
-template <int H, bool REC, bool STG = false, bool DEC = false, int UBT = 0>
+template <int H>
 int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                  int64_t ldx, int64_t rb, int64_t re, const float* w, const float* bias,
                  const float* scale, const float* shift, int flags, float* out, int64_t ldo,
-                 const float* rec, const float* coef8, hipStream_t st) {
-    using C = SCfg<H, STG>;
+                 hipStream_t st) {
+    using C = SCfg<H>;
     static int grid_cache[64] = {0};
     int dev = 0;
     MIGNN_HIP(hipGetDevice(&dev));
@@ -1132,8 +886,8 @@ int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, co
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL((gcn_f16x3_kernel<H, REC, STG, DEC, UBT>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col,
-                       ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, rec, coef8,
+    hipLaunchKernelGGL((gcn_f16x3_kernel<H>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x,
+                       ldx, rb, re, w, bias, scale, shift, flags, out, ldo,
                        (flags & MIGNN_DIAG_TRACE) ? g_trace16_host : nullptr);
     return launch_status("gcn_f16x3_kernel");
 }
@@ -1145,6 +899,19 @@ using namespace mignn;
 
 extern "C" int mignn_diag_set_trace_f16x3(void* buf) {
     g_trace16_host = static_cast<unsigned long long*>(buf);
+    return MIGNN_OK;
+}
+
+extern "C" int mignn_device_errors(unsigned int* out, int clear) {
+    MIGNN_REQUIRE(out, "device_errors: null pointer");
+    MIGNN_HIP(hipDeviceSynchronize());
+    MIGNN_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_device_errors), sizeof(unsigned int), 0,
+                                  hipMemcpyDeviceToHost));
+    if (clear) {
+        const unsigned int zero = 0u;
+        MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_device_errors), &zero, sizeof(unsigned int), 0,
+                                    hipMemcpyHostToDevice));
+    }
     return MIGNN_OK;
 }
 
@@ -1175,61 +942,8 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
     MIGNN_REQUIRE(x != out, "gcn_layer_f16x3: in-place not supported (neighbours read x)");
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
-    if (flags & MIGNN_SCHED_UB3)
-        return h == 128 ? launch_f16x3<128, false, true, false, 3>(row_ptr, col, ew, x, ldx, rb, re,
-                                                                   w, bias, scale, shift, flags,
-                                                                   out, ldo, nullptr, nullptr, st)
-                        : launch_f16x3<64, false, true, false, 3>(row_ptr, col, ew, x, ldx, rb, re,
-                                                                  w, bias, scale, shift, flags,
-                                                                  out, ldo, nullptr, nullptr, st);
-    if (flags & MIGNN_SCHED_UB4)
-        return h == 128 ? launch_f16x3<128, false, true, false, 4>(row_ptr, col, ew, x, ldx, rb, re,
-                                                                   w, bias, scale, shift, flags,
-                                                                   out, ldo, nullptr, nullptr, st)
-                        : launch_f16x3<64, false, true, false, 4>(row_ptr, col, ew, x, ldx, rb, re,
-                                                                  w, bias, scale, shift, flags,
-                                                                  out, ldo, nullptr, nullptr, st);
-    if ((flags & MIGNN_SCHED_DECOUPLED) && !(flags & MIGNN_SCHED_UNSTAGED))
-        return h == 128 ? launch_f16x3<128, false, true, true>(row_ptr, col, ew, x, ldx, rb, re, w,
-                                                               bias, scale, shift, flags, out, ldo,
-                                                               nullptr, nullptr, st)
-                        : launch_f16x3<64, false, true, true>(row_ptr, col, ew, x, ldx, rb, re, w,
-                                                              bias, scale, shift, flags, out, ldo,
-                                                              nullptr, nullptr, st);
-    if (!(flags & MIGNN_SCHED_UNSTAGED))
-        return h == 128 ? launch_f16x3<128, false, true>(row_ptr, col, ew, x, ldx, rb, re, w, bias,
-                                                         scale, shift, flags, out, ldo, nullptr,
-                                                         nullptr, st)
-                        : launch_f16x3<64, false, true>(row_ptr, col, ew, x, ldx, rb, re, w, bias,
-                                                        scale, shift, flags, out, ldo, nullptr,
-                                                        nullptr, st);
-    return h == 128 ? launch_f16x3<128, false>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,
-                                               shift, flags, out, ldo, nullptr, nullptr, st)
-                    : launch_f16x3<64, false>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,
-                                              shift, flags, out, ldo, nullptr, nullptr, st);
-}
-
-extern "C" int mignn_gcn_layer_f16x3_rec(const int32_t* row_ptr, const int32_t* col,
-                                         const float* ew, const float* rec, const float* coef8,
-                                         int64_t rb, int64_t re, int h, const float* w,
-                                         const float* bias, const float* scale,
-                                         const float* shift, int flags, float* out, int64_t ldo,
-                                         void* stream) {
-    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer_f16x3_rec: unknown flags 0x%x", flags);
-    MIGNN_REQUIRE(row_ptr && col && ew && rec && coef8 && w && out,
-                  "gcn_layer_f16x3_rec: null pointer");
-    MIGNN_REQUIRE(h == 64 || h == 128, "gcn_layer_f16x3_rec: h must be 64 or 128 (got %d)", h);
-    MIGNN_REQUIRE(aligned16(rec) && aligned16(coef8) && aligned16(w) && aligned16(out),
-                  "gcn_layer_f16x3_rec: unaligned");
-    MIGNN_REQUIRE(ldo % 4 == 0 && ldo >= h, "gcn_layer_f16x3_rec: bad ldo");
-    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_layer_f16x3_rec: bad row range");
-    MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bias, "gcn_layer_f16x3_rec: bias");
-    MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gcn_layer_f16x3_rec: affine");
-    if (re == rb) return MIGNN_OK;
-    hipStream_t st = as_stream(stream);
-    // x is never read in records mode (rows are expanded from rec)
-    return h == 128 ? launch_f16x3<128, true>(row_ptr, col, ew, nullptr, h, rb, re, w, bias, scale,
-                                              shift, flags, out, ldo, rec, coef8, st)
-                    : launch_f16x3<64, true>(row_ptr, col, ew, nullptr, h, rb, re, w, bias, scale,
-                                             shift, flags, out, ldo, rec, coef8, st);
+    return h == 128 ? launch_f16x3<128>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
+                                        flags, out, ldo, st)
+                    : launch_f16x3<64>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
+                                       flags, out, ldo, st);
 }

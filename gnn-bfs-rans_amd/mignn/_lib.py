@@ -26,6 +26,7 @@ _P = c_void_p
 SIGNATURES = {
     "mignn_abi_version": (c_int, []),
     "mignn_last_error": (ctypes.c_char_p, []),
+    "mignn_device_errors": (c_int, [_P, c_int]),
     "mignn_csr_scratch_bytes": (c_size_t, [c_int64, c_int64]),
     "mignn_csr_build": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_size_t, _P]),
     "mignn_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P, _P,
@@ -190,3 +191,24 @@ def last_error() -> str:
 def check(rc: int, what: str):
     if rc != 0:
         raise MignnError(f"{what} failed (status {rc}): {last_error()}")
+
+
+DEVERR_SPIN = 1
+_DEVERR_NAMES = {DEVERR_SPIN: "a bounded in-kernel wait (LDS hand-off) ran out"}
+
+
+def device_errors(clear: bool = True) -> int:
+    """The current device's sticky in-kernel error bits (mignn_device_errors;
+    synchronises the device).  Nonzero means some launch since the last
+    clear produced wrong output."""
+    word = ctypes.c_uint(0)
+    check(lib().mignn_device_errors(ctypes.addressof(word), 1 if clear else 0), "mignn_device_errors")
+    return int(word.value)
+
+
+def check_device_errors(what: str = "mignn kernels"):
+    """Raise if any launch since the last check recorded an in-kernel error."""
+    bits = device_errors(clear=True)
+    if bits:
+        names = [v for k, v in _DEVERR_NAMES.items() if bits & k] or [hex(bits)]
+        raise MignnError(f"{what}: device error {bits:#x}: " + "; ".join(names))

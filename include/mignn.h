@@ -39,6 +39,14 @@ enum mignn_status {
 int mignn_abi_version(void);
 const char* mignn_last_error(void);
 
+/* In-kernel protocol failures, sticky per device (a __device__ word of the
+ * library, not caller memory): MIGNN_DEVERR_SPIN = a bounded wait inside a
+ * fused layer kernel (gcn_f16x3.hip's LDS hand-offs) ran out -- that
+ * launch's output is wrong.  Reads (synchronously, after the device is idle)
+ * and optionally clears the word of the current device into *out. */
+enum { MIGNN_DEVERR_SPIN = 1 };
+int mignn_device_errors(unsigned int* out, int clear);
+
 /* ------------------------------------------------------------------------
  * Graph structure.
  * Replaces, on the device and without host syncs:

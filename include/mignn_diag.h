@@ -18,19 +18,12 @@ enum {
     MIGNN_DIAG_NO_EXT = 4096,         /* f16x3 GCN layer: skip the out-of-tile gathers */
     MIGNN_DIAG_NO_LOCAL = 8192,       /* f16x3 GCN layer: skip the in-tile (LDS) pass */
     MIGNN_DIAG_NO_TABLES = 16384,     /* f16x3 GCN layer: skip the lookup-table build */
-    MIGNN_DIAG_PLAIN_STORE = 32768,   /* f16x3 GCN layer: plain (not non-temporal) stores */
+    MIGNN_DIAG_PLAIN_STORE = 32768,   /* split-fp16 GEMM: unstaged (16 x 64-B) row stores */
     MIGNN_SCHED_INTERLEAVED = 65536,  /* f16x3 GCN layer: step s covers tiles [sG, (s+1)G) (the
                                          default: each XCD walks a contiguous tile range) */
     MIGNN_SCHED_PRIO_CONSUMERS = 131072, /* f16x3 GCN layer: consumer waves at s_setprio 1 */
     MIGNN_SCHED_PRIO_PRODUCERS = 262144, /* f16x3 GCN layer: producer waves at s_setprio 1 */
-    MIGNN_SCHED_DMA_LATE = 524288,       /* f16x3 GCN layer: own-row DMA after the epilogue */
-    MIGNN_SCHED_UNSTAGED = 1048576       /* f16x3 GCN layer: the round-1 form -- 3 image buffers,
-                                            stores straight from the 16x16 accumulators (the
-                                            default stages whole output rows in LDS) */,
-    MIGNN_SCHED_DECOUPLED = 2097152,     /* f16x3 GCN layer, EXPERIMENTAL: LDS-counter hand-offs
-                                            only, no block barrier per step (see gcn_f16x3.hip) */
-    MIGNN_SCHED_UB4 = 4194304,           /* f16x3 GCN layer: in-tile entries 4 per LDS batch */
-    MIGNN_SCHED_UB3 = 8388608            /* f16x3 GCN layer: in-tile entries 3 per LDS batch */
+    MIGNN_SCHED_DMA_LATE = 524288        /* f16x3 GCN layer: own-row DMA after the epilogue */
 };
 /* mignn_gcn_layer / mignn_gcn_layer_f16x3 / mignn_linear with the flags above */
 int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,

@@ -101,14 +101,6 @@ def gcn16(flags):
                                        P(W), P(b), P(sc), P(sh), flags, P(Y), H, st), "gcn16")
 
 
-SEG = int(os.environ.get("KB_SEG", "0"))
-
-
-def ring(flags):
-    _lib.check(L.mignn_gcn_layer_ring(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
-                                      P(W), P(b), P(sc), P(sh), flags, P(Y), H, SEG, st), "ring")
-
-
 def agg(_):
     _lib.check(L.mignn_gcn_aggregate(P(csr.row_ptr), P(csr.col), P(csr.dinv), P(X), H, 0, n, H,
                                      P(Y), H, st), "agg")
@@ -180,11 +172,10 @@ def diag(mode_blocks):
 
 
 cases = {
-    "ring": (ring, 15), "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_interleaved": (gcn16, 15 | 65536), "gcn16_prio_cons": (gcn16, 15 | 131072), "gcn16_prio_prod": (gcn16, 15 | 262144), "gcn16_dma_late": (gcn16, 15 | 524288),
-    "gcn16_dma_late_plain": (gcn16, 15 | 524288 | 32768), "gcn16_unstaged": (gcn16, 15 | 1048576), "gcn16_dec": (gcn16, 15 | 2097152), "gcn16_ub4": (gcn16, 15 | 4194304), "gcn16_ub3": (gcn16, 15 | 8388608), "gcn16_no_produce": (gcn16, 15 | 256),
+    "gcn_full": (gcn, 15), "gcn16_full": (gcn16, 15), "gcn16_interleaved": (gcn16, 15 | 65536), "gcn16_prio_cons": (gcn16, 15 | 131072), "gcn16_prio_prod": (gcn16, 15 | 262144), "gcn16_dma_late": (gcn16, 15 | 524288),
+    "gcn16_no_produce": (gcn16, 15 | 256),
     "gcn16_no_mfma": (gcn16, 15 | 512), "gcn16_no_ext": (gcn16, 15 | 4096),
     "gcn16_no_tables_ext": (gcn16, 15 | 4096 | 16384),
-    "gcn16_plain": (gcn16, 15 | 32768), "gcn16_no_produce_plain": (gcn16, 15 | 256 | 32768),
     "gcn16_no_tables_ext_local": (gcn16, 15 | 4096 | 16384 | 8192),
     "gcn16_no_local": (gcn16, 15 | 8192), "gcn16_no_ext_local": (gcn16, 15 | 4096 | 8192),
     "gcn16_only_dma": (gcn16, 15 | 256 | 512), "gcn_no_mfma": (gcn, 15 | 512), "gcn_no_gather": (gcn, 15 | 256),
@@ -244,23 +235,6 @@ if os.environ.get("KB_TRACE"):
          "c_epilogue": t[:, 1:60, 7] - t[:, 1:60, 6],
          "step": t[:, 2:61, 0] - t[:, 1:60, 0]}
     res["trace_cycles_median"] = {k: float(v.median()) for k, v in d.items()}
-if os.environ.get("KB_RTRACE"):
-    buf = torch.zeros(8 * 64 * 16, dtype=torch.int64, device=dev)
-    L.mignn_diag_set_trace_ring.argtypes = [_lib.c_void_p] if hasattr(_lib, "c_void_p") else None
-    import ctypes
-    L.mignn_diag_set_trace_ring.argtypes = [ctypes.c_void_p]
-    _lib.check(L.mignn_diag_set_trace_ring(P(buf)), "rtrace")
-    ring(15)
-    torch.cuda.synchronize()
-    _lib.check(L.mignn_diag_set_trace_ring(None), "rtrace")
-    t = buf.view(8, 64, 16).cpu().double()
-    names = ["idx", "dma", "decode", "ring_loop", "ext_sum", "split_seed", "mfma", "epilogue",
-             "issue_ext", "barrier"]
-    res["ring_trace_cycles_median"] = {}
-    for k in range(9):
-        res["ring_trace_cycles_median"][names[k]] = float((t[:, 2:60, k + 1] - t[:, 2:60, k]).median())
-    res["ring_trace_cycles_median"]["barrier"] = float((t[:, 3:61, 0] - t[:, 2:60, 9]).median())
-    res["ring_trace_cycles_median"]["step"] = float((t[:, 3:61, 0] - t[:, 2:60, 0]).median())
 if os.environ.get("KB_CHECK_HEAD"):
     headdiag(int(os.environ.get("KB_CHECK_HEAD_MODE", "0"))) if os.environ.get("KB_CHECK_HEAD_MODE") else head16(0)
     torch.cuda.synchronize()
@@ -282,9 +256,6 @@ if os.environ.get("KB_CHECK"):
                                        P(W), P(b), P(sc), P(sh),
                                        15 | int(os.environ.get("KB_CHECK_FLAGS", "0")), P(Y16), H, st),
                "gcn16")
-    YR = torch.full_like(X, float("nan"))
-    _lib.check(L.mignn_gcn_layer_ring(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
-                                      P(W), P(b), P(sc), P(sh), 15, P(YR), H, SEG, st), "ring")
     torch.cuda.synchronize()
     rows = torch.randint(0, n, (4096,), generator=torch.Generator().manual_seed(5))
     rp = csr.row_ptr.cpu().long()
@@ -311,9 +282,6 @@ if os.environ.get("KB_CHECK"):
     res["check"] = {"f32_vs_ref_max": (Y32[rr].double() - Yr).abs().max().item(),
                     "f16x3_vs_ref_max": (Y16[rr].double() - Yr).abs().max().item(),
                     "f16x3_vs_f32_max": (Y16 - Y32).abs().max().item(),
-                    "ring_vs_ref_max": (YR[rr].double() - Yr).abs().max().item(),
-                    "ring_vs_f32_max": (YR - Y32).abs().max().item(),
-                    "ring_nan_rows": int(torch.isnan(YR).any(1).sum().item()),
                     "f16x3_nan_rows": int(torch.isnan(Y16).any(1).sum().item()),
                     "f32_max": Y32.abs().max().item(), "X_max": X.abs().max().item()}
 print(json.dumps({"grid": [nx, ny, nz], "H": H, "ms": res}))
