@@ -120,6 +120,12 @@ SIGNATURES = {
     "mignn_input_proj_rows": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P, _P, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P, c_int64, _P]),
+    "mignn_gin_fused_prep_bytes": (c_size_t, [c_int]),
+    "mignn_gin_fused_prep": (c_int, [_P, c_int, _P, c_size_t, _P]),
+    "mignn_gin_layer_fused": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_float, _P,
+                                      _P, _P, _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_layer_fused": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
+                                      _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gcn_norm": (c_int, [_P, _P, _P, c_int64, c_int64, _P, _P]),
     "mignn_rows_gather": (c_int, [_P, c_int64, _P, c_int64, c_int, _P, c_int64, _P]),
     "mignn_grid_graph": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, _P, _P]),
@@ -141,6 +147,7 @@ DIAG_SIGNATURES = {
                                            _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gcn_layer_wave": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P,
                                      _P, c_int, _P, c_int64, c_int, _P]),
+    "mignn_diag_set_agg_gemm_waves": (c_int, [c_int]),
     "mignn_diag_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,
                                   _P, c_int64, _P, _P, c_int, _P, c_int64, _P]),
 }

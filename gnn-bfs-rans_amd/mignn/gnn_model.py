@@ -281,6 +281,17 @@ def f16x3_image(w: torch.Tensor) -> torch.Tensor:
     return img
 
 
+def gin_fused_image(w: torch.Tensor) -> torch.Tensor:
+    """k-permuted split-fp16 image of GIN's nn.2 weight [256, 256] for
+    mignn_gin_layer_fused (mignn_gin_fused_prep)."""
+    L = _lib.lib()
+    w = w.detach().float().contiguous()
+    img = torch.empty(L.mignn_gin_fused_prep_bytes(w.shape[1]), dtype=torch.uint8, device=w.device)
+    _lib.check(L.mignn_gin_fused_prep(_lib.ptr(w), w.shape[1], _lib.ptr(img), img.numel(),
+                                      _stream(w)), "mignn_gin_fused_prep")
+    return img
+
+
 def linear_f16x3(a: torch.Tensor, img: torch.Tensor, n: int, bias=None, *, relu=False,
                  residual=None, scale=None, shift=None, a2: Optional[torch.Tensor] = None,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -674,6 +685,12 @@ class FlowGNN(nn.Module):
             return self._cached(tag, i, srcs, lambda: f16x3_image(w))
         return None
 
+    def _fused256(self) -> bool:
+        """H = 256 GIN / GCN layers as one fused kernel (mignn_gin_layer_fused /
+        mignn_gcn_layer_fused; split-fp16 arithmetic) -- the default in f16x3
+        precision; MIGNN_FUSED256=0 runs the aggregate + GEMM launches instead."""
+        return self.precision == "f16x3" and os.environ.get("MIGNN_FUSED256", "1") != "0"
+
     def _mm(self, tag, i, srcs, w, a, bias=None, **kw):
         """Node transform by W = w: split-fp16 GEMM (mignn_linear_f16x3) or
         exact fp32 MFMA (mignn_linear), as _img decides."""
@@ -703,6 +720,13 @@ class FlowGNN(nn.Module):
                 _lib.check(fn(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
                               P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),
                            "mignn_gcn_layer")
+            elif H == 256 and self._fused256():
+                # aggregate + split-fp16 transform in one kernel (csrc/agg_gemm.hip)
+                img = self._cached("w_gcn", i, (w,), lambda: f16x3_image(w))
+                _lib.check(L.mignn_gcn_layer_fused(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x),
+                                                   x.stride(0), rb, re, H, P(img), P(b), P(scale),
+                                                   P(shift), epi, P(out), out.stride(0), st),
+                           "mignn_gcn_layer_fused")
             else:
                 agg = torch.empty((n, H), dtype=torch.float32, device=x.device)
                 _lib.check(L.mignn_gcn_aggregate(P(csr.row_ptr), P(csr.col), P(csr.dinv), P(x),
@@ -714,6 +738,16 @@ class FlowGNN(nn.Module):
         elif self.layer_type == "GIN":
             nn0, nn2 = layer.nn[0], layer.nn[2]
             eps = self._cached("eps", i, (layer.eps,), lambda: float(layer.eps.reshape(-1)[0]))
+            if H == 256 and self._fused256():
+                # sum aggregate + nn.0 + ReLU + nn.2 in one kernel (csrc/agg_gemm.hip):
+                # neither the aggregate nor the hidden layer reaches memory
+                img1 = self._cached("w_gin0", i, (nn0.weight,), lambda: f16x3_image(nn0.weight))
+                img2 = self._cached("w_gin2p", i, (nn2.weight,), lambda: gin_fused_image(nn2.weight))
+                _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(x), x.stride(0),
+                                                   rb, re, H, eps, P(img1), P(nn0.bias), P(img2),
+                                                   P(nn2.bias), P(scale), P(shift), epi, P(out),
+                                                   out.stride(0), st), "mignn_gin_layer_fused")
+                return
             agg = torch.empty((n, H), dtype=torch.float32, device=x.device)
             if H in (64, 128):
                 _lib.check(L.mignn_gin_layer(P(csr.row_ptr), P(csr.col), P(x), x.stride(0), rb, re,

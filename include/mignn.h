@@ -291,6 +291,32 @@ int mignn_gin_layer(const int32_t* row_ptr, const int32_t* col, const float* x, 
                     const float* scale, const float* shift, int flags,
                     float* tmp, int64_t ldt, float* out, int64_t ldo, void* stream);
 
+/* Fused H = 256 layers in split-fp16 arithmetic (csrc/agg_gemm.hip): the
+ * aggregate (and GIN's hidden layer) never reaches memory -- one kernel per
+ * layer instead of aggregate + GEMM (+ GEMM).  Rows [rb, re) of the CSR, out
+ * row r at out + r*ldo (as mignn_gcn_layer).  Sum order per row: CSR order,
+ * then GIN's (1 + eps) x_i term.
+ *   GIN (configs[4], gnn_model.py:70-75):
+ *     out_i = epi( relu((sum_j x_j + (1+eps) x_i) W1^T + b1) W2^T + b2 )
+ *     img1 = mignn_linear_f16x3_prep(W1 = nn.0.weight, 256, 256);
+ *     img2 = mignn_gin_fused_prep(W2 = nn.2.weight): the same image with k
+ *     permuted to the first transform's accumulator layout;
+ *     b1 = nn.0.bias (always applied, + ReLU); b2 with MIGNN_EPI_BIAS.
+ *   GCN at H = 256 (gnn_model.py:63):
+ *     out_i = epi( (sum_e ew_e x_{col e}) W^T + bias ),  img = linear_f16x3 image of W.
+ * Replaces mignn_sum_aggregate / mignn_gcn_aggregate + mignn_linear_f16x3 (x2). */
+size_t mignn_gin_fused_prep_bytes(int h);
+int mignn_gin_fused_prep(const float* w2, int h, void* img, size_t img_bytes, void* stream);
+int mignn_gin_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* x,
+                          int64_t ldx, int64_t row_begin, int64_t row_end, int h, float eps,
+                          const void* img1, const float* b1, const void* img2, const float* b2,
+                          const float* scale, const float* shift, int flags, float* out,
+                          int64_t ldo, void* stream);
+int mignn_gcn_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                          const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                          const void* img, const float* bias, const float* scale,
+                          const float* shift, int flags, float* out, int64_t ldo, void* stream);
+
 /* ------------------------------------------------------------------------
  * Mesh -> graph (reference graph_constructor.py).
  * owner [n_faces] / neighbour [n_internal_faces] int64 cell ids as read from

@@ -80,6 +80,9 @@ int mignn_gcn_layer_wave(const int32_t* row_ptr, const int32_t* col, const float
                          const float* w, const float* bias, const float* scale,
                          const float* shift, int flags, float* out, int64_t ldo, int variant,
                          void* stream);
+/* Fused H = 256 layers (csrc/agg_gemm.hip): waves per block, 8 (default, one
+ * 128-row block per CU) or 4 (64-row blocks, two per CU) -- timing study. */
+int mignn_diag_set_agg_gemm_waves(int waves);
 #ifdef __cplusplus
 }
 #endif

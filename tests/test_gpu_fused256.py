@@ -1,0 +1,196 @@
+"""Fused H = 256 layers (mignn_gin_layer_fused / mignn_gcn_layer_fused,
+csrc/agg_gemm.hip) against a float64 torch restatement of the same layer on
+the same CSR, and against the unfused launches they replace (aggregate +
+split-fp16 GEMM(s)).
+
+Graphs: random destination-major edge lists with degrees 0..12 (rows past the
+kernel's 8 register slots take its one-at-a-time path) and hub rows of 40-60
+entries, a row sub-range [rb, re) written at out + rb * ldo, rows scaled over
+2^+-20 (the online row exponent), every epilogue flag combination.  Bound:
+the split arithmetic's ~2^-22 per product, taken as 4e-6 of the magnitude of
+the chain computed on |values| (plus fp32 rounding of the result)."""
+
+import pytest
+import torch
+
+from mignn import _lib
+from mignn.gnn_model import build_csr, f16x3_image, gin_fused_image, linear_f16x3
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+H = 256
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm GPU")
+    _lib.lib()
+
+
+def _graph(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    deg = torch.randint(0, 13, (n,), generator=g)
+    hub = torch.randperm(n, generator=g)[:5]
+    deg[hub] = torch.randint(40, 61, (5,), generator=g)
+    dst = torch.repeat_interleave(torch.arange(n), deg)
+    src = torch.randint(0, n, (dst.numel(),), generator=g)
+    perm = torch.randperm(dst.numel(), generator=g)
+    return torch.stack([src[perm], dst[perm]]).to(DEV)
+
+
+def _csr_edges(csr, n):
+    rp = csr.row_ptr.cpu().long()
+    col = csr.col.cpu().long()[: int(rp[-1])]
+    dst = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+    return col, dst
+
+
+def _params(seed, scaled_rows=True, n=3000):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(n, H, device=DEV, generator=g)
+    if scaled_rows:
+        x *= torch.pow(2.0, torch.randint(-20, 21, (n, 1), device=DEV, generator=g).float())
+        x[:7] = 0.0
+    w1 = torch.randn(H, H, device=DEV, generator=g) / 16
+    w2 = torch.randn(H, H, device=DEV, generator=g) / 16
+    b1 = torch.randn(H, device=DEV, generator=g) * 0.1
+    b2 = torch.randn(H, device=DEV, generator=g) * 0.1
+    sc = torch.rand(H, device=DEV, generator=g) + 0.5
+    sh = torch.randn(H, device=DEV, generator=g) * 0.1
+    return x, w1, w2, b1, b2, sc, sh
+
+
+def _epi64(c, mag, x, b, sc, sh, flags):
+    if flags & _lib.EPI_BIAS:
+        c = c + b.double()
+        mag = mag + b.double().abs()
+    if flags & _lib.EPI_RESIDUAL:
+        c = x + c
+        mag = mag + x.abs()
+    if flags & _lib.EPI_AFFINE:
+        c = c * sc.double() + sh.double()
+        mag = mag * sc.double() + sh.double().abs()
+    if flags & _lib.EPI_RELU:
+        c = c.clamp_min(0)
+    return c, mag
+
+
+def _check(got, ref, mag, what):
+    err = (got.double() - ref).abs()
+    bound = 4e-6 * mag + 2 * torch.finfo(torch.float32).eps * ref.abs() + 1e-35
+    worst = float((err / bound).max())
+    assert worst <= 1.0, (what, float(err.max()), worst)
+
+
+FLAGS = [15, 0, 1 | 8, 2 | 4]
+
+
+@pytest.mark.parametrize("flags", FLAGS)
+@pytest.mark.parametrize("rb,re", [(0, 3000), (123, 2701)])
+def test_gin_fused_vs_fp64(flags, rb, re):
+    n = 3000
+    ei = _graph(n, 11)
+    csr = build_csr(ei, n, _lib.CSR_VERBATIM)
+    x, w1, w2, b1, b2, sc, sh = _params(5)
+    eps = 0.3
+    out = torch.full((n, H), float("nan"), device=DEV)
+    L = _lib.lib()
+    P = _lib.ptr
+    img1, img2 = f16x3_image(w1), gin_fused_image(w2)
+    _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(x), H, rb, re, H, eps,
+                                       P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), flags,
+                                       P(out), H, _lib.stream()), "gin_fused")
+    torch.cuda.synchronize()
+    col, dst = _csr_edges(csr, n)
+    X = x.double().cpu()
+    a = torch.zeros(n, H, dtype=torch.float64).index_add_(0, dst, X[col]) + (1 + eps) * X
+    am = torch.zeros(n, H, dtype=torch.float64).index_add_(0, dst, X[col].abs()) + (1 + eps) * X.abs()
+    W1, W2 = w1.double().cpu(), w2.double().cpu()
+    h = (a @ W1.T + b1.double().cpu()).clamp_min(0)
+    hm = am @ W1.T.abs() + b1.double().cpu().abs()
+    c = h @ W2.T
+    cm = hm @ W2.T.abs()
+    ref, mag = _epi64(c, cm, X, b2.cpu(), sc.cpu(), sh.cpu(), flags)
+    got = out.cpu()
+    _check(got[rb:re], ref[rb:re], mag[rb:re], f"gin flags={flags}")
+    assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
+
+
+@pytest.mark.parametrize("flags", FLAGS)
+def test_gcn_fused_vs_fp64(flags):
+    n = 3000
+    rb, re = 57, 2999
+    ei = _graph(n, 12)
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
+    x, w1, _, b1, _, sc, sh = _params(6)
+    out = torch.full((n, H), float("nan"), device=DEV)
+    L = _lib.lib()
+    P = _lib.ptr
+    img = f16x3_image(w1)
+    _lib.check(L.mignn_gcn_layer_fused(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), H, rb, re, H,
+                                       P(img), P(b1), P(sc), P(sh), flags, P(out), H,
+                                       _lib.stream()), "gcn_fused")
+    torch.cuda.synchronize()
+    col, dst = _csr_edges(csr, n)
+    ew = csr.ew.cpu().double()[: col.numel()]
+    X = x.double().cpu()
+    a = torch.zeros(n, H, dtype=torch.float64).index_add_(0, dst, ew[:, None] * X[col])
+    am = torch.zeros(n, H, dtype=torch.float64).index_add_(0, dst, (ew[:, None] * X[col]).abs())
+    W = w1.double().cpu()
+    ref, mag = _epi64(a @ W.T, am @ W.T.abs(), X, b1.cpu(), sc.cpu(), sh.cpu(), flags)
+    got = out.cpu()
+    _check(got[rb:re], ref[rb:re], mag[rb:re], f"gcn flags={flags}")
+    assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
+
+
+def test_gin_fused_matches_unfused_launches():
+    """The fused kernel against the launch sequence it replaces (sum aggregate
+    + two split-fp16 GEMMs): the same arithmetic up to the hidden layer's
+    exponent (one per row over all 256 columns vs the GEMM's online one) and
+    fp32 summation order."""
+    n = 20000
+    g = torch.Generator(device=DEV).manual_seed(3)
+    ei = torch.stack([torch.randint(0, n, (6 * n,), device=DEV, generator=g),
+                      torch.arange(n, device=DEV).repeat_interleave(6)])
+    csr = build_csr(ei, n, _lib.CSR_VERBATIM)
+    x, w1, w2, b1, b2, sc, sh = _params(7, scaled_rows=False, n=n)
+    L = _lib.lib()
+    P = _lib.ptr
+    out = torch.empty(n, H, device=DEV)
+    img1, img2 = f16x3_image(w1), gin_fused_image(w2)
+    _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(x), H, 0, n, H, 0.0,
+                                       P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15, P(out),
+                                       H, _lib.stream()), "gin_fused")
+    agg = torch.empty(n, H, device=DEV)
+    _lib.check(L.mignn_sum_aggregate(P(csr.row_ptr), P(csr.col), P(x), H, 1.0, 0, n, H, P(agg), H,
+                                     _lib.stream()), "sum_aggregate")
+    h1 = linear_f16x3(agg, img1, H, b1, relu=True)
+    ref = linear_f16x3(h1, f16x3_image(w2), H, b2, relu=True, residual=x, scale=sc, shift=sh)
+    torch.cuda.synchronize()
+    d = (out - ref).abs().max().item()
+    assert d <= 2e-6 * max(1.0, ref.abs().max().item()), d
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+def test_fused_block_shapes_agree(waves):
+    """The 4- and 8-wave block forms (mignn_diag_set_agg_gemm_waves) give
+    bitwise the same rows (same per-row arithmetic, different tiling)."""
+    n = 5000
+    ei = _graph(n, 13)
+    csr = build_csr(ei, n, _lib.CSR_VERBATIM)
+    x, w1, w2, b1, b2, sc, sh = _params(8, n=n)
+    L = _lib.lib()
+    P = _lib.ptr
+    img1, img2 = f16x3_image(w1), gin_fused_image(w2)
+    outs = []
+    for wv in (8, waves):
+        _lib.check(L.mignn_diag_set_agg_gemm_waves(wv), "waves")
+        o = torch.empty(n, H, device=DEV)
+        _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(x), H, 0, n, H, 0.1,
+                                           P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15, P(o),
+                                           H, _lib.stream()), "gin_fused")
+        outs.append(o)
+    _lib.check(L.mignn_diag_set_agg_gemm_waves(8), "waves")
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
