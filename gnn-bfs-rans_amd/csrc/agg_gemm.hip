@@ -377,6 +377,252 @@ __global__ __launch_bounds__(256) void perm_frag_kernel(const float* __restrict_
     *reinterpret_cast<f16x8*>(base + AFRAG) = l;
 }
 
+// ------------------------------------------------------------------ GATConv
+// Fused GAT layer (gnn_model.py:65-68; heads = 4, concat=False; H in {64, 128}):
+//   alpha_ijk = softmax_j( LeakyReLU(a_s[j][k] + a_d[i][k]) )   (+1e-16, PyG utils.softmax)
+//   out_i     = epi( sum_k (sum_j alpha_ijk x_j) Wcat_k^T + b; residual x_i, BN, ReLU )
+// with the logits a_s | a_d = x wlog^T precomputed ([n, 8], mignn_gat_layer)
+// and Wcat_k = W_k / heads (the head-mean folded into the weights): the
+// per-head aggregates [rows, 4H] never reach memory.  Per wave 16 rows; lane
+// (r, g) first owns head g of row r (scores, max, sum of exp, alphas -> LDS,
+// then every lane reads its row's 32 alphas), then per 32-column x chunk it
+// gathers its 8 columns of the row's neighbours once and forms the 4 heads'
+// weighted sums -- the B operands of W chunks (head k, chunk c) -- split with
+// the row's online exponent, 3 MFMAs per 16x16x32 block.  The 4 W chunks of
+// an x chunk (4 x H/16 column blocks of the linear_f16x3 image of Wcat
+// [H, 4H]) are LDS-DMA'd together, double-buffered, one barrier per x chunk.
+template <int H>
+struct GatCfg {
+    static_assert(H == 64 || H == 128, "gat_fused: H in {64, 128}");
+    static constexpr int AW = 8, NT = AW * 64, BM = 16 * AW;
+    static constexpr int NCB = H / 16;                 // output column blocks (N = H)
+    static constexpr int XC = H / 32;                  // x chunks
+    static constexpr int NPB = 16;                     // column blocks per image chunk (padded)
+    static constexpr int WCH = NCB * 2 * AFRAG;        // real bytes of one W chunk
+    static constexpr int STEPW = 4 * WCH;              // the 4 heads' chunks of one x chunk
+    static constexpr int OFF_AL = 2 * STEPW;           // alphas [AW][16][4][8]
+    static constexpr int OFF_ST = OFF_AL + AW * 16 * 4 * 8 * 4;   // (max, sum) [AW][16][4]
+    static constexpr int OFF_EPI = OFF_ST + AW * 16 * 4 * 8;       // QF | BF | SC | SH [H]
+    static constexpr int LDS_BYTES = OFF_EPI + 4 * H * 4;
+    static_assert(LDS_BYTES <= 160 * 1024, "gat_fused LDS");
+};
+
+template <int H>
+__global__ __launch_bounds__(GatCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void
+gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+                 const float* __restrict__ logits, const float* __restrict__ x, int64_t ldx,
+                 int64_t rb, int64_t re, float slope, const unsigned char* __restrict__ img,
+                 const float* __restrict__ bias, const float* __restrict__ scale,
+                 const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+    using C = GatCfg<H>;
+    constexpr int HEADS = 4;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
+    int32_t* const QF = reinterpret_cast<int32_t*>(lds + C::OFF_EPI);
+    float* const BF = reinterpret_cast<float*>(QF + H);
+    float* const SC = BF + H;
+    float* const SH = SC + H;
+
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
+    const int64_t per_xcd = gridDim.x >> 3;
+    const int64_t tile = static_cast<int64_t>(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;
+    const int64_t row = rb + tile * C::BM + 16 * wave + r;
+    const bool rv = row < re;
+    const int64_t rowc = rv ? row : re - 1;
+
+    // W chunks of x chunk t (heads 0..3: image chunks k XC + t) -> buffer t & 1
+    auto w_dma = [&](int t) {
+        if (t >= C::XC) return;
+        unsigned char* dst = lds + (t & 1) * C::STEPW;
+#pragma unroll
+        for (int pc = 0; pc < C::STEPW / 1024 / C::AW; ++pc) {
+            const int piece = wave + pc * C::AW;              // 1-KB piece of the step
+            const int hd = piece / (C::WCH / 1024), q = piece % (C::WCH / 1024);
+            const unsigned char* src = img + static_cast<size_t>(hd * C::XC + t) * C::NPB * 2 * AFRAG;
+            glds16_ag(src + q * 1024 + lane * 16, lds_addr_ag(dst + piece * 1024));
+        }
+    };
+    w_dma(0);
+    if (tid < H) {
+        const int32_t* q = reinterpret_cast<const int32_t*>(
+            img + static_cast<size_t>(4 * C::XC) * C::NPB * 2 * AFRAG);
+        QF[tid] = q[tid];
+        BF[tid] = (flags & MIGNN_EPI_BIAS) ? bias[tid] : 0.f;
+        SC[tid] = (flags & MIGNN_EPI_AFFINE) ? scale[tid] : 1.f;
+        SH[tid] = (flags & MIGNN_EPI_AFFINE) ? shift[tid] : 0.f;
+    }
+
+    // ---- CSR slots, scores of head g, softmax statistics, alphas
+    const int e0 = row_ptr[rowc];
+    const int deg = rv ? row_ptr[rowc + 1] - e0 : 0;
+    int cj[AS];
+#pragma unroll
+    for (int e = 0; e < AS; ++e) cj[e] = e < deg ? col[e0 + e] : -1;
+    const bool extra = __builtin_amdgcn_ballot_w64(deg > AS) != 0ull;
+    auto leaky = [&](float v) { return v > 0.f ? v : v * slope; };
+    const float ad = logits[rowc * (2 * HEADS) + HEADS + g];
+    float sc[AS];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < AS; ++e) {
+        sc[e] = cj[e] >= 0 ? leaky(logits[static_cast<int64_t>(cj[e]) * (2 * HEADS) + g] + ad) : -INFINITY;
+        mx = fmaxf(mx, sc[e]);
+    }
+    if (extra)
+        for (int e = AS; e < deg; ++e)
+            mx = fmaxf(mx, leaky(logits[static_cast<int64_t>(col[e0 + e]) * (2 * HEADS) + g] + ad));
+    float sm = 0.f;
+#pragma unroll
+    for (int e = 0; e < AS; ++e)
+        if (cj[e] >= 0) sm += expf(sc[e] - mx);
+    if (extra)
+        for (int e = AS; e < deg; ++e)
+            sm += expf(leaky(logits[static_cast<int64_t>(col[e0 + e]) * (2 * HEADS) + g] + ad) - mx);
+    sm += 1e-16f;
+    float* const AL = reinterpret_cast<float*>(lds + C::OFF_AL) + ((wave * 16 + r) * 4) * 8;
+    float* const ST = reinterpret_cast<float*>(lds + C::OFF_ST) + ((wave * 16 + r) * 4) * 2;
+    {
+        f32x4 a0, a1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            a0[e] = cj[e] >= 0 ? expf(sc[e] - mx) / sm : 0.f;
+            a1[e] = cj[e + 4] >= 0 ? expf(sc[e + 4] - mx) / sm : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(AL + g * 8) = a0;
+        *reinterpret_cast<f32x4*>(AL + g * 8 + 4) = a1;
+        ST[g * 2] = mx;
+        ST[g * 2 + 1] = sm;
+    }
+    f32x4 gv[AS][2];
+    // (row addresses recomputed per chunk from the 32-bit columns: 64-bit
+    // pointers held across the loop cost 16 registers)
+    auto gather = [&](int t) {
+#pragma unroll
+        for (int e = 0; e < AS; ++e) {
+            const float* sp = cj[e] >= 0 ? x + static_cast<int64_t>(cj[e]) * ldx + 8 * g + 32 * t
+                                         : g_zero_row_ag + 8 * g + 32 * t;
+            gv[e][0] = *reinterpret_cast<const f32x4*>(sp);
+            gv[e][1] = *reinterpret_cast<const f32x4*>(sp + 4);
+        }
+    };
+    gather(0);
+    f32x4 acc[C::NCB];
+#pragma unroll
+    for (int cb = 0; cb < C::NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int p = 100;
+    const unsigned char* const wl0 = lds + lane * 16;
+
+#pragma unroll 1
+    for (int t = 0; t < C::XC; ++t) {
+        chunk_barrier();                           // W chunks of t and this chunk's rows landed
+        w_dma(t + 1);
+        // the 4 heads' weighted sums of this x chunk (CSR order)
+        f32x4 a[HEADS][2];
+#pragma unroll
+        for (int k = 0; k < HEADS; ++k) {
+            a[k][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            a[k][1] = a[k][0];
+            // the row's alphas of head k (LDS, written by this wave: in order)
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(AL + k * 8);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(AL + k * 8 + 4);
+#pragma unroll
+            for (int e = 0; e < AS; ++e) {
+                const float w = e < 4 ? w0[e] : w1[e - 4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    a[k][0][i] = fmaf(w, gv[e][0][i], a[k][0][i]);
+                    a[k][1][i] = fmaf(w, gv[e][1][i], a[k][1][i]);
+                }
+            }
+        }
+        if (extra) {
+            // entries past the register slots: alphas from the saved statistics
+            for (int e = AS; e < deg; ++e) {
+                const int j = col[e0 + e];
+                const float* sp = x + static_cast<int64_t>(j) * ldx + 8 * g + 32 * t;
+                const f32x4 u0 = *reinterpret_cast<const f32x4*>(sp);
+                const f32x4 u1 = *reinterpret_cast<const f32x4*>(sp + 4);
+#pragma unroll
+                for (int k = 0; k < HEADS; ++k) {
+                    const float adk = logits[rowc * (2 * HEADS) + HEADS + k];
+                    const float w = expf(leaky(logits[static_cast<int64_t>(j) * (2 * HEADS) + k] + adk) -
+                                         ST[k * 2]) / ST[k * 2 + 1];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        a[k][0][i] = fmaf(w, u0[i], a[k][0][i]);
+                        a[k][1][i] = fmaf(w, u1[i], a[k][1][i]);
+                    }
+                }
+            }
+        }
+        // (the next chunk's loads not hoisted above the sums: two gather
+        // buffers live at once spilled registers)
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < C::XC) gather(t + 1);
+        const unsigned char* wb = wl0 + (t & 1) * C::STEPW;
+#pragma unroll
+        for (int k = 0; k < HEADS; ++k) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                m = max(m, max(__float_as_uint(fabsf(a[k][0][i])), __float_as_uint(fabsf(a[k][1][i]))));
+            const int pc = sexp_ag(rowmax4(m));
+            if (pc < p) {
+#pragma unroll
+                for (int cb = 0; cb < C::NCB; ++cb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
+                p = pc;
+            }
+            const float spv = p2_ag(p);
+            f16x8 bh, bl;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = (j < 4 ? a[k][0][j] : a[k][1][j - 4]) * spv;
+                const _Float16 hh = static_cast<_Float16>(v);
+                bh[j] = hh;
+                bl[j] = static_cast<_Float16>(v - static_cast<float>(hh));
+            }
+#pragma unroll
+            for (int cb = 0; cb < C::NCB; ++cb) {
+                const unsigned char* wf = wb + k * C::WCH + (2 * cb) * AFRAG;
+                const f16x8 wh = *reinterpret_cast<const f16x8*>(wf);
+                const f16x8 wl = *reinterpret_cast<const f16x8*>(wf + AFRAG);
+                acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[cb], 0, 0, 0);
+                acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, acc[cb], 0, 0, 0);
+                acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, acc[cb], 0, 0, 0);
+            }
+            // (one head's fragments at a time: hoisting the next heads' LDS
+            // reads above these MFMAs spilled registers)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // epilogue: lane (r, g) = row r, columns 16 cb + 4 g + i
+    const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
+    const float* const xr = x + rowc * ldx + 4 * g;
+    float* const orow = out + rowc * ldo + 4 * g;
+#pragma unroll
+    for (int cb = 0; cb < C::NCB; ++cb) {
+        const int n = 16 * cb + 4 * g;
+        const int4 q = *reinterpret_cast<const int4*>(&QF[n]);
+        const f32x4 bo = *reinterpret_cast<const f32x4*>(&BF[n]);
+        const f32x4 so = *reinterpret_cast<const f32x4*>(&SC[n]);
+        const f32x4 ho = *reinterpret_cast<const f32x4*>(&SH[n]);
+        const f32x4 xv = res ? *reinterpret_cast<const f32x4*>(xr + 16 * cb) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int qn[4] = {q.x, q.y, q.z, q.w};
+        f32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
+        if (rv) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(orow + 16 * cb));
+    }
+}
+
 template <int MODE, bool CHAIN, int AW>
 int launch_agg_gemm(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                     int64_t ldx, int64_t rb, int64_t re, float self_scale, const void* img1,
@@ -394,6 +640,21 @@ int launch_agg_gemm(const int32_t* row_ptr, const int32_t* col, const float* ew,
 }
 
 int g_agg_waves = 8;     // mignn_diag_set_agg_gemm_waves (timing study: 4 or 8)
+
+template <int H>
+int launch_gat_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
+                     const float* x, int64_t ldx, int64_t rb, int64_t re, float slope,
+                     const void* img, const float* bias, const float* scale, const float* shift,
+                     int flags, float* out, int64_t ldo, hipStream_t st) {
+    using C = GatCfg<H>;
+    const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
+    const int64_t nb = (ntiles + 7) / 8 * 8;
+    MIGNN_REQUIRE(nb < (int64_t(1) << 31), "gat_fused: too many rows");
+    hipLaunchKernelGGL((gat_fused_kernel<H>), dim3(static_cast<unsigned>(nb)), dim3(C::NT), 0, st,
+                       row_ptr, col, logits, x, ldx, rb, re, slope,
+                       static_cast<const unsigned char*>(img), bias, scale, shift, flags, out, ldo);
+    return launch_status("gat_fused_kernel");
+}
 
 }  // namespace
 }  // namespace mignn
@@ -479,3 +740,21 @@ extern "C" int mignn_diag_set_agg_gemm_waves(int waves) {
     g_agg_waves = waves;
     return MIGNN_OK;
 }
+
+// the fused GAT layer (see gat_fused_kernel); called by mignn_gat_layer when
+// it has the split image of wcat, heads = 4 and h in {64, 128}
+namespace mignn {
+int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
+                    const float* x, int64_t ldx, int64_t rb, int64_t re, int h, float slope,
+                    const void* img, const float* bias, const float* scale, const float* shift,
+                    int flags, float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(aligned16(x) && aligned16(out) && aligned16(img) && ldx % 4 == 0 && ldo % 4 == 0,
+                  "gat_layer: fused path needs 16-B aligned rows");
+    MIGNN_REQUIRE(x != out, "gat_layer: in-place not supported (neighbours read x)");
+    hipStream_t st = as_stream(stream);
+    return h == 128 ? launch_gat_fused<128>(row_ptr, col, logits, x, ldx, rb, re, slope, img, bias,
+                                            scale, shift, flags, out, ldo, st)
+                    : launch_gat_fused<64>(row_ptr, col, logits, x, ldx, rb, re, slope, img, bias,
+                                           scale, shift, flags, out, ldo, st);
+}
+}  // namespace mignn

@@ -27,6 +27,8 @@ namespace {
 
 inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
+bool g_gat_fused = true;     // mignn_diag_set_gat_fused (A/B timing against the launch sequence)
+
 // the transform of either arithmetic: img != NULL -> split fp16, else fp32 w
 int transform(const float* a, int64_t lda, int64_t m, int k1, const float* a2, int64_t lda2,
               int k2, const float* w, const void* img, int n, const float* bias,
@@ -80,6 +82,12 @@ extern "C" int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const
         ld_lg = 2 * heads;
     }
     MIGNN_REQUIRE(ld_lg == 2 * heads, "gat_layer: logits must be [n, 2*heads] contiguous");
+    // split-fp16 transform, 4 heads, h in {64, 128}: aggregation and head-mean
+    // transform in one kernel (agg_gemm.hip) -- the [rows, heads h] aggregate
+    // never reaches memory
+    if (wcat_img != nullptr && heads == 4 && (h == 64 || h == 128) && g_gat_fused)
+        return gat_layer_fused(row_ptr, col, lg, x, ldx, row_begin, row_end, h, negative_slope,
+                               wcat_img, bias, scale, shift, flags, out, ldo, stream);
     float* agg = reinterpret_cast<float*>(base);
     const int64_t lda = static_cast<int64_t>(heads) * h;
     // the aggregation writes row r at agg + r * lda for r in [row_begin, row_end)
@@ -134,4 +142,9 @@ extern "C" int mignn_transformer_layer(const int32_t* row_ptr, const int32_t* co
     return transform(agg, ldq, rows, k1, x + row_begin * ldx, ldx, h, wout, wout_img, h, bout,
                      x + row_begin * ldx, ldx, scale, shift, flags, out + row_begin * ldo, ldo,
                      stream);
+}
+
+extern "C" int mignn_diag_set_gat_fused(int on) {
+    g_gat_fused = on != 0;
+    return MIGNN_OK;
 }

@@ -165,6 +165,11 @@ int gcn_fused_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
                     int64_t ldx, int64_t rb, int64_t re, int h, const float* w, const float* bias,
                     const float* scale, const float* shift, int flags, float* out, int64_t ldo,
                     void* stream, int xm = 0);
+// the fused GAT layer (agg_gemm.hip): heads = 4, h in {64, 128}, wcat image
+int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
+                    const float* x, int64_t ldx, int64_t rb, int64_t re, int h, float slope,
+                    const void* img, const float* bias, const float* scale, const float* shift,
+                    int flags, float* out, int64_t ldo, void* stream);
 int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, int n,
                 const float* bias, const float* residual, int64_t ldr, const float* scale,
                 const float* shift, int flags, float* c, int64_t ldc, hipStream_t st,

@@ -117,7 +117,11 @@ __device__ __forceinline__ void dma16_diag(const void* src, uint32_t dst) {
         : "memory");
 }
 
-template <int D>
+// VAR 0: stores in the accumulator pattern, a block barrier per step;
+// VAR 1: whole-row stores (a half-wave per 512-B row), barrier per step;
+// VAR 2: whole-row stores, no barrier (each wave DMAs exactly its own 16 rows
+//        and waits for them itself)
+template <int D, int VAR>
 __global__ __launch_bounds__(256, 1) void diag_stream_kernel(const float* __restrict__ x, int64_t n,
                                                              float* __restrict__ out) {
     constexpr int H = 128, BM = 64, ROWB = 512, XB = BM * ROWB, NPIECE = XB / 1024 / 4;
@@ -126,6 +130,10 @@ __global__ __launch_bounds__(256, 1) void diag_stream_kernel(const float* __rest
     // DMA = the stores of steps s-D+2 .. s and the DMAs of steps s+2 .. s+D-1
     constexpr int N = (D - 1) * NST + (D - 2) * NPIECE;
     constexpr int WAIT = (N & 15) | ((N >> 4) << 14) | (7 << 4);
+    // VAR 2, at the start of step s for step s's own DMA: younger = the stores
+    // of steps s-D+1 .. s-1 and the DMAs of steps s+1 .. s+D-1
+    constexpr int N2 = (D - 1) * NST + (D - 1) * NPIECE;
+    constexpr int WAIT2 = (N2 & 15) | ((N2 >> 4) << 14) | (7 << 4);
     __shared__ __attribute__((aligned(16))) unsigned char lds[D * XB];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -156,6 +164,33 @@ __global__ __launch_bounds__(256, 1) void diag_stream_kernel(const float* __rest
         issue(s + D - 1);
         const int64_t t = tile_of(s);
         const unsigned char* const X = lds + (s % D) * XB;
+        if constexpr (VAR >= 1) {
+            if constexpr (VAR == 2) {
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_s_waitcnt(WAIT2);     // my own pieces of step s landed
+                asm volatile("" ::: "memory");
+            }
+            const int ch = lane & 31;
+            f32x4 v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int lr = 16 * wave + 2 * i + (lane >> 5);
+                v[i] = *reinterpret_cast<const f32x4*>(X + lr * ROWB + 16 * (ch ^ (lr & 15)));
+            }
+            const int64_t tt = t < ntiles ? t : 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int lr = 16 * wave + 2 * i + (lane >> 5);
+                __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tt * BM + lr) * H + 4 * ch));
+            }
+            if constexpr (VAR == 1) {
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_s_waitcnt(WAIT);
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            }
+            continue;
+        }
         const int lr = 16 * wave + r;
         f32x4 v[8];
 #pragma unroll
@@ -192,11 +227,14 @@ extern "C" int mignn_diag_gather(int mode, const int32_t* row_ptr, const int32_t
     hipLaunchKernelGGL((diag_gather_kernel<M, R, T>), dim3(g), dim3(256), 0, st, row_ptr, col, ew, x, n, nx, ny, nz, out)
     if (mode >= 16) {
         MIGNN_REQUIRE(n % 64 == 0 && blocks > 0 && blocks % 8 == 0, "diag stream: n % 64, blocks % 8");
-        const int d = mode & 15;
-        if (d == 2) hipLaunchKernelGGL((diag_stream_kernel<2>), dim3(blocks), dim3(256), 0, st, x, n, out);
-        else if (d == 3) hipLaunchKernelGGL((diag_stream_kernel<3>), dim3(blocks), dim3(256), 0, st, x, n, out);
-        else if (d == 4) hipLaunchKernelGGL((diag_stream_kernel<4>), dim3(blocks), dim3(256), 0, st, x, n, out);
-        else { set_error("diag stream: depth 2..4"); return MIGNN_ERR_ARG; }
+        const int d = mode & 15, var = (mode >> 5) & 3;
+#define MIGNN_STREAM(DD, VV) \
+        if (d == DD && var == VV) hipLaunchKernelGGL((diag_stream_kernel<DD, VV>), dim3(blocks), dim3(256), 0, st, x, n, out)
+        MIGNN_STREAM(2, 0); else MIGNN_STREAM(3, 0); else MIGNN_STREAM(4, 0);
+        else MIGNN_STREAM(2, 1); else MIGNN_STREAM(3, 1); else MIGNN_STREAM(4, 1);
+        else MIGNN_STREAM(2, 2); else MIGNN_STREAM(3, 2); else MIGNN_STREAM(4, 2);
+        else { set_error("diag stream: depth 2..4, variant 0..2"); return MIGNN_ERR_ARG; }
+#undef MIGNN_STREAM
         return launch_status("diag_stream_kernel");
     }
     const int base = mode & 3;

@@ -68,18 +68,22 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // staging tile: the consumers write their accumulator blocks there and store
 // whole rows (512 B per half-wave at H = 128) instead of 16 rows x 64 B per
 // instruction
-template <int H>
+// NC: consumer waves -- 4 (one per SIMD, 32 output columns each) or 8 (two
+// per SIMD, 16 columns each: half the per-wave MFMA / epilogue chain, the two
+// waves of a SIMD overlap; 16 waves per CU, <= 128 VGPRs)
+template <int H, int NC = 4>
 struct SCfg {
     static_assert(H == 64 || H == 128, "f16x3 GCN layer: H in {64, 128}");
+    static_assert(NC == 4 || NC == 8, "consumer waves");
     static constexpr int BM = 64;                  // rows per tile
     static constexpr int NPW = 8;                  // producer waves
-    static constexpr int NCW = 4;                  // consumer waves (one per SIMD)
+    static constexpr int NCW = NC;                 // consumer waves
     static constexpr int NT = (NPW + NCW) * 64;
     static constexpr int PROWS = BM / NPW;         // rows per producer wave (8)
     static constexpr int NQD = PROWS / 4;          // row quads per producer wave
     static constexpr int F = H / 16;               // floats per lane of a row (16 lanes / row)
     static constexpr int CH = F / 4;               // 16-B chunks per lane of a row
-    static constexpr int EX = H == 128 ? 4 : 6;    // out-of-tile register slots per row
+    static constexpr int EX = H == 128 ? (NC == 8 ? 3 : 4) : 6;   // out-of-tile register slots per row
     static constexpr int UB = H == 128 ? 2 : 4;    // in-tile slots per LDS batch (H = 128: 4
                                                    // spills at 3 waves / SIMD, 8 % slower;
                                                    // H = 64: 4 is 7 % faster than 2)
@@ -89,7 +93,7 @@ struct SCfg {
     static constexpr int VPL = H / 64;             // floats per lane, row-per-wave slow path
     static constexpr int ROWB = H * 4;             // bytes per own-image row (unpadded)
     static constexpr int AS = 144;                 // A row stride, halfs (72 words = 8 mod 64)
-    static constexpr int JB = 2;                   // 16-column blocks per consumer
+    static constexpr int JB = NC == 8 ? 1 : 2;     // 16-column blocks per consumer
     static constexpr int WN = H / 16 / JB;         // consumer column groups
     static constexpr int WM = NCW / WN;            // consumer row groups
     static constexpr int IB = BM / 16 / WM;        // 16-row blocks per consumer
@@ -278,14 +282,14 @@ __device__ __forceinline__ void p_load_entries(PIdx& t, const int32_t* __restric
     t.ew = lane < ne ? ew[e0 + lane] : 0.f;
 }
 
-template <int H>
-__global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
+template <int H, int NC>
+__global__ __launch_bounds__((SCfg<H, NC>::NT)) void gcn_f16x3_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t row_begin,
     int64_t row_end, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift, int flags,
     float* __restrict__ out, int64_t ldo, unsigned long long* trace) {
-    using C = SCfg<H>;
+    using C = SCfg<H, NC>;
     constexpr int UBE = C::UB;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
     int* const cntX = reinterpret_cast<int*>(lds + C::OFF_CNT);
@@ -867,12 +871,12 @@ __global__ __launch_bounds__(SCfg<H>::NT) void gcn_f16x3_kernel(
     }
 }
 
-template <int H>
+template <int H, int NC>
 int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                  int64_t ldx, int64_t rb, int64_t re, const float* w, const float* bias,
                  const float* scale, const float* shift, int flags, float* out, int64_t ldo,
                  hipStream_t st) {
-    using C = SCfg<H>;
+    using C = SCfg<H, NC>;
     static int grid_cache[64] = {0};
     int dev = 0;
     MIGNN_HIP(hipGetDevice(&dev));
@@ -886,7 +890,7 @@ int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, co
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL((gcn_f16x3_kernel<H>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x,
+    hipLaunchKernelGGL((gcn_f16x3_kernel<H, NC>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x,
                        ldx, rb, re, w, bias, scale, shift, flags, out, ldo,
                        (flags & MIGNN_DIAG_TRACE) ? g_trace16_host : nullptr);
     return launch_status("gcn_f16x3_kernel");
@@ -942,8 +946,13 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
     MIGNN_REQUIRE(x != out, "gcn_layer_f16x3: in-place not supported (neighbours read x)");
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
-    return h == 128 ? launch_f16x3<128>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
-                                        flags, out, ldo, st)
-                    : launch_f16x3<64>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
-                                       flags, out, ldo, st);
+    if (flags & MIGNN_SCHED_NC8)
+        return h == 128 ? launch_f16x3<128, 8>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,
+                                               shift, flags, out, ldo, st)
+                        : launch_f16x3<64, 8>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale,
+                                              shift, flags, out, ldo, st);
+    return h == 128 ? launch_f16x3<128, 4>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
+                                           flags, out, ldo, st)
+                    : launch_f16x3<64, 4>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
+                                          flags, out, ldo, st);
 }

@@ -23,7 +23,8 @@ enum {
                                          default: each XCD walks a contiguous tile range) */
     MIGNN_SCHED_PRIO_CONSUMERS = 131072, /* f16x3 GCN layer: consumer waves at s_setprio 1 */
     MIGNN_SCHED_PRIO_PRODUCERS = 262144, /* f16x3 GCN layer: producer waves at s_setprio 1 */
-    MIGNN_SCHED_DMA_LATE = 524288        /* f16x3 GCN layer: own-row DMA after the epilogue */
+    MIGNN_SCHED_DMA_LATE = 524288,       /* f16x3 GCN layer: own-row DMA after the epilogue */
+    MIGNN_SCHED_NC8 = 1048576            /* f16x3 GCN layer: 8 consumer waves (16 columns each) */
 };
 /* mignn_gcn_layer / mignn_gcn_layer_f16x3 / mignn_linear with the flags above */
 int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
@@ -83,6 +84,9 @@ int mignn_gcn_layer_wave(const int32_t* row_ptr, const int32_t* col, const float
 /* Fused H = 256 layers (csrc/agg_gemm.hip): waves per block, 8 (default, one
  * 128-row block per CU) or 4 (64-row blocks, two per CU) -- timing study. */
 int mignn_diag_set_agg_gemm_waves(int waves);
+/* mignn_gat_layer: 1 (default) = the fused kernel where it applies, 0 = the
+ * aggregate + transform launches (timing study) */
+int mignn_diag_set_gat_fused(int on);
 #ifdef __cplusplus
 }
 #endif

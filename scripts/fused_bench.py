@@ -18,14 +18,16 @@ from mignn.gnn_model import build_csr, f16x3_image, gin_fused_image, linear_f16x
 from mignn.synthetic import grid_graph  # noqa: E402
 
 dev = torch.device("cuda", 0)
-H = 256
 mode = os.environ.get("FB_MODE", "gin")
+H = 128 if mode == "gat" else 256
 nx, ny, nz = (int(v) for v in os.environ.get("FB_GRID", "500,400,63").split(","))
 pos, ei = grid_graph(nx, ny, nz, device=dev)
 n = pos.shape[0]
 perm, inv = locality_order(pos, ei)
 csr = build_csr(ei, n, _lib.CSR_VERBATIM if mode == "gin" else _lib.CSR_ONE_SELF_LOOP, relabel=inv)
+E_in = int(ei.shape[1])
 del ei, pos
+res_edges = E_in
 g = torch.Generator(device=dev).manual_seed(0)
 X = torch.randn(n, H, device=dev, generator=g)
 W1 = torch.randn(H, H, device=dev, generator=g) / 16
@@ -34,10 +36,26 @@ b1 = torch.randn(H, device=dev, generator=g) * 0.05
 b2 = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
-img1, img2, img2s = f16x3_image(W1), gin_fused_image(W2), f16x3_image(W2)
+if mode == "gat":
+    WLOG = torch.randn(8, H, device=dev, generator=g) / H ** 0.5
+    WCAT = torch.randn(H, 4 * H, device=dev, generator=g) / (2 * H) ** 0.5
+    img1 = f16x3_image(WCAT)
+    GSCR = torch.empty(max(_lib.lib().mignn_gat_layer_scratch_bytes(n, n, H, 4), 1), dtype=torch.uint8,
+                       device=dev)
+else:
+    img1, img2, img2s = f16x3_image(W1), gin_fused_image(W2), f16x3_image(W2)
 L = _lib.lib()
 P = _lib.ptr
 st = _lib.stream()
+
+
+def gat(on):
+    def f(Y):
+        _lib.check(L.mignn_diag_set_gat_fused(on), "gat_fused")
+        _lib.check(L.mignn_gat_layer(P(csr.row_ptr), P(csr.col), P(X), H, n, 0, n, H, 4, 0.2,
+                                     P(WLOG), None, 8, P(WCAT), P(img1), P(b1), P(sc), P(sh), 15,
+                                     P(GSCR), GSCR.numel(), P(Y), H, st), "gat_layer")
+    return f
 
 
 def fused(waves):
@@ -70,7 +88,8 @@ def unfused(Y):
         linear_f16x3(AGG, img1, H, b1, relu=True, residual=X, scale=sc, shift=sh, out=Y)
 
 
-cases = {"unfused": unfused, "fused_w8": fused(8), "fused_w4": fused(4)}
+cases = ({"unfused": gat(0), "fused": gat(1)} if mode == "gat" else
+         {"unfused": unfused, "fused_w8": fused(8), "fused_w4": fused(4)})
 outs = {k: torch.full_like(X, float("nan")) for k in cases}
 for k, f in cases.items():
     f(outs[k])
@@ -97,7 +116,7 @@ for rnd in range(reps + 1):
 res["ms"] = {k: round(statistics.median(v), 4) for k, v in times.items()}
 E = int(csr.row_ptr[-1].item())
 by = 4 * (2 * n * H + (n + 1) + E)
-fl = (4 if mode == "gin" else 2) * n * H * H * 3
+fl = {"gin": 4, "gcn": 2, "gat": 8}[mode] * n * H * H * 3
 res["frac_hbm"] = {k: round(by / (v * 1e-3) / 8e12, 4) for k, v in res["ms"].items()}
 res["f16_tflops"] = {k: round(fl / (v * 1e-3) / 1e12, 1) for k, v in res["ms"].items()}
 print(json.dumps(res), flush=True)

@@ -11,3 +11,5 @@ timeout -k 10 300 python -u scripts/fused_bench.py > gpurun_out/fused_gin.json 2
 rc=$?; cat gpurun_out/fused_gin.json; if [ $rc -ne 0 ]; then tail -20 gpurun_out/fused_gin.err; exit $rc; fi
 FB_MODE=gcn FB_GRID=250,200,200 timeout -k 10 300 python -u scripts/fused_bench.py > gpurun_out/fused_gcn.json 2> gpurun_out/fused_gcn.err
 rc=$?; cat gpurun_out/fused_gcn.json; if [ $rc -ne 0 ]; then tail -20 gpurun_out/fused_gcn.err; exit $rc; fi
+FB_MODE=gat FB_GRID=100,100,100 timeout -k 10 300 python -u scripts/fused_bench.py > gpurun_out/fused_gat.json 2> gpurun_out/fused_gat.err
+rc=$?; cat gpurun_out/fused_gat.json; if [ $rc -ne 0 ]; then tail -20 gpurun_out/fused_gat.err; exit $rc; fi

@@ -69,9 +69,23 @@ def stream(d, blocks):
 if H == 128:          # mignn_diag_gather's copy is written for 128-float rows
     cases["diag_copy"] = copy
     for d in [int(v) for v in os.environ.get("HB_STREAM", "").split(",") if v]:
-        cases[f"stream_d{d}"] = stream(d, 256)
+        for nb in [int(v) for v in os.environ.get("HB_STREAM_BLOCKS", "256").split(",")]:
+            for var in [int(v) for v in os.environ.get("HB_STREAM_VARS", "0").split(",")]:
+                cases[f"stream_d{d}_b{nb}_v{var}"] = stream(d | (var << 5), nb)
 for v in variants:
     cases[f"wave_v{v}"] = wave(v)
+
+
+def diagf(extra):
+    def f(Y):
+        _lib.check(L.mignn_diag_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n,
+                                                H, P(W), P(b), P(sc), P(sh), FL | extra, P(Y), H, st),
+                   "diag")
+    return f
+
+
+for ex in [int(v) for v in os.environ.get("HB_DIAGFLAGS", "").split(",") if v]:
+    cases[f"diag_{ex}"] = diagf(ex)
 res = {"grid": [nx, ny, nz], "H": H, "n": n}
 PMC = os.environ.get("HB_PMC") == "1"
 if PMC:                      # profiled passes: each case twice, nothing else

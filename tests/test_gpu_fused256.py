@@ -194,3 +194,65 @@ def test_fused_block_shapes_agree(waves):
     _lib.check(L.mignn_diag_set_agg_gemm_waves(8), "waves")
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+def _gat_layer(csr, x, n_x, rb, re, h, wlog, wcat, img, bias, sc, sh, flags, out):
+    L = _lib.lib()
+    P = _lib.ptr
+    nb = L.mignn_gat_layer_scratch_bytes(n_x, re - rb, h, 4)
+    scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=DEV)
+    _lib.check(L.mignn_gat_layer(P(csr.row_ptr), P(csr.col), P(x), x.stride(0), n_x, rb, re, h, 4,
+                                 0.2, P(wlog), None, 8, P(wcat), P(img), P(bias), P(sc), P(sh),
+                                 flags, P(scratch), nb, P(out), out.stride(0), _lib.stream()),
+               "gat_layer")
+
+
+@pytest.mark.parametrize("h", [64, 128])
+@pytest.mark.parametrize("flags", [15, 1 | 2])
+def test_gat_fused_vs_launches_and_fp64(h, flags):
+    """mignn_gat_layer's fused kernel (split-fp16 image given, 4 heads) against
+    its aggregate + transform launch sequence (mignn_diag_set_gat_fused(0))
+    and against a float64 restatement (PyG GATConv semantics on the CSR:
+    LeakyReLU(0.2) logits, softmax + 1e-16, head mean, bias) on a graph with
+    hub rows (the kernel's past-the-slots path) and a row sub-range."""
+    n = 4000
+    rb, re = 33, 3967
+    ei = _graph(n, 21)
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
+    g = torch.Generator(device=DEV).manual_seed(h + flags)
+    x = torch.randn(n, h, device=DEV, generator=g)
+    wlog = torch.randn(8, h, device=DEV, generator=g) / h ** 0.5
+    wcat = torch.randn(h, 4 * h, device=DEV, generator=g) / (2 * h) ** 0.5
+    bias = torch.randn(h, device=DEV, generator=g) * 0.1
+    sc = torch.rand(h, device=DEV, generator=g) + 0.5
+    sh = torch.randn(h, device=DEV, generator=g) * 0.1
+    img = f16x3_image(wcat)
+    outs = []
+    for fused in (1, 0):
+        _lib.check(_lib.lib().mignn_diag_set_gat_fused(fused), "gat_fused")
+        o = torch.full((n, h), float("nan"), device=DEV)
+        _gat_layer(csr, x, n, rb, re, h, wlog, wcat, img, bias, sc, sh, flags, o)
+        outs.append(o)
+    _lib.check(_lib.lib().mignn_diag_set_gat_fused(1), "gat_fused")
+    torch.cuda.synchronize()
+    got, launches = outs[0].cpu(), outs[1].cpu()
+    assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
+    # float64 restatement on the same CSR
+    col, dst = _csr_edges(csr, n)
+    X = x.double().cpu()
+    lg = X @ wlog.double().cpu().T                                   # [n, 8]
+    s = lg[col, :4] + lg[dst, 4:]
+    s = torch.where(s > 0, s, 0.2 * s)
+    mx = torch.full((n, 4), -float("inf"), dtype=torch.float64).scatter_reduce(
+        0, dst[:, None].expand_as(s), s, "amax", include_self=True)
+    pexp = torch.exp(s - mx[dst])
+    sm = torch.zeros((n, 4), dtype=torch.float64).index_add_(0, dst, pexp) + 1e-16
+    alpha = pexp / sm[dst]                                          # [E, 4]
+    agg = torch.zeros((n, 4, h), dtype=torch.float64).index_add_(
+        0, dst, alpha[:, :, None] * X[col][:, None, :]).reshape(n, 4 * h)
+    aggm = torch.zeros((n, 4, h), dtype=torch.float64).index_add_(
+        0, dst, alpha[:, :, None] * X[col].abs()[:, None, :]).reshape(n, 4 * h)
+    W = wcat.double().cpu()
+    ref, mag = _epi64(agg @ W.T, aggm @ W.T.abs(), X, bias.cpu(), sc.cpu(), sh.cpu(), flags)
+    _check(got[rb:re], ref[rb:re], mag[rb:re], f"gat fused h={h}")
+    _check(launches[rb:re], ref[rb:re], mag[rb:re], f"gat launches h={h}")
