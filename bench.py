@@ -248,7 +248,9 @@ def main():
     deg_plus_self = E_local / N_local + 1.0
     traffic = None
     tf = os.path.join(HERE, "profiles", "gcn_layer_traffic.json")
-    if os.path.exists(tf):
+    # (the PMC record is of the single-GPU launch over the whole mesh; at N > 1
+    # a rank's launches cover its interior / boundary row ranges: no record)
+    if os.path.exists(tf) and world == 1:
         try:
             with open(tf) as fh:
                 tj = json.load(fh)

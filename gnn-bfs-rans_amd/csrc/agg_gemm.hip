@@ -93,25 +93,51 @@ __device__ __forceinline__ void chunk_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// (two waves per SIMD: <= 256 VGPRs; AW = 4 -> two blocks per CU)
-template <int MODE, bool CHAIN, int AW>
-__global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) void agg_gemm_kernel(
+// s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier (N < 16)
+template <int N>
+__device__ __forceinline__ void vm_barrier() {
+    static_assert(N >= 0 && N < 16, "vmcnt");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x70 | N);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// Block: 8 waves x 16 rows = a 128-row tile (two 4x4x4 blocks of the
+// locality order), one block per CU (LDS 160 KB):
+//   W ring   [2][32 KB]   the streamed W chunks (LDS-DMA, one chunk ahead)
+//   own ring [3][16 KB]   chunk kc of the tile's own rows (LDS-DMA, two
+//                         chunks ahead); 16-B segment s of local row li at
+//                         position (s + li) & 7 (bank spread)
+//   ext      [8][3][2][1 KB]  per wave: chunk kc of each row's out-of-tile
+//                         neighbours, up to ES = 3 per row (LDS-DMA with
+//                         per-lane addresses, one chunk ahead)
+// Every load of the chunk loop is an LDS-DMA the compiler does not track, so
+// the counted waits are exact: at the top of step kc everything but the own
+// rows of chunk kc+1 (the youngest 2 pieces) must have landed.  A row whose
+// first AS entries hold more than ES out-of-tile ones, or with more than AS
+// entries, takes all its entries one at a time (correct, not fast).
+template <int MODE, bool CHAIN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void agg_gemm_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t rb,
     int64_t re, float self_scale, const unsigned char* __restrict__ img1,
     const float* __restrict__ b1, const unsigned char* __restrict__ img2,
     const float* __restrict__ b2, const float* __restrict__ scale,
     const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
-    constexpr int NT = AW * 64;
-    constexpr int BM = 16 * AW;
+    constexpr int AW = 8, BM = 16 * AW;
     constexpr int NC = AKP * (CHAIN ? 2 : 1);          // W chunks streamed per tile
-    __shared__ __attribute__((aligned(16))) unsigned char lds[2 * ACHUNK + 6 * AH * 4];
-    int32_t* const Q1 = reinterpret_cast<int32_t*>(lds + 2 * ACHUNK);   // W1 column exponents
-    float* const B1 = reinterpret_cast<float*>(Q1 + AH);               // GIN: nn.0 bias
-    int32_t* const QF = reinterpret_cast<int32_t*>(B1 + AH);            // final transform's exponents
-    float* const BF = reinterpret_cast<float*>(QF + AH);               // final bias (0 without BIAS)
-    float* const SC = BF + AH;                                          // BN scale (1) / shift (0)
-    float* const SH = SC + AH;
+    constexpr int OWNB = BM * 128;                      // one own-row chunk slice
+    constexpr int ES = 3;                               // out-of-tile slots per row
+    constexpr int EXTB = ES * 2 * 1024;                 // per wave
+    constexpr int OFF_OWN = 2 * ACHUNK;
+    constexpr int OFF_EXT = OFF_OWN + 3 * OWNB;
+    constexpr int LDS_BYTES = OFF_EXT + AW * EXTB;
+    static_assert(LDS_BYTES <= 160 * 1024, "agg_gemm LDS");
+    constexpr int WPC = ACHUNK / 1024 / AW;             // W pieces per wave per chunk (4)
+    constexpr int OPC = OWNB / 1024 / AW;               // own-row pieces per wave per chunk (2)
+    constexpr size_t FB = static_cast<size_t>(AKP) * ACB * 2 * AFRAG;   // image exponent table
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
 
     const int tid = threadIdx.x;
     int lane = tid & 63;
@@ -125,65 +151,98 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int64_t per_xcd = gridDim.x >> 3;
     const int64_t tile = static_cast<int64_t>(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
     if (tile >= ntiles) return;
-    const int64_t row = rb + tile * BM + 16 * wave + r;
+    const int64_t t0 = rb + tile * BM;
+    const int nloc = static_cast<int>(re - t0 < BM ? re - t0 : BM);
+    const int64_t row = t0 + 16 * wave + r;
     const bool rv = row < re;
     const int64_t rowc = rv ? row : re - 1;
+    const int lself = 16 * wave + r;
 
-    // W chunk c (W1 chunks, then W2's) -> LDS buffer c & 1: 32 pieces of 1 KB
-    auto w_dma = [&](int c) {
-        if (c >= NC) return;
+    // ---- LDS-DMA streams
+    auto w_dma = [&](int c) {                  // W chunk c (W1's, then W2's) -> buffer c & 1
+        if (c >= NC || (flags & MIGNN_SCHED_INTERLEAVED)) return;
         const unsigned char* src = c < AKP ? img1 + static_cast<size_t>(c) * ACHUNK
                                            : img2 + static_cast<size_t>(c - AKP) * ACHUNK;
         unsigned char* dst = lds + (c & 1) * ACHUNK;
 #pragma unroll
-        for (int pc = 0; pc < ACHUNK / 1024 / AW; ++pc) {
+        for (int pc = 0; pc < WPC; ++pc) {
             const int piece = wave + pc * AW;
             glds16_ag(src + piece * 1024 + lane * 16, lds_addr_ag(dst + piece * 1024));
         }
     };
-    w_dma(0);
+    auto own_dma = [&](int kc, int buf) {      // own rows' chunk kc -> ring buffer buf
+        const int kk = kc < AKP ? kc : AKP - 1;    // (past the last chunk: a dummy refill
+        unsigned char* dst = lds + OFF_OWN + buf * OWNB;   // of a free buffer: the count stays fixed)
+        int l = lane;
+        asm volatile("" : "+v"(l));
+#pragma unroll
+        for (int pc = 0; pc < OPC; ++pc) {
+            const int piece = wave + pc * AW;
+            const int li = 8 * piece + (l >> 3), sg = ((l & 7) - li) & 7;
+            int64_t rr = t0 + li;
+            if (rr >= re) rr = re - 1;                 // any valid row: never read
+            glds16_ag(x + rr * ldx + 32 * kk + 4 * sg, lds_addr_ag(dst + piece * 1024));
+        }
+    };
 
-    // per-column vectors of the epilogues
-    if (tid < AH) {
-        constexpr size_t FB = static_cast<size_t>(AKP) * ACB * 2 * AFRAG;
-        Q1[tid] = reinterpret_cast<const int32_t*>(img1 + FB)[tid];
-        B1[tid] = CHAIN ? b1[tid] : 0.f;
-        QF[tid] = reinterpret_cast<const int32_t*>((CHAIN ? img2 : img1) + FB)[tid];
-        BF[tid] = (flags & MIGNN_EPI_BIAS) ? (CHAIN ? b2 : b1)[tid] : 0.f;
-        SC[tid] = (flags & MIGNN_EPI_AFFINE) ? scale[tid] : 1.f;
-        SH[tid] = (flags & MIGNN_EPI_AFFINE) ? shift[tid] : 0.f;
-    }
-
-    // the row's CSR entries (first AS in registers; empty slots -> the zero row)
+    // ---- the row's CSR entries: per slot e < AS a code -- local row li (in
+    // this tile), 256 + k (the row's k-th out-of-tile entry, column xc[k]),
+    // -1 (empty); rows the slots cannot hold take the slow path
     const int e0 = row_ptr[rowc];
     const int deg = rv ? row_ptr[rowc + 1] - e0 : 0;
-    const float* src[AS];
+    int code[AS];
     float wgt[AS];
+    int xc[ES];
+#pragma unroll
+    for (int k = 0; k < ES; ++k) xc[k] = -1;
+    int next = 0;
 #pragma unroll
     for (int e = 0; e < AS; ++e) {
         const int c = e < deg ? col[e0 + e] : -1;
-        src[e] = c >= 0 ? x + static_cast<int64_t>(c) * ldx + 8 * g : g_zero_row_ag + 8 * g;
         wgt[e] = (MODE == AGG_GCN && e < deg) ? ew[e0 + e] : 0.f;
-    }
-    const float* const xself = x + rowc * ldx + 8 * g;
-    // wave-uniform: does any row have entries past the register slots?
-    const bool extra = __builtin_amdgcn_ballot_w64(deg > AS) != 0ull;
-
-    // one chunk's gathered values: AS entries (+ GIN's own row), 8 floats each
-    constexpr int NV = AS + (MODE == AGG_GIN ? 1 : 0);
-    f32x4 gv[NV][2];
-    auto gather = [&](int kc) {
+        const uint32_t off = static_cast<uint32_t>(c - static_cast<int>(t0));
+        if (c < 0) {
+            code[e] = -1;
+        } else if (off < static_cast<uint32_t>(nloc)) {
+            code[e] = static_cast<int>(off);
+        } else {
+            code[e] = 256 + next;
 #pragma unroll
-        for (int e = 0; e < AS; ++e) {
-            gv[e][0] = *reinterpret_cast<const f32x4*>(src[e] + 32 * kc);
-            gv[e][1] = *reinterpret_cast<const f32x4*>(src[e] + 32 * kc + 4);
+            for (int k = 0; k < ES; ++k)
+                if (k == next) xc[k] = c;
+            ++next;
         }
-        if constexpr (MODE == AGG_GIN) {
-            gv[AS][0] = *reinterpret_cast<const f32x4*>(xself + 32 * kc);
-            gv[AS][1] = *reinterpret_cast<const f32x4*>(xself + 32 * kc + 4);
-        }
+    }
+    const bool slow = deg > AS || next > ES;
+    if (slow) {
+#pragma unroll
+        for (int e = 0; e < AS; ++e) code[e] = -1;
+#pragma unroll
+        for (int k = 0; k < ES; ++k) xc[k] = -1;
+    }
+    const bool any_slow = __builtin_amdgcn_ballot_w64(slow) != 0ull;
+    unsigned char* const EXT = lds + OFF_EXT + wave * EXTB;
+    // (slots no row of the wave uses are skipped: only the own rows' refill,
+    // issued last, is counted by the waits)
+    bool xs_used[ES];
+#pragma unroll
+    for (int k = 0; k < ES; ++k) xs_used[k] = __builtin_amdgcn_ballot_w64(xc[k] >= 0) != 0ull;
+    auto ext_dma = [&](int kc) {               // chunk kc of the row's out-of-tile entries
+#pragma unroll
+        for (int k = 0; k < ES; ++k)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (!xs_used[k]) continue;
+                const float* sp = xc[k] >= 0 ? x + static_cast<int64_t>(xc[k]) * ldx + 32 * kc + 8 * g + 4 * h
+                                             : g_zero_row_ag + 32 * kc + 8 * g + 4 * h;
+                glds16_ag(sp, lds_addr_ag(EXT + (2 * k + h) * 1024));
+            }
     };
-    gather(0);
+
+    own_dma(0, 0);
+    own_dma(1, 1);
+    w_dma(0);
+    ext_dma(0);
 
     f32x4 acc[ACB];
 #pragma unroll
@@ -194,26 +253,50 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     // ---------------------------------------------------------------- transform 1
 #pragma unroll 1
     for (int kc = 0; kc < AKP; ++kc) {
-        chunk_barrier();                           // W chunk kc and this chunk's rows landed
+        // chunk kc's W, own rows and out-of-tile rows landed (only the own rows
+        // of chunk kc+1 may fly), every wave done with the buffers refilled below
+        if (kc == 0) vm_barrier<0>();
+        else vm_barrier<OPC>();
         w_dma(kc + 1);                             // into the buffer chunk kc-1 used
+        const unsigned char* const ob = lds + OFF_OWN + (kc % 3) * OWNB;
         // the aggregate's 8 values of this chunk (CSR order)
         f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+        const bool dsum = !(flags & MIGNN_DIAG_NO_PRODUCE);
 #pragma unroll
         for (int e = 0; e < AS; ++e) {
+            if (!dsum) break;
+            const int c = code[e];
+            uint32_t ad0, ad1;                     // LDS byte offsets of the 2 x 16 B
+            if (c >= 256) {
+                ad0 = static_cast<uint32_t>(OFF_EXT + wave * EXTB + (2 * (c - 256)) * 1024 + lane * 16);
+                ad1 = ad0 + 1024;
+            } else {
+                const int li = c < 0 ? 0 : c;
+                const uint32_t rp = static_cast<uint32_t>(OFF_OWN + (kc % 3) * OWNB + li * 128);
+                ad0 = rp + 16 * ((2 * g + li) & 7);
+                ad1 = rp + 16 * ((2 * g + 1 + li) & 7);
+            }
+            f32x4 v0 = *reinterpret_cast<const f32x4*>(lds + ad0);
+            f32x4 v1 = *reinterpret_cast<const f32x4*>(lds + ad1);
+            if (c < 0) {
+                v0 = f32x4{0.f, 0.f, 0.f, 0.f};
+                v1 = v0;
+            }
             if constexpr (MODE == AGG_GCN) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    a0[i] = fmaf(wgt[e], gv[e][0][i], a0[i]);
-                    a1[i] = fmaf(wgt[e], gv[e][1][i], a1[i]);
+                    a0[i] = fmaf(wgt[e], v0[i], a0[i]);
+                    a1[i] = fmaf(wgt[e], v1[i], a1[i]);
                 }
             } else {
-                a0 += gv[e][0];
-                a1 += gv[e][1];
+                a0 += v0;
+                a1 += v1;
             }
+            if ((e & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
-        if (extra) {
-            // entries past the register slots, one at a time (CSR order)
-            for (int e = AS; e < deg; ++e) {
+        if (any_slow && slow) {
+            // every entry of the row, one at a time (CSR order)
+            for (int e = 0; e < deg; ++e) {
                 const int c = col[e0 + e];
                 const float w = MODE == AGG_GCN ? ew[e0 + e] : 1.f;
                 const float* sp = x + static_cast<int64_t>(c) * ldx + 8 * g + 32 * kc;
@@ -227,14 +310,20 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
             }
         }
         if constexpr (MODE == AGG_GIN) {
+            const unsigned char* rp = ob + lself * 128;
+            const f32x4 s0 = *reinterpret_cast<const f32x4*>(rp + 16 * ((2 * g + lself) & 7));
+            const f32x4 s1 = *reinterpret_cast<const f32x4*>(rp + 16 * ((2 * g + 1 + lself) & 7));
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                a0[i] = fmaf(self_scale, gv[AS][0][i], a0[i]);
-                a1[i] = fmaf(self_scale, gv[AS][1][i], a1[i]);
+                a0[i] = fmaf(self_scale, s0[i], a0[i]);
+                a1[i] = fmaf(self_scale, s1[i], a1[i]);
             }
         }
-        // the next chunk's rows fly while this chunk's MFMAs run
-        if (kc + 1 < AKP) gather(kc + 1);
+        // refills: this wave's out-of-tile rows of chunk kc+1 (its reads of
+        // the ext buffer above are issued: an LDS-DMA does not overtake them),
+        // the own rows of chunk kc+2 into the buffer chunk kc-1 used
+        if (kc + 1 < AKP && !(flags & MIGNN_DIAG_NO_EXT)) ext_dma(kc + 1);
+        if (!(flags & MIGNN_DIAG_NO_TABLES)) own_dma(kc + 2, (kc + 2) % 3);
         // split with the row's online exponent
         uint32_t m = 0;
 #pragma unroll
@@ -248,11 +337,11 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
                 for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
             p = pc;
         }
-        const float sp = p2_ag(p);
+        const float spv = p2_ag(p);
         f16x8 bh, bl;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float v = (j < 4 ? a0[j] : a1[j - 4]) * sp;
+            const float v = (j < 4 ? a0[j] : a1[j - 4]) * spv;
             const _Float16 hh = static_cast<_Float16>(v);
             bh[j] = hh;
             bl[j] = static_cast<_Float16>(v - static_cast<float>(hh));
@@ -260,6 +349,7 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         const unsigned char* wb = wl0 + (kc & 1) * ACHUNK;
 #pragma unroll
         for (int cb = 0; cb < ACB; ++cb) {
+            if (flags & MIGNN_DIAG_NO_MFMA) break;
             const f16x8 wh = *reinterpret_cast<const f16x8*>(wb + (2 * cb) * AFRAG);
             const f16x8 wl = *reinterpret_cast<const f16x8*>(wb + (2 * cb + 1) * AFRAG);
             acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[cb], 0, 0, 0);
@@ -272,11 +362,12 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         // ------------------------------------------------------------ transform 2
         // h = relu(acc 2^-(p + q1) + b1) in the accumulator layout: lane (r, g)
         // holds h[r][16 cb + 4 g + i]; one exponent per row over all 256
+        const int32_t* const q1 = reinterpret_cast<const int32_t*>(img1 + FB);
         uint32_t m = 0;
 #pragma unroll
         for (int cb = 0; cb < ACB; ++cb) {
-            const int4 q = *reinterpret_cast<const int4*>(&Q1[16 * cb + 4 * g]);
-            const f32x4 bb = *reinterpret_cast<const f32x4*>(&B1[16 * cb + 4 * g]);
+            const int4 q = *reinterpret_cast<const int4*>(q1 + 16 * cb + 4 * g);
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(b1 + 16 * cb + 4 * g);
             const int qn[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -287,13 +378,13 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
             }
         }
         p = sexp_ag(rowmax4(m));
-        const float sp = p2_ag(p);
+        const float spv = p2_ag(p);
         f16x8 hh[AKP], hl[AKP];
 #pragma unroll
         for (int kc = 0; kc < AKP; ++kc)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float v = acc[2 * kc + (j >> 2)][j & 3] * sp;
+                const float v = acc[2 * kc + (j >> 2)][j & 3] * spv;
                 const _Float16 t = static_cast<_Float16>(v);
                 hh[kc][j] = t;
                 hl[kc][j] = static_cast<_Float16>(v - static_cast<float>(t));
@@ -302,11 +393,12 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kc = 0; kc < AKP; ++kc) {
-            chunk_barrier();                       // W2 chunk kc landed
+            vm_barrier<0>();                       // W2 chunk kc landed
             w_dma(AKP + kc + 1);
             const unsigned char* wb = wl0 + ((AKP + kc) & 1) * ACHUNK;
 #pragma unroll
             for (int cb = 0; cb < ACB; ++cb) {
+                if (flags & MIGNN_DIAG_NO_MFMA) break;
                 const f16x8 wh = *reinterpret_cast<const f16x8*>(wb + (2 * cb) * AFRAG);
                 const f16x8 wl = *reinterpret_cast<const f16x8*>(wb + (2 * cb + 1) * AFRAG);
                 acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, hh[kc], acc[cb], 0, 0, 0);
@@ -317,27 +409,74 @@ __global__ __launch_bounds__(AW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
 
     // -------------------------------------------------------------------- epilogue
-    // lane (r, g): row r, columns 16 cb + 4 g + i; bias, residual x_i, BN, ReLU
-    // (gnn_model.py:184-191 order: conv + bias, + x, BN, ReLU)
+    // drain (no LDS-DMA may land after the loop: the dummy own-row refills),
+    // then the whole LDS is free: staging rows [BM][1 KB] | epilogue vectors.
+    // Each wave DMAs its 16 own rows in whole (the residual), every lane
+    // replaces its 64 values -- rows r, columns 16 cb + 4 g + i: bias,
+    // residual, BN, ReLU (gnn_model.py:184-191 order: conv + bias, + x, BN,
+    // ReLU) -- in place, and the wave stores whole 1-KB rows (the accumulator
+    // layout would store 16 rows x 64 B per instruction).  16-B chunk c of
+    // staging row li at position c ^ (li & 15).
+    vm_barrier<0>();
     const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
-    const float* const xr = x + rowc * ldx + 4 * g;
-    float* const orow = out + rowc * ldo + 4 * g;
+    const bool hb = (flags & MIGNN_EPI_BIAS) != 0, ha = (flags & MIGNN_EPI_AFFINE) != 0;
+    if (flags & MIGNN_DIAG_NO_LOCAL) {         // (ablation: no epilogue)
+        if (rv && acc[0][0] == 12345.f) out[rowc * ldo] = acc[1][1];
+        return;
+    }
+    unsigned char* const STG = lds;
+    float* const EV = reinterpret_cast<float*>(lds + BM * 1024);   // q | bias | scale | shift
+    if (tid < AH) {
+        const int32_t* const qf = reinterpret_cast<const int32_t*>((CHAIN ? img2 : img1) + FB);
+        const float* const bf = CHAIN ? b2 : b1;
+        reinterpret_cast<int32_t*>(EV)[tid] = qf[tid];
+        EV[AH + tid] = hb ? bf[tid] : 0.f;
+        EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
+        EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
+    }
+    if (res) {
+        int l = lane;
+        asm volatile("" : "+v"(l));
 #pragma unroll
-    for (int cb = 0; cb < ACB; ++cb) {
-        const int n = 16 * cb + 4 * g;
-        const int4 q = *reinterpret_cast<const int4*>(&QF[n]);
-        const f32x4 bo = *reinterpret_cast<const f32x4*>(&BF[n]);
-        const f32x4 so = *reinterpret_cast<const f32x4*>(&SC[n]);
-        const f32x4 ho = *reinterpret_cast<const f32x4*>(&SH[n]);
-        const f32x4 xv = res ? *reinterpret_cast<const f32x4*>(xr + 16 * cb) : f32x4{0.f, 0.f, 0.f, 0.f};
-        const int qn[4] = {q.x, q.y, q.z, q.w};
-        f32x4 o;
+        for (int i = 0; i < 16; ++i) {
+            const int li = 16 * wave + i;
+            int64_t rr = t0 + li;
+            if (rr >= re) rr = re - 1;
+            glds16_ag(x + rr * ldx + 4 * (l ^ (li & 15)), lds_addr_ag(STG + li * 1024));
+        }
+    }
+    vm_barrier<0>();
+    {
+        unsigned char* const srow = STG + lself * 1024;
+        const int32_t* const EQ = reinterpret_cast<const int32_t*>(EV);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
-        if (rv) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(orow + 16 * cb));
+        for (int cb = 0; cb < ACB; ++cb) {
+            const int n = 16 * cb + 4 * g;
+            f32x4* const slot = reinterpret_cast<f32x4*>(srow + 16 * ((4 * cb + g) ^ (lself & 15)));
+            const f32x4 xv = res ? *slot : f32x4{0.f, 0.f, 0.f, 0.f};
+            const int4 q = *reinterpret_cast<const int4*>(EQ + n);
+            const f32x4 bo = *reinterpret_cast<const f32x4*>(EV + AH + n);
+            const f32x4 so = *reinterpret_cast<const f32x4*>(EV + 2 * AH + n);
+            const f32x4 ho = *reinterpret_cast<const f32x4*>(EV + 3 * AH + n);
+            const int qn[4] = {q.x, q.y, q.z, q.w};
+            f32x4 o;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
+            *slot = o;
+        }
+    }
+    // this wave's 16 rows out (its own staging rows: in-order LDS)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int li = 16 * wave + i;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(STG + li * 1024 + lane * 16);
+        if (t0 + li < re)
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + li) * ldo + 4 * (lane ^ (li & 15))));
     }
 }
+
+int g_fused_diag_flags = 0;   // mignn_diag_set_fused_flags (timing ablations; wrong results)
 
 // k-permuted split image of W2 [256, 256] for the chained transform: element
 // j of lane (m, g) in fragment (kc, cb) = W2[16 cb + m][16 (2 kc + j / 4) +
@@ -623,23 +762,22 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     }
 }
 
-template <int MODE, bool CHAIN, int AW>
+template <int MODE, bool CHAIN>
 int launch_agg_gemm(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                     int64_t ldx, int64_t rb, int64_t re, float self_scale, const void* img1,
                     const float* b1, const void* img2, const float* b2, const float* scale,
                     const float* shift, int flags, float* out, int64_t ldo, hipStream_t st) {
-    constexpr int BM = 16 * AW;
+    constexpr int BM = 128;
     const int64_t ntiles = (re - rb + BM - 1) / BM;
     const int64_t nb = (ntiles + 7) / 8 * 8;
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "agg_gemm: too many rows");
-    hipLaunchKernelGGL((agg_gemm_kernel<MODE, CHAIN, AW>), dim3(static_cast<unsigned>(nb)),
-                       dim3(AW * 64), 0, st, row_ptr, col, ew, x, ldx, rb, re, self_scale,
+    hipLaunchKernelGGL((agg_gemm_kernel<MODE, CHAIN>), dim3(static_cast<unsigned>(nb)), dim3(512),
+                       0, st, row_ptr, col, ew, x, ldx, rb, re, self_scale,
                        static_cast<const unsigned char*>(img1), b1,
                        static_cast<const unsigned char*>(img2), b2, scale, shift, flags, out, ldo);
     return launch_status("agg_gemm_kernel");
 }
 
-int g_agg_waves = 8;     // mignn_diag_set_agg_gemm_waves (timing study: 4 or 8)
 
 template <int H>
 int launch_gat_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
@@ -709,10 +847,8 @@ extern "C" int mignn_gin_layer_fused(const int32_t* row_ptr, const int32_t* col,
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
     const float s = 1.0f + eps;
-    if (g_agg_waves == 4)
-        return launch_agg_gemm<AGG_GIN, true, 4>(row_ptr, col, nullptr, x, ldx, rb, re, s, img1, b1,
-                                                 img2, b2, scale, shift, flags, out, ldo, st);
-    return launch_agg_gemm<AGG_GIN, true, 8>(row_ptr, col, nullptr, x, ldx, rb, re, s, img1, b1,
+    flags |= g_fused_diag_flags;
+    return launch_agg_gemm<AGG_GIN, true>(row_ptr, col, nullptr, x, ldx, rb, re, s, img1, b1,
                                              img2, b2, scale, shift, flags, out, ldo, st);
 }
 
@@ -728,18 +864,11 @@ extern "C" int mignn_gcn_layer_fused(const int32_t* row_ptr, const int32_t* col,
     MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bias, "gcn_layer_fused: bias");
     if (re == rb) return MIGNN_OK;
     hipStream_t st = as_stream(stream);
-    if (g_agg_waves == 4)
-        return launch_agg_gemm<AGG_GCN, false, 4>(row_ptr, col, ew, x, ldx, rb, re, 1.f, img, bias,
-                                                  nullptr, nullptr, scale, shift, flags, out, ldo, st);
-    return launch_agg_gemm<AGG_GCN, false, 8>(row_ptr, col, ew, x, ldx, rb, re, 1.f, img, bias,
+    flags |= g_fused_diag_flags;
+    return launch_agg_gemm<AGG_GCN, false>(row_ptr, col, ew, x, ldx, rb, re, 1.f, img, bias,
                                               nullptr, nullptr, scale, shift, flags, out, ldo, st);
 }
 
-extern "C" int mignn_diag_set_agg_gemm_waves(int waves) {
-    MIGNN_REQUIRE(waves == 4 || waves == 8, "set_agg_gemm_waves: 4 or 8");
-    g_agg_waves = waves;
-    return MIGNN_OK;
-}
 
 // the fused GAT layer (see gat_fused_kernel); called by mignn_gat_layer when
 // it has the split image of wcat, heads = 4 and h in {64, 128}
@@ -758,3 +887,10 @@ int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* log
                                            scale, shift, flags, out, ldo, st);
 }
 }  // namespace mignn
+
+extern "C" int mignn_diag_set_fused_flags(int flags) {
+    g_fused_diag_flags = flags & (MIGNN_DIAG_NO_PRODUCE | MIGNN_DIAG_NO_MFMA | MIGNN_DIAG_NO_EXT |
+                                  MIGNN_DIAG_NO_TABLES | MIGNN_DIAG_NO_LOCAL |
+                                  MIGNN_SCHED_INTERLEAVED);
+    return MIGNN_OK;
+}

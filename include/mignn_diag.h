@@ -81,9 +81,12 @@ int mignn_gcn_layer_wave(const int32_t* row_ptr, const int32_t* col, const float
                          const float* w, const float* bias, const float* scale,
                          const float* shift, int flags, float* out, int64_t ldo, int variant,
                          void* stream);
-/* Fused H = 256 layers (csrc/agg_gemm.hip): waves per block, 8 (default, one
- * 128-row block per CU) or 4 (64-row blocks, two per CU) -- timing study. */
-int mignn_diag_set_agg_gemm_waves(int waves);
+/* Fused H = 256 layers (csrc/agg_gemm.hip) timing ablations, OR-ed into every
+ * launch until reset with 0 (results wrong by design): NO_PRODUCE = no
+ * aggregate sums, NO_MFMA = no MFMAs, NO_EXT = no out-of-tile row DMA,
+ * NO_TABLES = no own-row chunk DMA, NO_LOCAL = no epilogue, SCHED_INTERLEAVED =
+ * no W chunk DMA. */
+int mignn_diag_set_fused_flags(int flags);
 /* mignn_gat_layer: 1 (default) = the fused kernel where it applies, 0 = the
  * aggregate + transform launches (timing study) */
 int mignn_diag_set_gat_fused(int on);

@@ -58,9 +58,9 @@ def gat(on):
     return f
 
 
-def fused(waves):
+def fused(diag=0):
     def f(Y):
-        _lib.check(L.mignn_diag_set_agg_gemm_waves(waves), "waves")
+        _lib.check(L.mignn_diag_set_fused_flags(diag), "diag")
         if mode == "gin":
             _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
                                                P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15,
@@ -89,7 +89,9 @@ def unfused(Y):
 
 
 cases = ({"unfused": gat(0), "fused": gat(1)} if mode == "gat" else
-         {"unfused": unfused, "fused_w8": fused(8), "fused_w4": fused(4)})
+         {"unfused": unfused, "fused": fused()})
+for dflag in [int(v) for v in os.environ.get("FB_ABLATE", "").split(",") if v]:
+    cases[f"fused_ablate_{dflag}"] = fused(dflag)
 outs = {k: torch.full_like(X, float("nan")) for k in cases}
 for k, f in cases.items():
     f(outs[k])
@@ -99,6 +101,7 @@ res = {"mode": mode, "grid": [nx, ny, nz], "n": n,
                      "nan_rows": int(torch.isnan(outs[k]).any(1).sum().item())} for k in cases},
        "ref_max": outs["unfused"].abs().max().item()}
 del outs
+_lib.check(L.mignn_diag_set_fused_flags(0), "diag")
 Y = torch.empty_like(X)
 reps = int(os.environ.get("FB_REPS", "5"))
 times = {k: [] for k in cases}
@@ -114,6 +117,7 @@ for rnd in range(reps + 1):
         if rnd > 0:
             times[k].append(e0.elapsed_time(e1) / 3)
 res["ms"] = {k: round(statistics.median(v), 4) for k, v in times.items()}
+_lib.check(L.mignn_diag_set_fused_flags(0), "diag")
 E = int(csr.row_ptr[-1].item())
 by = 4 * (2 * n * H + (n + 1) + E)
 fl = {"gin": 4, "gcn": 2, "gat": 8}[mode] * n * H * H * 3

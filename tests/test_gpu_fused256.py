@@ -172,10 +172,8 @@ def test_gin_fused_matches_unfused_launches():
     assert d <= 2e-6 * max(1.0, ref.abs().max().item()), d
 
 
-@pytest.mark.parametrize("waves", [4, 8])
-def test_fused_block_shapes_agree(waves):
-    """The 4- and 8-wave block forms (mignn_diag_set_agg_gemm_waves) give
-    bitwise the same rows (same per-row arithmetic, different tiling)."""
+def test_fused_deterministic():
+    """Two launches give bitwise the same rows (fixed sum order, no atomics)."""
     n = 5000
     ei = _graph(n, 13)
     csr = build_csr(ei, n, _lib.CSR_VERBATIM)
@@ -184,14 +182,12 @@ def test_fused_block_shapes_agree(waves):
     P = _lib.ptr
     img1, img2 = f16x3_image(w1), gin_fused_image(w2)
     outs = []
-    for wv in (8, waves):
-        _lib.check(L.mignn_diag_set_agg_gemm_waves(wv), "waves")
+    for _ in range(2):
         o = torch.empty(n, H, device=DEV)
         _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(x), H, 0, n, H, 0.1,
                                            P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15, P(o),
                                            H, _lib.stream()), "gin_fused")
         outs.append(o)
-    _lib.check(L.mignn_diag_set_agg_gemm_waves(8), "waves")
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
 
