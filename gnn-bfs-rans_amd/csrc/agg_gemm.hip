@@ -103,6 +103,63 @@ __device__ __forceinline__ void vm_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// Staged epilogue of the fused kernels (call with the LDS free, every wave):
+// each wave DMAs its 16 own rows (the residual) into staging rows of NCB*64 B
+// (16-B chunk c of row li at position c ^ (li & 15)), every lane replaces its
+// NCB*4 values -- row lself, columns 16 cb + 4 g + i: bias, residual, BN, ReLU
+// (gnn_model.py:184-191 order: conv + bias, + x, BN, ReLU) -- in place, and
+// the wave stores whole rows (the accumulator layout would store 16 rows x
+// 64 B per instruction).  EV = [q (int) | bias | scale | shift][NCB*16] in LDS,
+// written by the caller before the call.
+template <int NCB>
+__device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float* EV,
+                                                const f32x4 (&acc)[NCB], int p, int flags,
+                                                const float* __restrict__ x, int64_t ldx,
+                                                float* __restrict__ out, int64_t ldo, int64_t t0,
+                                                int64_t re, int wave, int lane, int lself, int g) {
+    constexpr int N = NCB * 16, CPR = NCB * 4, ROWB = NCB * 64, RPI = 64 / CPR, NI = 16 / RPI;
+    const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int ci = l % CPR, ri = l / CPR;
+    if (res) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int li = 16 * wave + RPI * i + ri;
+            int64_t rr = t0 + li;
+            if (rr >= re) rr = re - 1;
+            glds16_ag(x + rr * ldx + 4 * (ci ^ (li & 15)), lds_addr_ag(STG + (16 * wave + RPI * i) * ROWB));
+        }
+    }
+    vm_barrier<0>();                           // (EV of every wave; this wave's rows landed)
+    unsigned char* const srow = STG + lself * ROWB;
+    const int32_t* const EQ = reinterpret_cast<const int32_t*>(EV);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+        const int n = 16 * cb + 4 * g;
+        f32x4* const slot = reinterpret_cast<f32x4*>(srow + 16 * ((4 * cb + g) ^ (lself & 15)));
+        const f32x4 xv = res ? *slot : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int4 q = *reinterpret_cast<const int4*>(EQ + n);
+        const f32x4 bo = *reinterpret_cast<const f32x4*>(EV + N + n);
+        const f32x4 so = *reinterpret_cast<const f32x4*>(EV + 2 * N + n);
+        const f32x4 ho = *reinterpret_cast<const f32x4*>(EV + 3 * N + n);
+        const int qn[4] = {q.x, q.y, q.z, q.w};
+        f32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
+        *slot = o;
+    }
+    // this wave's rows out (its own staging rows: in-order LDS)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int li = 16 * wave + RPI * i + ri;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(STG + li * ROWB + ci * 16);
+        if (t0 + li < re)
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + li) * ldo + 4 * (ci ^ (li & 15))));
+    }
+}
+
 // Block: 8 waves x 16 rows = a 128-row tile (two 4x4x4 blocks of the
 // locality order), one block per CU (LDS 160 KB):
 //   W ring   [2][32 KB]   the streamed W chunks (LDS-DMA, one chunk ahead)
@@ -418,13 +475,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     // layout would store 16 rows x 64 B per instruction).  16-B chunk c of
     // staging row li at position c ^ (li & 15).
     vm_barrier<0>();
-    const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
     const bool hb = (flags & MIGNN_EPI_BIAS) != 0, ha = (flags & MIGNN_EPI_AFFINE) != 0;
     if (flags & MIGNN_DIAG_NO_LOCAL) {         // (ablation: no epilogue)
         if (rv && acc[0][0] == 12345.f) out[rowc * ldo] = acc[1][1];
         return;
     }
-    unsigned char* const STG = lds;
     float* const EV = reinterpret_cast<float*>(lds + BM * 1024);   // q | bias | scale | shift
     if (tid < AH) {
         const int32_t* const qf = reinterpret_cast<const int32_t*>((CHAIN ? img2 : img1) + FB);
@@ -434,46 +489,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
         EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
         EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
     }
-    if (res) {
-        int l = lane;
-        asm volatile("" : "+v"(l));
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int li = 16 * wave + i;
-            int64_t rr = t0 + li;
-            if (rr >= re) rr = re - 1;
-            glds16_ag(x + rr * ldx + 4 * (l ^ (li & 15)), lds_addr_ag(STG + li * 1024));
-        }
-    }
-    vm_barrier<0>();
-    {
-        unsigned char* const srow = STG + lself * 1024;
-        const int32_t* const EQ = reinterpret_cast<const int32_t*>(EV);
-#pragma unroll
-        for (int cb = 0; cb < ACB; ++cb) {
-            const int n = 16 * cb + 4 * g;
-            f32x4* const slot = reinterpret_cast<f32x4*>(srow + 16 * ((4 * cb + g) ^ (lself & 15)));
-            const f32x4 xv = res ? *slot : f32x4{0.f, 0.f, 0.f, 0.f};
-            const int4 q = *reinterpret_cast<const int4*>(EQ + n);
-            const f32x4 bo = *reinterpret_cast<const f32x4*>(EV + AH + n);
-            const f32x4 so = *reinterpret_cast<const f32x4*>(EV + 2 * AH + n);
-            const f32x4 ho = *reinterpret_cast<const f32x4*>(EV + 3 * AH + n);
-            const int qn[4] = {q.x, q.y, q.z, q.w};
-            f32x4 o;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
-            *slot = o;
-        }
-    }
-    // this wave's 16 rows out (its own staging rows: in-order LDS)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int li = 16 * wave + i;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(STG + li * 1024 + lane * 16);
-        if (t0 + li < re)
-            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + li) * ldo + 4 * (lane ^ (li & 15))));
-    }
+    staged_epilogue<ACB>(lds, EV, acc, p, flags, x, ldx, out, ldo, t0, re, wave, lane, lself, g);
 }
 
 int g_fused_diag_flags = 0;   // mignn_diag_set_fused_flags (timing ablations; wrong results)
@@ -741,25 +757,18 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    // epilogue: lane (r, g) = row r, columns 16 cb + 4 g + i
-    const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
-    const float* const xr = x + rowc * ldx + 4 * g;
-    float* const orow = out + rowc * ldo + 4 * g;
-#pragma unroll
-    for (int cb = 0; cb < C::NCB; ++cb) {
-        const int n = 16 * cb + 4 * g;
-        const int4 q = *reinterpret_cast<const int4*>(&QF[n]);
-        const f32x4 bo = *reinterpret_cast<const f32x4*>(&BF[n]);
-        const f32x4 so = *reinterpret_cast<const f32x4*>(&SC[n]);
-        const f32x4 ho = *reinterpret_cast<const f32x4*>(&SH[n]);
-        const f32x4 xv = res ? *reinterpret_cast<const f32x4*>(xr + 16 * cb) : f32x4{0.f, 0.f, 0.f, 0.f};
-        const int qn[4] = {q.x, q.y, q.z, q.w};
-        f32x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
-        if (rv) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(orow + 16 * cb));
+    // epilogue (staged, whole-row stores): the W / alpha buffers are free once
+    // every wave is past its last MFMA; the vectors move after the staging rows
+    vm_barrier<0>();
+    float* const EV2 = reinterpret_cast<float*>(lds + C::BM * H * 4);
+    if (tid < H) {
+        reinterpret_cast<int32_t*>(EV2)[tid] = QF[tid];
+        EV2[H + tid] = BF[tid];
+        EV2[2 * H + tid] = SC[tid];
+        EV2[3 * H + tid] = SH[tid];
     }
+    staged_epilogue<C::NCB>(lds, EV2, acc, p, flags, x, ldx, out, ldo, rb + tile * C::BM, re, wave,
+                            lane, 16 * wave + r, g);
 }
 
 template <int MODE, bool CHAIN>
