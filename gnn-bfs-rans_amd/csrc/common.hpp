@@ -160,11 +160,6 @@ int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const
                                int64_t ldq, const float* x, int64_t ldx, int64_t rb, int64_t re,
                                int h, int heads, float score_scale, float* out, int64_t ldo,
                                bool use_cq, void* stream);
-// the fused split-fp16 GCN layer (gcn_fused.hip), arguments checked by the caller
-int gcn_fused_layer(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
-                    int64_t ldx, int64_t rb, int64_t re, int h, const float* w, const float* bias,
-                    const float* scale, const float* shift, int flags, float* out, int64_t ldo,
-                    void* stream, int xm = 0);
 // the fused GAT layer (agg_gemm.hip): heads = 4, h in {64, 128}, wcat image
 int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
                     const float* x, int64_t ldx, int64_t rb, int64_t re, int h, float slope,

@@ -145,8 +145,6 @@ DIAG_SIGNATURES = {
                                      _P, c_int, _P, c_int64, _P]),
     "mignn_diag_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                            _P, _P, _P, c_int, _P, c_int64, _P]),
-    "mignn_gcn_layer_wave": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P,
-                                     _P, c_int, _P, c_int64, c_int, _P]),
     "mignn_diag_set_gat_fused": (c_int, [c_int]),
     "mignn_diag_set_fused_flags": (c_int, [c_int]),
     "mignn_diag_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,

@@ -73,14 +73,6 @@ int mignn_diag_clock(int blocks, int iters, int64_t* out, void* stream);
 int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img, float* out,
                         void* stream);
 
-/* EXPERIMENTAL (round 3): the wave-independent split-fp16 GCN layer
- * (csrc/gcn_wave.hip), same contract as mignn_gcn_layer_f16x3; variant selects
- * the occupancy / gather-group / residual-timing instance (timing study). */
-int mignn_gcn_layer_wave(const int32_t* row_ptr, const int32_t* col, const float* ew,
-                         const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
-                         const float* w, const float* bias, const float* scale,
-                         const float* shift, int flags, float* out, int64_t ldo, int variant,
-                         void* stream);
 /* Fused H = 256 layers (csrc/agg_gemm.hip) timing ablations, OR-ed into every
  * launch until reset with 0 (results wrong by design): NO_PRODUCE = no
  * aggregate sums, NO_MFMA = no MFMAs, NO_EXT = no out-of-tile row DMA,

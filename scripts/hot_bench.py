@@ -1,8 +1,11 @@
-"""Hot-kernel study (round 3): the fused split-fp16 GCN layer variants on the
+"""Hot-kernel study (round 3): the fused split-fp16 GCN layer and its diagnostic variants on the
 bench mesh (250x200x200 periodic hex, 10M nodes, the model's locality order),
 timed with HIP events in interleaved rounds, each checked against an fp64
 reference on sampled rows and against the producer/consumer kernel.
-Env: HB_H (128), HB_GRID, HB_VARIANTS (comma list of wave variants), HB_REPS."""
+Env: HB_H (128), HB_GRID, HB_DIAGFLAGS (comma list of mignn_diag_gcn_layer_f16x3 flag sets),
+HB_STREAM / HB_STREAM_BLOCKS / HB_STREAM_VARS (the streaming-skeleton diag kernel), HB_REPS.
+(The round-3 wave-independent and symmetric fused-tile kernels measured 4.1-5.4 ms and 4.5 ms
+against 3.06 ms and were removed)"""
 import json
 import os
 import statistics
@@ -45,19 +48,11 @@ def old(Y):
                                        P(W), P(b), P(sc), P(sh), FL, P(Y), H, st), "old")
 
 
-def wave(v):
-    def f(Y):
-        _lib.check(L.mignn_gcn_layer_wave(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
-                                          P(W), P(b), P(sc), P(sh), FL, P(Y), H, v, st), "wave")
-    return f
-
-
 def copy(Y):
     _lib.check(L.mignn_diag_gather(2, P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), n, nx, ny, nz, 0,
                                    P(Y), st), "copy")
 
 
-variants = [int(v) for v in os.environ.get("HB_VARIANTS", "0,1,2,3").split(",") if v]
 cases = {"old_f16x3": old}
 def stream(d, blocks):
     def f(Y):
@@ -72,8 +67,6 @@ if H == 128:          # mignn_diag_gather's copy is written for 128-float rows
         for nb in [int(v) for v in os.environ.get("HB_STREAM_BLOCKS", "256").split(",")]:
             for var in [int(v) for v in os.environ.get("HB_STREAM_VARS", "0").split(",")]:
                 cases[f"stream_d{d}_b{nb}_v{var}"] = stream(d | (var << 5), nb)
-for v in variants:
-    cases[f"wave_v{v}"] = wave(v)
 
 
 def diagf(extra):
