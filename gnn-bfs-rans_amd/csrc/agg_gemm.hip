@@ -498,16 +498,18 @@ int g_fused_diag_flags = 0;   // mignn_diag_set_fused_flags (timing ablations; w
 // j of lane (m, g) in fragment (kc, cb) = W2[16 cb + m][16 (2 kc + j / 4) +
 // 4 g + j % 4] * 2^q (q per output column, as gprep_exp_kernel); layout and
 // exponent table as mignn_linear_f16x3_prep's image
-__global__ __launch_bounds__(256) void perm_exp_kernel(const float* __restrict__ w,
+// (n <= 256 output columns; columns past n are zero, exponent 100)
+__global__ __launch_bounds__(256) void perm_exp_kernel(const float* __restrict__ w, int n,
                                                        int32_t* __restrict__ q) {
     const int colm = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     uint32_t m = 0;
-    for (int i = lane; i < AH; i += 64) m = max(m, __float_as_uint(fabsf(w[colm * AH + i])));
+    if (colm < n)
+        for (int i = lane; i < AH; i += 64) m = max(m, __float_as_uint(fabsf(w[colm * AH + i])));
     for (int o = 32; o > 0; o >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o)));
     if (lane == 0) q[colm] = sexp_ag(m);
 }
-__global__ __launch_bounds__(256) void perm_frag_kernel(const float* __restrict__ w,
+__global__ __launch_bounds__(256) void perm_frag_kernel(const float* __restrict__ w, int n,
                                                         const int32_t* __restrict__ q,
                                                         unsigned char* __restrict__ img) {
     const int t = blockIdx.x * 256 + threadIdx.x;   // (kc, cb, lane)
@@ -522,7 +524,7 @@ __global__ __launch_bounds__(256) void perm_frag_kernel(const float* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int kk = 16 * (2 * kc + (j >> 2)) + 4 * gq + (j & 3);
-        const float v = w[colm * AH + kk] * sc;
+        const float v = colm < n ? w[colm * AH + kk] * sc : 0.f;
         const _Float16 hh = static_cast<_Float16>(v);
         h[j] = hh;
         l[j] = static_cast<_Float16>(v - static_cast<float>(hh));
@@ -530,6 +532,267 @@ __global__ __launch_bounds__(256) void perm_frag_kernel(const float* __restrict_
     unsigned char* base = img + ((static_cast<size_t>(kc) * ACB + cb) * 2) * AFRAG + lane * 16;
     *reinterpret_cast<f16x8*>(base) = h;
     *reinterpret_cast<f16x8*>(base + AFRAG) = l;
+}
+
+// k-permuted image of W [n <= 256, 256] (layout of mignn_linear_f16x3_prep's
+// image, 16 column blocks, exponent table after the fragments)
+int perm_prep(const float* w, int n, unsigned char* img, hipStream_t st) {
+    int32_t* q = reinterpret_cast<int32_t*>(img + static_cast<size_t>(AKP) * ACB * 2 * AFRAG);
+    hipLaunchKernelGGL(perm_exp_kernel, dim3(AH / 4), dim3(256), 0, st, w, n, q);
+    int rc = launch_status("perm_exp_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(perm_frag_kernel, dim3((AKP * ACB * 64 + 255) / 256), dim3(256), 0, st, w, n,
+                       q, img);
+    return launch_status("perm_frag_kernel");
+}
+
+// ------------------------------------------------------------------ H = 256 output head
+// output_proj at H = 256 (gnn_model.py:90-100, :195; configs[3] / configs[4]):
+//   out = W4 relu(W3 relu(W2 relu(W1 x + b1) + b2) + b3) + b4,
+//   W1, W2 [256, 256], W3 [128, 256], W4 [out_dim <= 8, 128]
+// in one launch: per wave 16 rows; the three wide transforms in split-fp16
+// MFMA arithmetic chained through the accumulators (transforms 2 and 3 take
+// the previous one's relu'd accumulator as their B operand, with k-permuted
+// images -- §3.13 of DESIGN.md), W chunks streamed through LDS; the last
+// layer (128 -> out_dim) in fp32 VALU from the accumulators, its dot products
+// summed over the row's 4 lanes.  The three [N, 256 | 128] intermediates of
+// the launch sequence never reach memory.
+// Image: W1 (linear_f16x3 image) | W2 (k-permuted) | W3 (k-permuted, 128
+// columns in 16 padded blocks) | b1 b2 b3 b4 (fp32, 4 KB) | W4 [8][128] fp32.
+constexpr size_t HIMG = static_cast<size_t>(AKP) * ACB * 2 * AFRAG + AH * 4;   // one W image
+constexpr size_t HOFF_B = 3 * HIMG;
+constexpr size_t HOFF_W4 = HOFF_B + 4096;
+constexpr size_t HEAD256_BYTES = HOFF_W4 + 8 * 128 * 4;
+
+__global__ __launch_bounds__(256) void head256_vec_kernel(const float* __restrict__ b1,
+                                                          const float* __restrict__ b2,
+                                                          const float* __restrict__ b3,
+                                                          const float* __restrict__ w4,
+                                                          const float* __restrict__ b4, int out_dim,
+                                                          unsigned char* __restrict__ img) {
+    float* bv = reinterpret_cast<float*>(img + HOFF_B);
+    float* w = reinterpret_cast<float*>(img + HOFF_W4);
+    for (int i = threadIdx.x; i < 256; i += 256) {
+        bv[i] = b1[i];
+        bv[256 + i] = b2[i];
+        if (i < 128) bv[512 + i] = b3[i];
+        if (i < 8) bv[640 + i] = i < out_dim ? b4[i] : 0.f;
+    }
+    for (int i = threadIdx.x; i < 8 * 128; i += 256) w[i] = (i / 128) < out_dim ? w4[i] : 0.f;
+}
+
+// Block: 8 waves x 16 rows.  LDS: W ring [3][32 KB] (two chunks ahead) | per
+// wave an x ring [3][16 rows x 128 B] (transform 1's B operand, two chunks
+// ahead) | q1 q2 q3, b1 b2 b3 b4, W4.  Every load of the chunk loop is an
+// LDS-DMA the compiler does not track, 4 W pieces + 2 x pieces per wave per
+// step (dummy refills of a free buffer past the last chunk keep the count
+// fixed), so one counted wait per step is exact: everything but the youngest
+// step's 6 pieces has landed.
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void head256_kernel(
+    const float* __restrict__ x, int64_t ldx, int64_t n, const unsigned char* __restrict__ img,
+    int out_dim, float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
+    constexpr int AW = 8, BM = 16 * AW;
+    constexpr int NC = 3 * AKP;                          // W1, W2, W3 chunks
+    constexpr int XB = 16 * 128;                         // one x chunk of a wave
+    constexpr int OFF_X = 3 * ACHUNK;
+    constexpr int OFF_V = OFF_X + AW * 3 * XB;           // q1 q2 q3 | b1 b2 b3 b4 | W4
+    constexpr int VB = 3 * 1024 + 4096 + 8 * 128 * 4;
+    constexpr int LDS_BYTES = OFF_V + VB;
+    static_assert(LDS_BYTES <= 160 * 1024, "head256 LDS");
+    constexpr int WPC = ACHUNK / 1024 / AW;              // W pieces per wave per chunk (4)
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t ntiles = (n + BM - 1) / BM;
+    const int64_t per_xcd = gridDim.x >> 3;
+    const int64_t tile = static_cast<int64_t>(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;
+    const int64_t row = tile * BM + 16 * wave + r;
+    const bool rv = row < n;
+
+    // exponent tables, biases and W4 -> LDS (ordinary loads, before any DMA)
+    {
+        const int4* const vsrc = reinterpret_cast<const int4*>(img + HOFF_B);
+        int4* const vdst = reinterpret_cast<int4*>(lds + OFF_V + 3 * 1024);
+        for (int i = tid; i < (VB - 3 * 1024) / 16; i += AW * 64) vdst[i] = vsrc[i];
+        if (tid < 3 * 64) {
+            const int t = tid >> 6;
+            reinterpret_cast<int4*>(lds + OFF_V + t * 1024)[tid & 63] =
+                reinterpret_cast<const int4*>(img + t * HIMG + HIMG - AH * 4)[tid & 63];
+        }
+    }
+    const int32_t* const QV = reinterpret_cast<const int32_t*>(lds + OFF_V);
+    const float* const BV = reinterpret_cast<const float*>(lds + OFF_V + 3 * 1024);
+    const float* const W4 = BV + 1024;
+
+    // W chunk c (transform c / 8, k chunk c % 8) -> W buffer c % 3; past the
+    // last chunk a dummy refill of the free buffer
+    auto w_dma = [&](int c) {
+        const int cc = c < NC ? c : NC - 1;
+        const unsigned char* src = img + (cc / AKP) * HIMG + static_cast<size_t>(cc % AKP) * ACHUNK;
+        unsigned char* dst = lds + (c % 3) * ACHUNK;
+#pragma unroll
+        for (int pc = 0; pc < WPC; ++pc) {
+            const int piece = wave + pc * AW;
+            glds16_ag(src + piece * 1024 + lane * 16, lds_addr_ag(dst + piece * 1024));
+        }
+    };
+    // x chunk kc of the wave's 16 rows -> its x buffer kc % 3 (row li at li *
+    // 128, 16-B segment s at s * 16); past chunk 7 a dummy refill
+    auto x_dma = [&](int kc) {
+        const int kk = kc < AKP ? kc : AKP - 1;
+        unsigned char* dst = lds + OFF_X + (wave * 3 + kc % 3) * XB;
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc) {
+            int64_t rr = tile * BM + 16 * wave + 8 * pc + (lane >> 3);
+            if (rr >= n) rr = n - 1;
+            glds16_ag(x + rr * ldx + 32 * kk + 4 * (lane & 7), lds_addr_ag(dst + pc * 1024));
+        }
+    };
+    w_dma(0);
+    x_dma(0);
+    w_dma(1);
+    x_dma(1);
+
+    f32x4 acc[ACB];
+#pragma unroll
+    for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int p = 100;
+    const unsigned char* const wl0 = lds + lane * 16;
+    auto mfma3 = [&](const unsigned char* wb, int ncb, const f16x8& bh, const f16x8& bl) {
+#pragma unroll
+        for (int cb = 0; cb < ACB; ++cb) {
+            if (cb >= ncb) break;
+            const f16x8 wh = *reinterpret_cast<const f16x8*>(wb + (2 * cb) * AFRAG);
+            const f16x8 wl = *reinterpret_cast<const f16x8*>(wb + (2 * cb + 1) * AFRAG);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, acc[cb], 0, 0, 0);
+        }
+    };
+    // top of step c: chunk c's W (and x) landed, every wave done with the
+    // buffers refilled next; then the refills of chunk c + 2
+    auto step_sync = [&](int c) {
+        vm_barrier<WPC + 2>();
+        w_dma(c + 2);
+        x_dma(c + 2);
+    };
+    // ---- transform 1: x W1^T, B operand from the x ring, online exponent
+    const unsigned char* const xr = lds + OFF_X + wave * 3 * XB + r * 128 + 32 * g;
+#pragma unroll 1
+    for (int kc = 0; kc < AKP; ++kc) {
+        step_sync(kc);
+        const f32x4 c0 = *reinterpret_cast<const f32x4*>(xr + (kc % 3) * XB);
+        const f32x4 c1 = *reinterpret_cast<const f32x4*>(xr + (kc % 3) * XB + 16);
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            m = max(m, max(__float_as_uint(fabsf(c0[i])), __float_as_uint(fabsf(c1[i]))));
+        const int pc = sexp_ag(rowmax4(m));
+        if (pc < p) {
+#pragma unroll
+            for (int cb = 0; cb < ACB; ++cb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
+            p = pc;
+        }
+        const float spv = p2_ag(p);
+        f16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float v = (j < 4 ? c0[j] : c1[j - 4]) * spv;
+            const _Float16 hh = static_cast<_Float16>(v);
+            bh[j] = hh;
+            bl[j] = static_cast<_Float16>(v - static_cast<float>(hh));
+        }
+        mfma3(wl0 + (kc % 3) * ACHUNK, ACB, bh, bl);
+    }
+    // ---- transforms 2 and 3 from the relu'd accumulators (k-permuted images)
+    f16x8 hh[AKP], hl[AKP];
+    auto relu_split = [&](const int32_t* q, const float* bias) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int cb = 0; cb < ACB; ++cb) {
+            const int4 qv = *reinterpret_cast<const int4*>(q + 16 * cb + 4 * g);
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + 16 * cb + 4 * g);
+            const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float h = ldexpf(acc[cb][i], -(p + qn[i])) + bb[i];
+                h = h < 0.f ? 0.f : h;
+                acc[cb][i] = h;
+                m = max(m, __float_as_uint(fabsf(h)));
+            }
+        }
+        p = sexp_ag(rowmax4(m));
+        const float spv = p2_ag(p);
+#pragma unroll
+        for (int kc = 0; kc < AKP; ++kc)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = acc[2 * kc + (j >> 2)][j & 3] * spv;
+                const _Float16 t16 = static_cast<_Float16>(v);
+                hh[kc][j] = t16;
+                hl[kc][j] = static_cast<_Float16>(v - static_cast<float>(t16));
+            }
+#pragma unroll
+        for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    relu_split(QV, BV);                              // h1 = relu(x W1^T + b1)
+#pragma unroll
+    for (int kc = 0; kc < AKP; ++kc) {
+        step_sync(AKP + kc);
+        mfma3(wl0 + ((AKP + kc) % 3) * ACHUNK, ACB, hh[kc], hl[kc]);
+    }
+    relu_split(QV + 256, BV + 256);                  // h2 = relu(h1 W2^T + b2)
+#pragma unroll
+    for (int kc = 0; kc < AKP; ++kc) {
+        step_sync(2 * AKP + kc);
+        mfma3(wl0 + ((2 * AKP + kc) % 3) * ACHUNK, ACB / 2, hh[kc], hl[kc]);
+    }
+    __builtin_amdgcn_s_waitcnt(0x70);                // drain the dummy refills
+    // ---- h3 = relu(h2 W3^T + b3): lane (r, g) holds h3[r][16 cb + 4 g + i], cb < 8;
+    // out[r][o] = sum_k h3[k] W4[o][k] + b4[o] (fp32; summed over the row's 4 lanes)
+    float h3[ACB / 2][4];
+#pragma unroll
+    for (int cb = 0; cb < ACB / 2; ++cb) {
+        const int4 qv = *reinterpret_cast<const int4*>(QV + 512 + 16 * cb + 4 * g);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(BV + 512 + 16 * cb + 4 * g);
+        const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float h = ldexpf(acc[cb][i], -(p + qn[i])) + bb[i];
+            h3[cb][i] = h < 0.f ? 0.f : h;
+        }
+    }
+    float o[8];
+#pragma unroll
+    for (int oc = 0; oc < 8; ++oc) {
+        float sacc = 0.f;
+        if (oc < out_dim) {
+#pragma unroll
+            for (int cb = 0; cb < ACB / 2; ++cb) {
+                const f32x4 wv = *reinterpret_cast<const f32x4*>(W4 + oc * 128 + 16 * cb + 4 * g);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sacc = fmaf(h3[cb][i], wv[i], sacc);
+            }
+            const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(sacc), __float_as_uint(sacc), false, false);
+            sacc = __uint_as_float(static_cast<uint32_t>(r16[0])) + __uint_as_float(static_cast<uint32_t>(r16[1]));
+            const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sacc), __float_as_uint(sacc), false, false);
+            sacc = __uint_as_float(static_cast<uint32_t>(r32[0])) + __uint_as_float(static_cast<uint32_t>(r32[1]));
+            sacc += BV[640 + oc];
+        }
+        o[oc] = sacc;
+    }
+    if (rv && g == 0) {
+        const int64_t orow = out_rows != nullptr ? static_cast<int64_t>(out_rows[row]) : row;
+#pragma unroll
+        for (int oc = 0; oc < 8; ++oc)
+            if (oc < out_dim) out[orow * ldo + oc] = o[oc];
+    }
 }
 
 // ------------------------------------------------------------------ GATConv
@@ -592,7 +855,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
 
     // W chunks of x chunk t (heads 0..3: image chunks k XC + t) -> buffer t & 1
     auto w_dma = [&](int t) {
-        if (t >= C::XC) return;
+        if (t >= C::XC || (flags & MIGNN_SCHED_INTERLEAVED)) return;
         unsigned char* dst = lds + (t & 1) * C::STEPW;
 #pragma unroll
         for (int pc = 0; pc < C::STEPW / 1024 / C::AW; ++pc) {
@@ -718,7 +981,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         // (the next chunk's loads not hoisted above the sums: two gather
         // buffers live at once spilled registers)
         __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < C::XC) gather(t + 1);
+        if (t + 1 < C::XC && !(flags & MIGNN_DIAG_NO_PRODUCE)) gather(t + 1);
         const unsigned char* wb = wl0 + (t & 1) * C::STEPW;
 #pragma unroll
         for (int k = 0; k < HEADS; ++k) {
@@ -745,6 +1008,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
             }
 #pragma unroll
             for (int cb = 0; cb < C::NCB; ++cb) {
+                if (flags & MIGNN_DIAG_NO_MFMA) break;
                 const unsigned char* wf = wb + k * C::WCH + (2 * cb) * AFRAG;
                 const f16x8 wh = *reinterpret_cast<const f16x8*>(wf);
                 const f16x8 wl = *reinterpret_cast<const f16x8*>(wf + AFRAG);
@@ -760,6 +1024,10 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     // epilogue (staged, whole-row stores): the W / alpha buffers are free once
     // every wave is past its last MFMA; the vectors move after the staging rows
     vm_barrier<0>();
+    if (flags & MIGNN_DIAG_NO_LOCAL) {         // (ablation: no epilogue)
+        if (rv && acc[0][0] == 12345.f) out[rowc * ldo] = acc[1][1];
+        return;
+    }
     float* const EV2 = reinterpret_cast<float*>(lds + C::BM * H * 4);
     if (tid < H) {
         reinterpret_cast<int32_t*>(EV2)[tid] = QF[tid];
@@ -817,15 +1085,7 @@ extern "C" int mignn_gin_fused_prep(const float* w2, int h, void* img, size_t im
     MIGNN_REQUIRE(w2 && img && h == AH, "gin_fused_prep: h must be 256");
     MIGNN_REQUIRE(img_bytes >= mignn_gin_fused_prep_bytes(h), "gin_fused_prep: image too small");
     MIGNN_REQUIRE(aligned16(img), "gin_fused_prep: image not 16-B aligned");
-    hipStream_t st = as_stream(stream);
-    auto* base = static_cast<unsigned char*>(img);
-    int32_t* q = reinterpret_cast<int32_t*>(base + static_cast<size_t>(AKP) * ACB * 2 * AFRAG);
-    hipLaunchKernelGGL(perm_exp_kernel, dim3(AH / 4), dim3(256), 0, st, w2, q);
-    int rc = launch_status("perm_exp_kernel");
-    if (rc) return rc;
-    hipLaunchKernelGGL(perm_frag_kernel, dim3((AKP * ACB * 64 + 255) / 256), dim3(256), 0, st, w2,
-                       q, base);
-    return launch_status("perm_frag_kernel");
+    return perm_prep(w2, AH, static_cast<unsigned char*>(img), as_stream(stream));
 }
 
 static int check_common(const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx,
@@ -890,6 +1150,7 @@ int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* log
                   "gat_layer: fused path needs 16-B aligned rows");
     MIGNN_REQUIRE(x != out, "gat_layer: in-place not supported (neighbours read x)");
     hipStream_t st = as_stream(stream);
+    flags |= g_fused_diag_flags;
     return h == 128 ? launch_gat_fused<128>(row_ptr, col, logits, x, ldx, rb, re, slope, img, bias,
                                             scale, shift, flags, out, ldo, st)
                     : launch_gat_fused<64>(row_ptr, col, logits, x, ldx, rb, re, slope, img, bias,
@@ -903,3 +1164,30 @@ extern "C" int mignn_diag_set_fused_flags(int flags) {
                                   MIGNN_SCHED_INTERLEAVED);
     return MIGNN_OK;
 }
+
+namespace mignn {
+size_t head256_prep_bytes() { return HEAD256_BYTES; }
+
+int head256_prep(const float* w1, const float* b1, const float* w2, const float* b2,
+                 const float* w3, const float* b3, const float* w4, const float* b4, int out_dim,
+                 void* img, void* stream) {
+    hipStream_t st = as_stream(stream);
+    auto* im = static_cast<unsigned char*>(img);
+    if (int rc = mignn_linear_f16x3_prep(w1, AH, AH, im, HIMG, stream)) return rc;
+    if (int rc = perm_prep(w2, AH, im + HIMG, st)) return rc;
+    if (int rc = perm_prep(w3, AH / 2, im + 2 * HIMG, st)) return rc;
+    hipLaunchKernelGGL(head256_vec_kernel, dim3(1), dim3(256), 0, st, b1, b2, b3, w4, b4, out_dim, im);
+    return launch_status("head256_vec_kernel");
+}
+
+int head256(const float* x, int64_t ldx, int64_t n, const void* img, int out_dim, float* out,
+            int64_t ldo, const int32_t* out_rows, void* stream) {
+    const int64_t ntiles = (n + 127) / 128;
+    const int64_t nb = (ntiles + 7) / 8 * 8;
+    MIGNN_REQUIRE(nb < (int64_t(1) << 31), "mlp_head: too many rows");
+    hipLaunchKernelGGL(head256_kernel, dim3(static_cast<unsigned>(nb)), dim3(512), 0,
+                       as_stream(stream), x, ldx, n, static_cast<const unsigned char*>(img),
+                       out_dim, out, ldo, out_rows);
+    return launch_status("head256_kernel");
+}
+}  // namespace mignn

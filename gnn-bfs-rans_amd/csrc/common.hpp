@@ -165,6 +165,13 @@ int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* log
                     const float* x, int64_t ldx, int64_t rb, int64_t re, int h, float slope,
                     const void* img, const float* bias, const float* scale, const float* shift,
                     int flags, float* out, int64_t ldo, void* stream);
+// the fused H = 256 output head (agg_gemm.hip), arguments checked by mlp_f16x3.hip
+size_t head256_prep_bytes();
+int head256_prep(const float* w1, const float* b1, const float* w2, const float* b2,
+                 const float* w3, const float* b3, const float* w4, const float* b4, int out_dim,
+                 void* img, void* stream);
+int head256(const float* x, int64_t ldx, int64_t n, const void* img, int out_dim, float* out,
+            int64_t ldo, const int32_t* out_rows, void* stream);
 int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, int n,
                 const float* bias, const float* residual, int64_t ldr, const float* scale,
                 const float* shift, int flags, float* c, int64_t ldc, hipStream_t st,

@@ -354,7 +354,8 @@ __global__ __launch_bounds__(NWV * 64) void mlp_head_kernel(
 using namespace mignn;
 
 extern "C" size_t mignn_mlp_head_prep_bytes(int h) {
-    return h == 128 ? MCfg<128>::IMG_BYTES : h == 64 ? MCfg<64>::IMG_BYTES : 0;
+    return h == 256 ? head256_prep_bytes()
+                    : h == 128 ? MCfg<128>::IMG_BYTES : h == 64 ? MCfg<64>::IMG_BYTES : 0;
 }
 
 extern "C" int mignn_mlp_head_prep(const float* w1, const float* b1, const float* w2,
@@ -363,11 +364,12 @@ extern "C" int mignn_mlp_head_prep(const float* w1, const float* b1, const float
                                    void* img, size_t img_bytes, void* stream) {
     MIGNN_REQUIRE(w1 && b1 && w2 && b2 && w3 && b3 && w4 && b4 && img,
                   "mlp_head_prep: null pointer");
-    MIGNN_REQUIRE(h == 64 || h == 128, "mlp_head_prep: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(h == 64 || h == 128 || h == 256, "mlp_head_prep: h must be 64, 128 or 256 (got %d)", h);
     MIGNN_REQUIRE(out_dim >= 1 && out_dim <= 8, "mlp_head_prep: out_dim must be 1..8 (got %d)",
                   out_dim);
     MIGNN_REQUIRE(img_bytes >= mignn_mlp_head_prep_bytes(h), "mlp_head_prep: image too small");
     MIGNN_REQUIRE(aligned16(img), "mlp_head_prep: unaligned image");
+    if (h == 256) return head256_prep(w1, b1, w2, b2, w3, b3, w4, b4, out_dim, img, stream);
     hipStream_t st = as_stream(stream);
     auto* im = static_cast<unsigned char*>(img);
     if (h == 128)
@@ -383,13 +385,14 @@ extern "C" int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, con
                               int out_dim, float* out, int64_t ldo, const int32_t* out_rows,
                               void* stream) {
     MIGNN_REQUIRE(x && img && out, "mlp_head: null pointer");
-    MIGNN_REQUIRE(h == 64 || h == 128, "mlp_head: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(h == 64 || h == 128 || h == 256, "mlp_head: h must be 64, 128 or 256 (got %d)", h);
     MIGNN_REQUIRE(out_dim >= 1 && out_dim <= 8, "mlp_head: out_dim must be 1..8 (got %d)",
                   out_dim);
     MIGNN_REQUIRE(aligned16(x) && ldx % 4 == 0 && ldx >= h, "mlp_head: x must be 16-B rows");
     MIGNN_REQUIRE(ldo >= out_dim, "mlp_head: bad ldo");
     MIGNN_REQUIRE(aligned16(img), "mlp_head: unaligned image");
     if (n <= 0) return MIGNN_OK;
+    if (h == 256) return head256(x, ldx, n, img, out_dim, out, ldo, out_rows, stream);
     hipStream_t st = as_stream(stream);
     static int cus_cache[64] = {0};
     int dev = 0;

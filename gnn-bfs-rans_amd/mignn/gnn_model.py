@@ -833,11 +833,13 @@ class FlowGNN(nn.Module):
 
     def _output_mlp(self, x, tmp, out, rows=None, inv=None):
         """output_proj (gnn_model.py:90-100, :195): Lin-ReLU-Lin-ReLU-Lin-ReLU-Lin.
-        precision "f16x3" with H in {64, 128} and output_dim <= 8: one fused
-        launch (mignn_mlp_head, split-fp16 MFMA); otherwise four fp32 launches."""
+        precision "f16x3" with H in {64, 128} (or 256 with the fused H = 256 kernels
+        on) and output_dim <= 8: one fused launch (mignn_mlp_head, split-fp16
+        MFMA); otherwise four launches."""
         l0, l3, l6, l8 = (self.output_proj[i] for i in (0, 3, 6, 8))
         H = self.hidden_dim
-        if self.precision == "f16x3" and H in (64, 128) and self.output_dim <= 8:
+        if (self.precision == "f16x3" and self.output_dim <= 8
+                and (H in (64, 128) or (H == 256 and self._fused256()))):
             L = _lib.lib()
             P = _lib.ptr
             ts = (l0.weight, l0.bias, l3.weight, l3.bias, l6.weight, l6.bias, l8.weight,

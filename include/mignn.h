@@ -250,7 +250,7 @@ int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const floa
                           const float* shift, int flags, float* out, int64_t ldo, void* stream);
 
 /* Fused output head (output_proj, gnn_model.py:90-100, :195) in split-fp16
- * MFMA arithmetic, h in {64, 128}, out_dim 1..8:
+ * MFMA arithmetic, h in {64, 128, 256}, out_dim 1..8:
  *   out = W4 relu(W3 relu(W2 relu(W1 x + b1) + b2) + b3) + b4
  * with W1, W2: [h, h], W3: [h/2, h], W4: [out_dim, h/2] (torch Linear layout).
  * mignn_mlp_head_prep writes the head image (fp16 hi/lo weight fragments,
@@ -260,7 +260,9 @@ int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const floa
  * launches of FlowGNN.output_proj (eval mode: Dropout is the identity).
  * Error vs fp64 ~1e-6 relative.  x: n rows of h floats, 16-B aligned rows;
  * result row r goes to out row out_rows[r] (NULL: r), i.e. back from the
- * locality order to the caller's node order. */
+ * locality order to the caller's node order.  h = 256 (configs[3]/[4]):
+ * per-column weight exponents and per-row activation exponents, the three
+ * wide transforms chained in registers (agg_gemm.hip head256_kernel). */
 size_t mignn_mlp_head_prep_bytes(int h);
 int mignn_mlp_head_prep(const float* w1, const float* b1, const float* w2, const float* b2,
                         const float* w3, const float* b3, const float* w4, const float* b4,

@@ -49,9 +49,10 @@ P = _lib.ptr
 st = _lib.stream()
 
 
-def gat(on):
+def gat(on, diag=0):
     def f(Y):
         _lib.check(L.mignn_diag_set_gat_fused(on), "gat_fused")
+        _lib.check(L.mignn_diag_set_fused_flags(diag), "diag")
         _lib.check(L.mignn_gat_layer(P(csr.row_ptr), P(csr.col), P(X), H, n, 0, n, H, 4, 0.2,
                                      P(WLOG), None, 8, P(WCAT), P(img1), P(b1), P(sc), P(sh), 15,
                                      P(GSCR), GSCR.numel(), P(Y), H, st), "gat_layer")
@@ -91,7 +92,7 @@ def unfused(Y):
 cases = ({"unfused": gat(0), "fused": gat(1)} if mode == "gat" else
          {"unfused": unfused, "fused": fused()})
 for dflag in [int(v) for v in os.environ.get("FB_ABLATE", "").split(",") if v]:
-    cases[f"fused_ablate_{dflag}"] = fused(dflag)
+    cases[f"fused_ablate_{dflag}"] = gat(1, dflag) if mode == "gat" else fused(dflag)
 outs = {k: torch.full_like(X, float("nan")) for k in cases}
 for k, f in cases.items():
     f(outs[k])

@@ -20,7 +20,8 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob("gpurun_out/pmcl/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        for k in ("sum_rows_kernel", "tf_rows_kernel", "gat_rows_kernel", "gemm_f16x3_kernel"):
+        for k in ("sum_rows_kernel", "tf_rows_kernel", "gat_rows_kernel", "gemm_f16x3_kernel",
+                  "agg_gemm_kernel", "gat_fused_kernel"):
             if k in n:
                 vals[(k, r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in sorted(vals.items()):

@@ -15,12 +15,14 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 config = sys.argv[2] if len(sys.argv) > 2 else "GCN_L4_H128_250x200x200"
-KERNEL = sys.argv[3] if len(sys.argv) > 3 else "gcn_f16x3_kernel<128>"
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else "gcn_f16x3_kernel<128"
 vals = {}
 for f in glob.glob(f"{root}/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         if KERNEL in r["Kernel_Name"]:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+if not vals.get("FETCH_SIZE"):
+    sys.exit(f"no FETCH_SIZE records for {KERNEL!r} under {root}; nothing written")
 mean = {k: statistics.mean(v) for k, v in vals.items()}
 out = {
     "config": config, "kernel": KERNEL, "launches_sampled": len(vals.get("FETCH_SIZE", [])),

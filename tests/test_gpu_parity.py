@@ -255,13 +255,14 @@ def _head_ref(x, ws, bs):
     return h
 
 
-@pytest.mark.parametrize("H", [64, 128])
+@pytest.mark.parametrize("H", [64, 128, 256])
 @pytest.mark.parametrize("case", [(1000, 7, 0, 0), (37, 8, 0, 1), (1, 3, 4, 0), (20011, 7, 12, 5),
                                   (64, 1, 0, 0), (4096, 7, 0, 0, "wide")])
 def test_mlp_head_f16x3_vs_fp64(H, case):
-    """Fused split-fp16 output head: partial 32-row blocks, 1..8 outputs,
+    """Fused split-fp16 output head: partial row blocks, 1..8 outputs,
     strided x / out (padding left untouched), inputs spanning 2^+-8 in
-    magnitude ("wide": per-row exponents matter)."""
+    magnitude ("wide": per-row exponents matter); H = 256 is the chained
+    three-transform kernel of agg_gemm.hip."""
     n, od, padx, pado = case[:4]
     g = torch.Generator().manual_seed(n + H + od)
     ld = H + padx
@@ -288,10 +289,11 @@ def test_mlp_head_f16x3_vs_fp64(H, case):
     assert torch.isnan(got[:, od:]).all()
 
 
-def test_mlp_head_scatter_rows():
+@pytest.mark.parametrize("H", [128, 256])
+def test_mlp_head_scatter_rows(H):
     """out_rows: result row r lands in out row out_rows[r] (locality order ->
     caller order); identical values to the unscattered launch."""
-    H, n, od = 128, 777, 7
+    n, od = 777, 7
     g = torch.Generator().manual_seed(11)
     x = torch.randn(n, H, generator=g).to(DEV)
     dims = [(H, H), (H, H), (H // 2, H), (od, H // 2)]
@@ -315,7 +317,7 @@ def test_mlp_head_rejects_bad_shapes():
     img = torch.zeros(1 << 18, dtype=torch.uint8, device=DEV)
     out = torch.zeros(4, 8, device=DEV)
     rc = L.mignn_mlp_head(P(x), 96, 4, 96, P(img), 7, P(out), 8, None, _lib.stream())
-    assert rc == 1 and "h must be 64 or 128" in _lib.last_error()
+    assert rc == 1 and "h must be 64, 128 or 256" in _lib.last_error()
     rc = L.mignn_mlp_head(P(x), 96, 4, 64, P(img), 9, P(out), 8, None, _lib.stream())
     assert rc == 1
     rc = L.mignn_mlp_head(P(x) + 4, 96, 4, 64, P(img), 7, P(out), 8, None, _lib.stream())
