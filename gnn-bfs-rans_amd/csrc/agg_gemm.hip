@@ -103,6 +103,14 @@ __device__ __forceinline__ void vm_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// sum over the 4 lanes of a row (every lane gets the same value)
+__device__ __forceinline__ float rowsum4(float v) {
+    const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(static_cast<uint32_t>(r16[0])) + __uint_as_float(static_cast<uint32_t>(r16[1]));
+    const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(static_cast<uint32_t>(r32[0])) + __uint_as_float(static_cast<uint32_t>(r32[1]));
+}
+
 // Staged epilogue of the fused kernels (call with the LDS free, every wave):
 // each wave DMAs its 16 own rows (the residual) into staging rows of NCB*64 B
 // (16-B chunk c of row li at position c ^ (li & 15)), every lane replaces its
@@ -581,26 +589,17 @@ __global__ __launch_bounds__(256) void head256_vec_kernel(const float* __restric
     for (int i = threadIdx.x; i < 8 * 128; i += 256) w[i] = (i / 128) < out_dim ? w4[i] : 0.f;
 }
 
-// Block: 8 waves x 16 rows.  LDS: W ring [3][32 KB] (two chunks ahead) | per
-// wave an x ring [3][16 rows x 128 B] (transform 1's B operand, two chunks
-// ahead) | q1 q2 q3, b1 b2 b3 b4, W4.  Every load of the chunk loop is an
-// LDS-DMA the compiler does not track, 4 W pieces + 2 x pieces per wave per
-// step (dummy refills of a free buffer past the last chunk keep the count
-// fixed), so one counted wait per step is exact: everything but the youngest
-// step's 6 pieces has landed.
+// Block: 8 waves x 16 rows; W chunks through a 2-buffer LDS ring (LDS-DMA one
+// chunk ahead, one barrier per chunk), x rows one chunk ahead in registers.
+// (A 3-deep W ring with x by LDS-DMA and counted waits measured slower: 13.7
+// vs 13.0 ms at 12.6M rows.)
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void head256_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n, const unsigned char* __restrict__ img,
     int out_dim, float* __restrict__ out, int64_t ldo, const int32_t* __restrict__ out_rows) {
     constexpr int AW = 8, BM = 16 * AW;
     constexpr int NC = 3 * AKP;                          // W1, W2, W3 chunks
-    constexpr int XB = 16 * 128;                         // one x chunk of a wave
-    constexpr int OFF_X = 3 * ACHUNK;
-    constexpr int OFF_V = OFF_X + AW * 3 * XB;           // q1 q2 q3 | b1 b2 b3 b4 | W4
-    constexpr int VB = 3 * 1024 + 4096 + 8 * 128 * 4;
-    constexpr int LDS_BYTES = OFF_V + VB;
-    static_assert(LDS_BYTES <= 160 * 1024, "head256 LDS");
-    constexpr int WPC = ACHUNK / 1024 / AW;              // W pieces per wave per chunk (4)
-    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+    constexpr int OFF_V = 2 * ACHUNK;                    // b1 b2 b3 b4 | W4 copies
+    __shared__ __attribute__((aligned(16))) unsigned char lds[OFF_V + 4096 + 8 * 128 * 4];
     const int tid = threadIdx.x;
     int lane = tid & 63;
     asm volatile("" : "+v"(lane));
@@ -612,50 +611,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
     if (tile >= ntiles) return;
     const int64_t row = tile * BM + 16 * wave + r;
     const bool rv = row < n;
+    const int64_t rowc = rv ? row : n - 1;
 
-    // exponent tables, biases and W4 -> LDS (ordinary loads, before any DMA)
-    {
-        const int4* const vsrc = reinterpret_cast<const int4*>(img + HOFF_B);
-        int4* const vdst = reinterpret_cast<int4*>(lds + OFF_V + 3 * 1024);
-        for (int i = tid; i < (VB - 3 * 1024) / 16; i += AW * 64) vdst[i] = vsrc[i];
-        if (tid < 3 * 64) {
-            const int t = tid >> 6;
-            reinterpret_cast<int4*>(lds + OFF_V + t * 1024)[tid & 63] =
-                reinterpret_cast<const int4*>(img + t * HIMG + HIMG - AH * 4)[tid & 63];
-        }
-    }
-    const int32_t* const QV = reinterpret_cast<const int32_t*>(lds + OFF_V);
-    const float* const BV = reinterpret_cast<const float*>(lds + OFF_V + 3 * 1024);
-    const float* const W4 = BV + 1024;
-
-    // W chunk c (transform c / 8, k chunk c % 8) -> W buffer c % 3; past the
-    // last chunk a dummy refill of the free buffer
+    // W chunk c: transform c / 8, k chunk c % 8 (W3: its 8 real column blocks only)
     auto w_dma = [&](int c) {
-        const int cc = c < NC ? c : NC - 1;
-        const unsigned char* src = img + (cc / AKP) * HIMG + static_cast<size_t>(cc % AKP) * ACHUNK;
-        unsigned char* dst = lds + (c % 3) * ACHUNK;
-#pragma unroll
-        for (int pc = 0; pc < WPC; ++pc) {
-            const int piece = wave + pc * AW;
+        if (c >= NC) return;
+        const int t = c / AKP, kc = c % AKP;
+        const unsigned char* src = img + t * HIMG + static_cast<size_t>(kc) * ACHUNK;
+        unsigned char* dst = lds + (c & 1) * ACHUNK;
+        const int npieces = t == 2 ? ACHUNK / 2 / 1024 : ACHUNK / 1024;
+        for (int piece = wave; piece < npieces; piece += AW)
             glds16_ag(src + piece * 1024 + lane * 16, lds_addr_ag(dst + piece * 1024));
-        }
-    };
-    // x chunk kc of the wave's 16 rows -> its x buffer kc % 3 (row li at li *
-    // 128, 16-B segment s at s * 16); past chunk 7 a dummy refill
-    auto x_dma = [&](int kc) {
-        const int kk = kc < AKP ? kc : AKP - 1;
-        unsigned char* dst = lds + OFF_X + (wave * 3 + kc % 3) * XB;
-#pragma unroll
-        for (int pc = 0; pc < 2; ++pc) {
-            int64_t rr = tile * BM + 16 * wave + 8 * pc + (lane >> 3);
-            if (rr >= n) rr = n - 1;
-            glds16_ag(x + rr * ldx + 32 * kk + 4 * (lane & 7), lds_addr_ag(dst + pc * 1024));
-        }
     };
     w_dma(0);
-    x_dma(0);
-    w_dma(1);
-    x_dma(1);
+    // biases and W4 -> LDS (read after the first barrier)
+    for (int i = tid; i < (4096 + 8 * 128 * 4) / 16; i += AW * 64)
+        reinterpret_cast<f32x4*>(lds + OFF_V)[i] = reinterpret_cast<const f32x4*>(img + HOFF_B)[i];
+    const float* const BV = reinterpret_cast<const float*>(lds + OFF_V);
+    const float* const W4 = reinterpret_cast<const float*>(lds + OFF_V + 4096);
+
+    // x chunk kc of the row (B-operand layout), one chunk ahead in registers
+    const float* const xrow = x + rowc * ldx + 8 * g;
+    f32x4 xa[2], xb[2];
+    xa[0] = *reinterpret_cast<const f32x4*>(xrow);
+    xa[1] = *reinterpret_cast<const f32x4*>(xrow + 4);
 
     f32x4 acc[ACB];
 #pragma unroll
@@ -673,24 +652,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
             acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, acc[cb], 0, 0, 0);
         }
     };
-    // top of step c: chunk c's W (and x) landed, every wave done with the
-    // buffers refilled next; then the refills of chunk c + 2
-    auto step_sync = [&](int c) {
-        vm_barrier<WPC + 2>();
-        w_dma(c + 2);
-        x_dma(c + 2);
-    };
-    // ---- transform 1: x W1^T, B operand from the x ring, online exponent
-    const unsigned char* const xr = lds + OFF_X + wave * 3 * XB + r * 128 + 32 * g;
-#pragma unroll 1
-    for (int kc = 0; kc < AKP; ++kc) {
-        step_sync(kc);
-        const f32x4 c0 = *reinterpret_cast<const f32x4*>(xr + (kc % 3) * XB);
-        const f32x4 c1 = *reinterpret_cast<const f32x4*>(xr + (kc % 3) * XB + 16);
+    // ---- transform 1: x W1^T, A split chunk by chunk with the online exponent
+    auto step1 = [&](int kc, f32x4 (&cur)[2], f32x4 (&nxt)[2]) {
+        chunk_barrier();                       // W1 chunk kc and x chunk kc landed
+        w_dma(kc + 1);
+        if (kc + 1 < AKP) {
+            nxt[0] = *reinterpret_cast<const f32x4*>(xrow + 32 * (kc + 1));
+            nxt[1] = *reinterpret_cast<const f32x4*>(xrow + 32 * (kc + 1) + 4);
+        }
         uint32_t m = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            m = max(m, max(__float_as_uint(fabsf(c0[i])), __float_as_uint(fabsf(c1[i]))));
+            m = max(m, max(__float_as_uint(fabsf(cur[0][i])), __float_as_uint(fabsf(cur[1][i]))));
         const int pc = sexp_ag(rowmax4(m));
         if (pc < p) {
 #pragma unroll
@@ -703,19 +676,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
         f16x8 bh, bl;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float v = (j < 4 ? c0[j] : c1[j - 4]) * spv;
+            const float v = cur[j >> 2][j & 3] * spv;
             const _Float16 hh = static_cast<_Float16>(v);
             bh[j] = hh;
             bl[j] = static_cast<_Float16>(v - static_cast<float>(hh));
         }
-        mfma3(wl0 + (kc % 3) * ACHUNK, ACB, bh, bl);
+        mfma3(wl0 + (kc & 1) * ACHUNK, ACB, bh, bl);
+    };
+#pragma unroll 1
+    for (int kc = 0; kc < AKP; kc += 2) {
+        step1(kc, xa, xb);
+        step1(kc + 1, xb, xa);
     }
     // ---- transforms 2 and 3 from the relu'd accumulators (k-permuted images)
     f16x8 hh[AKP], hl[AKP];
-    auto relu_split = [&](const int32_t* q, const float* bias) {
+    auto relu_split = [&](int t, int ncb, const float* bias) {
+        const int32_t* const q = reinterpret_cast<const int32_t*>(img + t * HIMG + HIMG - AH * 4);
         uint32_t m = 0;
 #pragma unroll
         for (int cb = 0; cb < ACB; ++cb) {
+            if (cb >= ncb) break;
             const int4 qv = *reinterpret_cast<const int4*>(q + 16 * cb + 4 * g);
             const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + 16 * cb + 4 * g);
             const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
@@ -741,25 +721,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
 #pragma unroll
         for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    relu_split(QV, BV);                              // h1 = relu(x W1^T + b1)
+    relu_split(0, ACB, BV);                          // h1 = relu(x W1^T + b1)
 #pragma unroll
     for (int kc = 0; kc < AKP; ++kc) {
-        step_sync(AKP + kc);
-        mfma3(wl0 + ((AKP + kc) % 3) * ACHUNK, ACB, hh[kc], hl[kc]);
+        chunk_barrier();
+        w_dma(AKP + kc + 1);
+        mfma3(wl0 + ((AKP + kc) & 1) * ACHUNK, ACB, hh[kc], hl[kc]);
     }
-    relu_split(QV + 256, BV + 256);                  // h2 = relu(h1 W2^T + b2)
+    relu_split(1, ACB, BV + 256);                    // h2 = relu(h1 W2^T + b2)
 #pragma unroll
     for (int kc = 0; kc < AKP; ++kc) {
-        step_sync(2 * AKP + kc);
-        mfma3(wl0 + ((2 * AKP + kc) % 3) * ACHUNK, ACB / 2, hh[kc], hl[kc]);
+        chunk_barrier();
+        w_dma(2 * AKP + kc + 1);
+        mfma3(wl0 + ((2 * AKP + kc) & 1) * ACHUNK, ACB / 2, hh[kc], hl[kc]);
     }
-    __builtin_amdgcn_s_waitcnt(0x70);                // drain the dummy refills
     // ---- h3 = relu(h2 W3^T + b3): lane (r, g) holds h3[r][16 cb + 4 g + i], cb < 8;
     // out[r][o] = sum_k h3[k] W4[o][k] + b4[o] (fp32; summed over the row's 4 lanes)
+    const int32_t* const q3 = reinterpret_cast<const int32_t*>(img + 2 * HIMG + HIMG - AH * 4);
     float h3[ACB / 2][4];
 #pragma unroll
     for (int cb = 0; cb < ACB / 2; ++cb) {
-        const int4 qv = *reinterpret_cast<const int4*>(QV + 512 + 16 * cb + 4 * g);
+        const int4 qv = *reinterpret_cast<const int4*>(q3 + 16 * cb + 4 * g);
         const f32x4 bb = *reinterpret_cast<const f32x4*>(BV + 512 + 16 * cb + 4 * g);
         const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
@@ -779,11 +761,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
 #pragma unroll
                 for (int i = 0; i < 4; ++i) sacc = fmaf(h3[cb][i], wv[i], sacc);
             }
-            const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(sacc), __float_as_uint(sacc), false, false);
-            sacc = __uint_as_float(static_cast<uint32_t>(r16[0])) + __uint_as_float(static_cast<uint32_t>(r16[1]));
-            const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sacc), __float_as_uint(sacc), false, false);
-            sacc = __uint_as_float(static_cast<uint32_t>(r32[0])) + __uint_as_float(static_cast<uint32_t>(r32[1]));
-            sacc += BV[640 + oc];
+            sacc = rowsum4(sacc) + BV[640 + oc];
         }
         o[oc] = sacc;
     }
@@ -1039,6 +1017,369 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
                             lane, 16 * wave + r, g);
 }
 
+// ------------------------------------------------------------------ TransformerConv
+// H = 256, 4 heads (configs[3]; gnn_model.py:65-68, PyG TransformerConv,
+// concat=False, root_weight): with qt_i = [W_k^T q_i per head] (the Q~K
+// transform, one split-fp16 GEMM before this kernel; attn_layers.hip):
+//   s_ij^h  = qt_i^h . x_j / sqrt(C)                      (score, per head)
+//   a_ij^h  = softmax_j(s_ij^h)                           (PyG utils.softmax, +1e-16)
+//   out_i   = epi([sum_j a_ij^h x_j (4 heads) | sum_j a_ij^h | x_i] . wout^T + b)
+// in one kernel: pass 1 forms the 4 x 8 scores of a row's first 8 CSR entries
+// in registers (lane (r, g) dots its 64 columns, the row's 4 lanes sum), the
+// softmax statistics per head (online over further groups of 8 for longer
+// rows); pass 2 builds the weighted sums one 32-wide k chunk at a time for the
+// 4 heads in the MFMA B-operand layout and feeds them, split with the row's
+// online exponent, straight into the output transform (image k order: chunk
+// 4 kc + head, then x_i's 8 chunks, then the alpha-sum chunk --
+// mignn_transformer_fused_prep).  Neither the [rows, 4 x 256 + 4] aggregate
+// nor its re-read reach HBM.  Entries past the 8th: raw scores of the next 16
+// kept in LDS, later ones recomputed (correct, not fast).
+constexpr int TF_HEADS = 4;
+constexpr int TF_KIN = TF_HEADS * AH + TF_HEADS + AH;   // wout: [W_v / heads | b_v / heads | W_skip]
+constexpr int TF_NC = TF_HEADS * AKP + AKP + 1;          // 41 k chunks of the fused image
+constexpr size_t TF_IMG_FRAG = static_cast<size_t>(TF_NC) * ACB * 2 * AFRAG;
+constexpr size_t TF_IMG_BYTES = TF_IMG_FRAG + AH * 4;
+constexpr int TF_XS = 16;                                // extra raw scores per row kept in LDS
+constexpr float TF_EPS = 1e-16f;                         // PyG utils.softmax
+
+__device__ __forceinline__ int tf_src_k(int kk) {       // fused-image k -> wout column (-1: 0)
+    const int t = kk >> 5, i = kk & 31;
+    if (t < TF_HEADS * AKP) return (t & 3) * AH + 32 * (t >> 2) + i;
+    if (t < TF_HEADS * AKP + AKP) return TF_HEADS * AH + TF_HEADS + 32 * (t - TF_HEADS * AKP) + i;
+    return i < TF_HEADS ? TF_HEADS * AH + i : -1;
+}
+
+__global__ __launch_bounds__(256) void tf_prep_exp_kernel(const float* __restrict__ w,
+                                                          int32_t* __restrict__ q) {
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    uint32_t m = 0;
+    for (int i = lane; i < TF_KIN; i += 64) m = max(m, __float_as_uint(fabsf(w[c * TF_KIN + i])));
+    for (int o = 32; o > 0; o >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o)));
+    if (lane == 0) q[c] = sexp_ag(m);
+}
+
+__global__ __launch_bounds__(256) void tf_prep_frag_kernel(const float* __restrict__ w,
+                                                           const int32_t* __restrict__ q,
+                                                           unsigned char* __restrict__ img) {
+    const int t = blockIdx.x * 256 + threadIdx.x;        // (chunk, cb, lane)
+    if (t >= TF_NC * ACB * 64) return;
+    const int lane = t & 63, cb = (t >> 6) % ACB, kc = (t >> 6) / ACB;
+    const int c = 16 * cb + (lane & 15);
+    const float sc = p2_ag(q[c]);
+    f16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = tf_src_k(32 * kc + 8 * (lane >> 4) + j);
+        const float v = k >= 0 ? w[c * TF_KIN + k] * sc : 0.f;
+        const _Float16 hh = static_cast<_Float16>(v);
+        h[j] = hh;
+        l[j] = static_cast<_Float16>(v - static_cast<float>(hh));
+    }
+    unsigned char* base = img + ((static_cast<size_t>(kc) * ACB + cb) * 2) * AFRAG + lane * 16;
+    *reinterpret_cast<f16x8*>(base) = h;
+    *reinterpret_cast<f16x8*>(base + AFRAG) = l;
+}
+
+
+// Block: 8 waves x 16 rows (128-row tile), one block per CU.  LDS: W ring
+// [3][32 KB] (LDS-DMA two chunks ahead, one counted wait + barrier per chunk)
+// | per row TF_XS extra raw scores; after the loop the whole LDS is the
+// staged epilogue's (rows [128][1 KB] | q bias scale shift).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void tf_fused_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ qt, int64_t ldq, const float* __restrict__ x, int64_t ldx,
+    int64_t rb, int64_t re, float score_scale, const unsigned char* __restrict__ img,
+    const float* __restrict__ bias, const float* __restrict__ scale,
+    const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+    constexpr int AW = 8, BM = 16 * AW;
+    constexpr int WPC = ACHUNK / 1024 / AW;              // W pieces per wave per chunk (4)
+    constexpr int OFF_XS = 3 * ACHUNK;
+    constexpr int OFF_AL = OFF_XS + BM * TF_XS * 16;     // per row the 8 x 4 softmax weights
+    constexpr int LDS_BYTES = OFF_AL + BM * 128;
+    static_assert(OFF_AL >= BM * 1024 && LDS_BYTES >= BM * 1024 + 4 * AH * 4, "tf_fused LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t ntiles = (re - rb + BM - 1) / BM;
+    const int64_t per_xcd = gridDim.x >> 3;
+    const int64_t tile = static_cast<int64_t>(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;
+    const int64_t t0 = rb + tile * BM;
+    const int64_t row = t0 + 16 * wave + r;
+    const bool rv = row < re;
+    const int64_t rowc = rv ? row : re - 1;
+    const int lself = 16 * wave + r;
+
+    auto w_dma = [&](int c) {                  // chunk c -> buffer c % 3 (dummy past the last)
+        const int cc = c < TF_NC ? c : TF_NC - 1;
+        const unsigned char* src = img + static_cast<size_t>(cc) * ACHUNK;
+        unsigned char* dst = lds + (c % 3) * ACHUNK;
+#pragma unroll
+        for (int pc = 0; pc < WPC; ++pc) {
+            const int piece = wave + pc * AW;
+            glds16_ag(src + piece * 1024 + lane * 16, lds_addr_ag(dst + piece * 1024));
+        }
+    };
+    w_dma(0);
+    w_dma(1);
+
+    const int e0 = row_ptr[rowc];
+    const int deg = rv ? row_ptr[rowc + 1] - e0 : 0;
+    const float* const qrow = qt + rowc * ldq + 8 * g;
+    auto xrow = [&](int c) -> const float* {   // lane's columns of row c (the zero row for c < 0)
+        return c >= 0 ? x + static_cast<int64_t>(c) * ldx + 8 * g : g_zero_row_ag + 8 * g;
+    };
+    auto dot8 = [](const f32x4& a0, const f32x4& a1, const f32x4& b0, const f32x4& b1, float d) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d = fmaf(a0[i], b0[i], d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d = fmaf(a1[i], b1[i], d);
+        return d;
+    };
+    // scores of 8 entries (columns cj, -1 = none), 4 heads
+    auto scores8 = [&](const int (&cj)[8], float (&sc)[TF_HEADS][8]) {
+#pragma unroll
+        for (int h = 0; h < TF_HEADS; ++h)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sc[h][t] = 0.f;
+#pragma unroll 1
+        for (int kc = 0; kc < AKP; ++kc) {
+            f32x4 q0[TF_HEADS], q1[TF_HEADS];
+#pragma unroll
+            for (int h = 0; h < TF_HEADS; ++h) {
+                q0[h] = *reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc);
+                q1[h] = *reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc + 4);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const float* xp = xrow(cj[t]) + 32 * kc;
+                const f32x4 v0 = *reinterpret_cast<const f32x4*>(xp);
+                const f32x4 v1 = *reinterpret_cast<const f32x4*>(xp + 4);
+#pragma unroll
+                for (int h = 0; h < TF_HEADS; ++h) sc[h][t] = dot8(q0[h], q1[h], v0, v1, sc[h][t]);
+                if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < TF_HEADS; ++h)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sc[h][t] = rowsum4(sc[h][t]) * score_scale;
+    };
+    // the 4 scores of one entry (column c), recomputed
+    auto score1 = [&](int c, float (&r4)[TF_HEADS]) {
+        float d[TF_HEADS] = {0.f, 0.f, 0.f, 0.f};
+        const float* const xp0 = xrow(c);
+#pragma unroll 1
+        for (int kc = 0; kc < AKP; ++kc) {
+            const f32x4 v0 = *reinterpret_cast<const f32x4*>(xp0 + 32 * kc);
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(xp0 + 32 * kc + 4);
+#pragma unroll
+            for (int h = 0; h < TF_HEADS; ++h)
+                d[h] = dot8(*reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc),
+                            *reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc + 4), v0, v1, d[h]);
+        }
+#pragma unroll
+        for (int h = 0; h < TF_HEADS; ++h) r4[h] = rowsum4(d[h]) * score_scale;
+    };
+
+    // ---- pass 1: scores and softmax statistics
+    int cj[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) cj[t] = t < deg ? col[e0 + t] : -1;
+    float s[TF_HEADS][8];
+    if (flags & MIGNN_DIAG_NO_EXT) {           // (ablation: no pass 1)
+#pragma unroll
+        for (int h = 0; h < TF_HEADS; ++h)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) s[h][t] = 0.f;
+    } else {
+        scores8(cj, s);
+    }
+    float m[TF_HEADS], l[TF_HEADS];
+#pragma unroll
+    for (int h = 0; h < TF_HEADS; ++h) {
+        float mm = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (t < deg) mm = fmaxf(mm, s[h][t]);
+        float ll = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (t < deg) ll += expf(s[h][t] - mm);
+        m[h] = mm;
+        l[h] = ll;
+    }
+    const bool slow = deg > 8;
+    const bool any_slow = __builtin_amdgcn_ballot_w64(slow) != 0ull;
+    float* const XS = reinterpret_cast<float*>(lds + OFF_XS) + lself * TF_XS * 4;
+    if (any_slow && slow) {                    // further groups of 8: online statistics
+        for (int eb = 8; eb < deg; eb += 8) {
+            int cj2[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) cj2[t] = eb + t < deg ? col[e0 + eb + t] : -1;
+            float s2[TF_HEADS][8];
+            scores8(cj2, s2);
+#pragma unroll
+            for (int h = 0; h < TF_HEADS; ++h) {
+                float bm = -INFINITY;
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (eb + t < deg) bm = fmaxf(bm, s2[h][t]);
+                const float mn = fmaxf(m[h], bm);
+                float ll = l[h] * expf(m[h] - mn);
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (eb + t < deg) ll += expf(s2[h][t] - mn);
+                m[h] = mn;
+                l[h] = ll;
+            }
+            if (g == 0) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (eb + t < deg && eb + t - 8 < TF_XS)
+                        *reinterpret_cast<f32x4*>(XS + 4 * (eb + t - 8)) =
+                            f32x4{s2[0][t], s2[1][t], s2[2][t], s2[3][t]};
+            }
+        }
+    }
+    // softmax weights of the first 8 entries -> LDS (entry t: 4 heads; lane
+    // group g writes entries 2g, 2g + 1; read back by the row's 4 lanes)
+    float inv[TF_HEADS];
+#pragma unroll
+    for (int h = 0; h < TF_HEADS; ++h) inv[h] = 1.f / (l[h] + TF_EPS);
+    float* const AL = reinterpret_cast<float*>(lds + OFF_AL) + lself * 32;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        f32x4 av;
+#pragma unroll
+        for (int h = 0; h < TF_HEADS; ++h) av[h] = t < deg ? expf(s[h][t] - m[h]) * inv[h] : 0.f;
+        if ((t >> 1) == g) *reinterpret_cast<f32x4*>(AL + 4 * t) = av;
+    }
+
+    // ---- pass 2: weighted sums -> output transform (41 k chunks)
+    f32x4 acc[ACB];
+#pragma unroll
+    for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int p = 100;
+    int c = 0;
+    const unsigned char* const wl0 = lds + lane * 16;
+    auto step = [&](const f32x4& a0, const f32x4& a1) {
+        // split with the row's online exponent
+        uint32_t mb = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            mb = max(mb, max(__float_as_uint(fabsf(a0[i])), __float_as_uint(fabsf(a1[i]))));
+        const int pc = sexp_ag(rowmax4(mb));
+        if (pc < p) {
+#pragma unroll
+            for (int cb = 0; cb < ACB; ++cb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
+            p = pc;
+        }
+        const float spv = p2_ag(p);
+        f16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float v = (j < 4 ? a0[j] : a1[j - 4]) * spv;
+            const _Float16 hh = static_cast<_Float16>(v);
+            bh[j] = hh;
+            bl[j] = static_cast<_Float16>(v - static_cast<float>(hh));
+        }
+        // chunk c landed (only chunk c + 1's pieces may fly), every wave done
+        // with the buffer refilled next
+        vm_barrier<WPC>();
+        w_dma(c + 2);
+        const unsigned char* wb = wl0 + (c % 3) * ACHUNK;
+#pragma unroll
+        for (int cb = 0; cb < ACB; ++cb) {
+            if (flags & MIGNN_DIAG_NO_MFMA) break;
+            const f16x8 wh = *reinterpret_cast<const f16x8*>(wb + (2 * cb) * AFRAG);
+            const f16x8 wl = *reinterpret_cast<const f16x8*>(wb + (2 * cb + 1) * AFRAG);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, acc[cb], 0, 0, 0);
+        }
+        ++c;
+    };
+#pragma unroll 1
+    for (int kc = 0; kc < AKP; ++kc) {
+        f32x4 a0[TF_HEADS], a1[TF_HEADS];
+#pragma unroll
+        for (int h = 0; h < TF_HEADS; ++h) a0[h] = a1[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (flags & MIGNN_DIAG_NO_PRODUCE) break;   // (ablation: no weighted sums)
+            const float* xp = xrow(cj[t]) + 32 * kc;
+            const f32x4 v0 = *reinterpret_cast<const f32x4*>(xp);
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(xp + 4);
+            const f32x4 av = *reinterpret_cast<const f32x4*>(AL + 4 * t);
+#pragma unroll
+            for (int h = 0; h < TF_HEADS; ++h)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    a0[h][i] = fmaf(av[h], v0[i], a0[h][i]);
+                    a1[h][i] = fmaf(av[h], v1[i], a1[h][i]);
+                }
+            if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        if (any_slow && slow) {
+            for (int e = 8; e < deg; ++e) {
+                const int ce = col[e0 + e];
+                float r4[TF_HEADS];
+                if (e - 8 < TF_XS) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(XS + 4 * (e - 8));
+#pragma unroll
+                    for (int h = 0; h < TF_HEADS; ++h) r4[h] = v[h];
+                } else {
+                    score1(ce, r4);
+                }
+                const float* xp = xrow(ce) + 32 * kc;
+                const f32x4 v0 = *reinterpret_cast<const f32x4*>(xp);
+                const f32x4 v1 = *reinterpret_cast<const f32x4*>(xp + 4);
+#pragma unroll
+                for (int h = 0; h < TF_HEADS; ++h) {
+                    const float a = expf(r4[h] - m[h]) * inv[h];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        a0[h][i] = fmaf(a, v0[i], a0[h][i]);
+                        a1[h][i] = fmaf(a, v1[i], a1[h][i]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < TF_HEADS; ++h) step(a0[h], a1[h]);
+    }
+    // x_i (lin_skip), 8 chunks
+    const float* const xi = x + rowc * ldx + 8 * g;
+#pragma unroll 1
+    for (int kc = 0; kc < AKP; ++kc)
+        step(*reinterpret_cast<const f32x4*>(xi + 32 * kc), *reinterpret_cast<const f32x4*>(xi + 32 * kc + 4));
+    // alpha sums (x b_v / heads): k = 0..3 of the last chunk, lane group 0
+    {
+        f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (g == 0) a0 = f32x4{l[0] * inv[0], l[1] * inv[1], l[2] * inv[2], l[3] * inv[3]};
+        step(a0, f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+
+    // ---- epilogue: drain (the dummy refills), LDS free -> staged epilogue
+    vm_barrier<0>();
+    const bool hb = (flags & MIGNN_EPI_BIAS) != 0, ha = (flags & MIGNN_EPI_AFFINE) != 0;
+    float* const EV = reinterpret_cast<float*>(lds + BM * 1024);   // q | bias | scale | shift
+    if (tid < AH) {
+        reinterpret_cast<int32_t*>(EV)[tid] = reinterpret_cast<const int32_t*>(img + TF_IMG_FRAG)[tid];
+        EV[AH + tid] = hb ? bias[tid] : 0.f;
+        EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
+        EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
+    }
+    staged_epilogue<ACB>(lds, EV, acc, p, flags, x, ldx, out, ldo, t0, re, wave, lane, lself, g);
+}
+
 template <int MODE, bool CHAIN>
 int launch_agg_gemm(const int32_t* row_ptr, const int32_t* col, const float* ew, const float* x,
                     int64_t ldx, int64_t rb, int64_t re, float self_scale, const void* img1,
@@ -1189,5 +1530,40 @@ int head256(const float* x, int64_t ldx, int64_t n, const void* img, int out_dim
                        as_stream(stream), x, ldx, n, static_cast<const unsigned char*>(img),
                        out_dim, out, ldo, out_rows);
     return launch_status("head256_kernel");
+}
+}  // namespace mignn
+
+// ------------------------------------------------------------------ TransformerConv, fused
+namespace mignn {
+size_t tf_fused_prep_bytes() { return TF_IMG_BYTES; }
+
+int tf_fused_prep(const float* wout, void* img, void* stream) {
+    hipStream_t st = as_stream(stream);
+    auto* base = static_cast<unsigned char*>(img);
+    int32_t* q = reinterpret_cast<int32_t*>(base + TF_IMG_FRAG);
+    hipLaunchKernelGGL(tf_prep_exp_kernel, dim3(AH / 4), dim3(256), 0, st, wout, q);
+    if (int rc = launch_status("tf_prep_exp_kernel")) return rc;
+    hipLaunchKernelGGL(tf_prep_frag_kernel, dim3((TF_NC * ACB * 64 + 255) / 256), dim3(256), 0, st,
+                       wout, q, base);
+    return launch_status("tf_prep_frag_kernel");
+}
+
+int tf_fused(const int32_t* row_ptr, const int32_t* col, const float* qt, int64_t ldq,
+             const float* x, int64_t ldx, int64_t rb, int64_t re, float score_scale,
+             const void* img, const float* bias, const float* scale, const float* shift, int flags,
+             float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(aligned16(x) && aligned16(out) && aligned16(img) && aligned16(qt) &&
+                      ldx % 4 == 0 && ldo % 4 == 0 && ldq % 4 == 0 && ldq >= TF_HEADS * AH,
+                  "transformer_layer: fused path needs 16-B aligned rows");
+    MIGNN_REQUIRE(x != out, "transformer_layer: in-place not supported (neighbours read x)");
+    constexpr int BM = 128;
+    const int64_t ntiles = (re - rb + BM - 1) / BM;
+    const int64_t nb = (ntiles + 7) / 8 * 8;
+    MIGNN_REQUIRE(nb < (int64_t(1) << 31), "transformer_layer: too many rows");
+    hipLaunchKernelGGL(tf_fused_kernel, dim3(static_cast<unsigned>(nb)), dim3(512), 0,
+                       as_stream(stream), row_ptr, col, qt, ldq, x, ldx, rb, re, score_scale,
+                       static_cast<const unsigned char*>(img), bias, scale, shift,
+                       flags | g_fused_diag_flags, out, ldo);
+    return launch_status("tf_fused_kernel");
 }
 }  // namespace mignn

@@ -144,6 +144,47 @@ extern "C" int mignn_transformer_layer(const int32_t* row_ptr, const int32_t* co
                      stream);
 }
 
+extern "C" size_t mignn_transformer_fused_prep_bytes(int h, int heads) {
+    return h == 256 && heads == 4 ? tf_fused_prep_bytes() : 0;
+}
+
+extern "C" int mignn_transformer_fused_prep(const float* wout, int h, int heads, void* img,
+                                            size_t img_bytes, void* stream) {
+    MIGNN_REQUIRE(wout && img, "transformer_fused_prep: null pointer");
+    MIGNN_REQUIRE(h == 256 && heads == 4, "transformer_fused_prep: h = 256, heads = 4 only");
+    MIGNN_REQUIRE(img_bytes >= tf_fused_prep_bytes(), "transformer_fused_prep: image too small");
+    MIGNN_REQUIRE(aligned16(img), "transformer_fused_prep: image not 16-B aligned");
+    return tf_fused_prep(wout, img, stream);
+}
+
+extern "C" int mignn_transformer_layer_fused(
+    const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx, int64_t row_begin,
+    int64_t row_end, int h, int heads, float score_scale, const void* wqk_img, const float* bqk,
+    const void* wout_fimg, const float* bout, const float* scale, const float* shift, int flags,
+    void* scratch, size_t scratch_bytes, float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "transformer_layer_fused: unknown flags 0x%x",
+                  flags);
+    MIGNN_REQUIRE(row_ptr && col && x && out && bqk && wqk_img && wout_fimg,
+                  "transformer_layer_fused: null pointer");
+    MIGNN_REQUIRE(h == 256 && heads == 4, "transformer_layer_fused: h = 256, heads = 4 only");
+    MIGNN_REQUIRE(row_begin >= 0 && row_end >= row_begin, "transformer_layer_fused: bad row range");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "transformer_layer_fused: affine");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bout, "transformer_layer_fused: bias");
+    const int64_t rows = row_end - row_begin;
+    if (rows == 0) return MIGNN_OK;
+    const size_t need = mignn_transformer_layer_scratch_bytes(rows, h, heads);
+    MIGNN_REQUIRE(scratch && aligned16(scratch) && scratch_bytes >= need,
+                  "transformer_layer_fused: scratch %zu < required %zu", scratch_bytes, need);
+    const int64_t ldq = static_cast<int64_t>(heads) * h;   // qt rows: 4 x 256 floats
+    float* qt = static_cast<float*>(scratch);
+    if (int rc = mignn_linear_f16x3(x + row_begin * ldx, ldx, rows, h, nullptr, 0, 0, wqk_img,
+                                    heads * h, bqk, nullptr, 0, nullptr, nullptr, MIGNN_EPI_BIAS,
+                                    qt, ldq, stream))
+        return rc;
+    return tf_fused(row_ptr, col, qt - row_begin * ldq, ldq, x, ldx, row_begin, row_end,
+                    score_scale, wout_fimg, bout, scale, shift, flags, out, ldo, stream);
+}
+
 extern "C" int mignn_diag_set_gat_fused(int on) {
     g_gat_fused = on != 0;
     return MIGNN_OK;

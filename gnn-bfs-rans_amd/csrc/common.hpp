@@ -165,6 +165,14 @@ int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* log
                     const float* x, int64_t ldx, int64_t rb, int64_t re, int h, float slope,
                     const void* img, const float* bias, const float* scale, const float* shift,
                     int flags, float* out, int64_t ldo, void* stream);
+// the fused TransformerConv (H = 256, 4 heads; agg_gemm.hip): image of wout
+// in the fused k order, and the aggregate + output transform kernel over qt
+size_t tf_fused_prep_bytes();
+int tf_fused_prep(const float* wout, void* img, void* stream);
+int tf_fused(const int32_t* row_ptr, const int32_t* col, const float* qt, int64_t ldq,
+             const float* x, int64_t ldx, int64_t rb, int64_t re, float score_scale,
+             const void* img, const float* bias, const float* scale, const float* shift, int flags,
+             float* out, int64_t ldo, void* stream);
 // the fused H = 256 output head (agg_gemm.hip), arguments checked by mlp_f16x3.hip
 size_t head256_prep_bytes();
 int head256_prep(const float* w1, const float* b1, const float* w2, const float* b2,

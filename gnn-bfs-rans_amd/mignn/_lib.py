@@ -51,6 +51,11 @@ SIGNATURES = {
     "mignn_transformer_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_int,
                                         c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int, _P,
                                         c_size_t, _P, c_int64, _P]),
+    "mignn_transformer_fused_prep_bytes": (c_size_t, [c_int, c_int]),
+    "mignn_transformer_fused_prep": (c_int, [_P, c_int, c_int, _P, c_size_t, _P]),
+    "mignn_transformer_layer_fused": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_int,
+                                              c_float, _P, _P, _P, _P, _P, _P, c_int, _P, c_size_t,
+                                              _P, c_int64, _P]),
     "mignn_transformer_aggregate": (c_int, [_P, _P, _P, c_int64, _P, c_int64, c_int64, c_int64,
                                             c_int, c_int, c_float, _P, c_int64, _P]),
     "mignn_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P, _P,

@@ -787,9 +787,24 @@ class FlowGNN(nn.Module):
             # one C-ABI call (csrc/attn_layers.hip): Q~K transform, softmax
             # aggregation, output transform over [agg | x]
             img_q = self._img("w_tfq", i, ts, wqk)
-            img_o = self._img("w_tfo", i, ts, wout)
             nb = L.mignn_transformer_layer_scratch_bytes(n, H, HEADS)
             scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
+            if H == 256 and HEADS == 4 and self._fused256():
+                # aggregation + output transform in one kernel (agg_gemm.hip)
+                def make():
+                    img = torch.empty(L.mignn_transformer_fused_prep_bytes(H, HEADS),
+                                      dtype=torch.uint8, device=x.device)
+                    _lib.check(L.mignn_transformer_fused_prep(P(wout), H, HEADS, P(img),
+                                                              img.numel(), st),
+                               "mignn_transformer_fused_prep")
+                    return img
+                fimg = self._cached("w_tff", i, ts, make)
+                _lib.check(L.mignn_transformer_layer_fused(
+                    P(csr.row_ptr), P(csr.col), P(x), x.stride(0), rb, re, H, HEADS,
+                    1.0 / math.sqrt(H), P(img_q), P(bqk), P(fimg), P(bout), P(scale), P(shift),
+                    epi, P(scratch), nb, P(out), out.stride(0), st), "mignn_transformer_layer_fused")
+                return
+            img_o = self._img("w_tfo", i, ts, wout)
             _lib.check(L.mignn_transformer_layer(
                 P(csr.row_ptr), P(csr.col), P(x), x.stride(0), rb, re, H, HEADS,
                 1.0 / math.sqrt(H), P(wqk), P(img_q), P(bqk), P(wout), P(img_o), P(bout),

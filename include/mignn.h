@@ -215,6 +215,23 @@ int mignn_transformer_layer(const int32_t* row_ptr, const int32_t* col, const fl
                             const float* bout, const float* scale, const float* shift, int flags,
                             void* scratch, size_t scratch_bytes, float* out, int64_t ldo,
                             void* stream);
+/* TransformerConv at h = 256, 4 heads (configs[3]) with the aggregation and
+ * the output transform in one kernel (the [rows, heads*h + heads] aggregate
+ * never reaches memory): qt = x wqk^T + bqk (split-fp16 GEMM into scratch),
+ * then per row the scores, softmax and weighted sums feed the output
+ * transform directly.  wout_fimg: mignn_transformer_fused_prep's image of
+ * wout (same wout as mignn_transformer_layer, k reordered for the kernel);
+ * the other arguments and the scratch size as mignn_transformer_layer.
+ * Rows with more than 24 CSR entries are correct, not fast. */
+size_t mignn_transformer_fused_prep_bytes(int h, int heads);
+int mignn_transformer_fused_prep(const float* wout, int h, int heads, void* img, size_t img_bytes,
+                                 void* stream);
+int mignn_transformer_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* x,
+                                  int64_t ldx, int64_t row_begin, int64_t row_end, int h,
+                                  int heads, float score_scale, const void* wqk_img,
+                                  const float* bqk, const void* wout_fimg, const float* bout,
+                                  const float* scale, const float* shift, int flags, void* scratch,
+                                  size_t scratch_bytes, float* out, int64_t ldo, void* stream);
 
 /* PyG gcn_norm edge weights per CSR entry (rows [row_begin, row_end)):
  *   ew[e] = dinv[col[e]] * dinv[i]   (= dinv[src] * 1 * dinv[dst], GCNConv gnn_model.py:63) */

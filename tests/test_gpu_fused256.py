@@ -252,3 +252,92 @@ def test_gat_fused_vs_launches_and_fp64(h, flags):
     ref, mag = _epi64(agg @ W.T, aggm @ W.T.abs(), X, bias.cpu(), sc.cpu(), sh.cpu(), flags)
     _check(got[rb:re], ref[rb:re], mag[rb:re], f"gat fused h={h}")
     _check(launches[rb:re], ref[rb:re], mag[rb:re], f"gat launches h={h}")
+
+
+def _tf_layer(fused, csr, x, rb, re, wqk, bqk, wout, bout, sc, sh, flags, out):
+    L = _lib.lib()
+    P = _lib.ptr
+    nb = L.mignn_transformer_layer_scratch_bytes(re - rb, H, 4)
+    scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=DEV)
+    img_q = f16x3_image(wqk)
+    if fused:
+        fimg = torch.empty(L.mignn_transformer_fused_prep_bytes(H, 4), dtype=torch.uint8,
+                           device=DEV)
+        _lib.check(L.mignn_transformer_fused_prep(P(wout), H, 4, P(fimg), fimg.numel(),
+                                                  _lib.stream()), "tf_fused_prep")
+        _lib.check(L.mignn_transformer_layer_fused(
+            P(csr.row_ptr), P(csr.col), P(x), H, rb, re, H, 4, 1.0 / 16, P(img_q), P(bqk), P(fimg),
+            P(bout), P(sc), P(sh), flags, P(scratch), nb, P(out), H, _lib.stream()), "tf_fused")
+    else:
+        _lib.check(L.mignn_transformer_layer(
+            P(csr.row_ptr), P(csr.col), P(x), H, rb, re, H, 4, 1.0 / 16, P(wqk), P(img_q), P(bqk),
+            P(wout), P(f16x3_image(wout)), P(bout), P(sc), P(sh), flags, P(scratch), nb, P(out), H,
+            _lib.stream()), "tf_layer")
+
+
+@pytest.mark.parametrize("flags", [15, 1 | 2])
+def test_transformer_fused_vs_launches_and_fp64(flags):
+    """mignn_transformer_layer_fused (scores, softmax, weighted sums and the
+    output transform in one kernel) against mignn_transformer_layer's launch
+    sequence and a float64 restatement (PyG TransformerConv on the CSR, 4
+    heads, concat=False, root weight: softmax + 1e-16 of q_i . k_j / sqrt(C),
+    head mean of the weighted values, + lin_skip) in the re-associated weights
+    the layer takes (wqk = Wk^T Wq, wout = [Wv / 4 | bv / 4 | W_skip]).  The
+    graph has empty rows and hub rows of 40-60 entries (past the kernel's 8
+    register slots and 16 LDS-kept scores: the recompute path); a row range."""
+    n = 3000
+    rb, re = 45, 2980
+    ei = _graph(n, 31)
+    csr = build_csr(ei, n, _lib.CSR_VERBATIM)
+    g = torch.Generator(device=DEV).manual_seed(flags)
+    x = torch.randn(n, H, device=DEV, generator=g)
+    x *= torch.pow(2.0, torch.randint(-3, 4, (n, 1), device=DEV, generator=g).float())
+    wqk = torch.randn(4 * H, H, device=DEV, generator=g) / 16
+    bqk = torch.randn(4 * H, device=DEV, generator=g) * 0.1
+    wout = torch.randn(H, 4 * H + 4 + H, device=DEV, generator=g) / (4 * H + 4 + H) ** 0.5
+    bout = torch.randn(H, device=DEV, generator=g) * 0.1
+    sc = torch.rand(H, device=DEV, generator=g) + 0.5
+    sh = torch.randn(H, device=DEV, generator=g) * 0.1
+    outs = []
+    for fused in (True, False):
+        o = torch.full((n, H), float("nan"), device=DEV)
+        _tf_layer(fused, csr, x, rb, re, wqk, bqk, wout, bout, sc, sh, flags, o)
+        outs.append(o)
+    torch.cuda.synchronize()
+    got, launches = outs[0].cpu(), outs[1].cpu()
+    assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
+    col, dst = _csr_edges(csr, n)
+    X = x.double().cpu()
+    qt = X @ wqk.double().cpu().T + bqk.double().cpu()              # [n, 4H]
+    s = (qt[dst].view(-1, 4, H) * X[col][:, None, :]).sum(-1) / 16   # [E, 4]
+    mx = torch.full((n, 4), -float("inf"), dtype=torch.float64).scatter_reduce(
+        0, dst[:, None].expand_as(s), s, "amax", include_self=True)
+    pexp = torch.exp(s - mx[dst])
+    sm = torch.zeros((n, 4), dtype=torch.float64).index_add_(0, dst, pexp) + 1e-16
+    alpha = pexp / sm[dst]
+    agg = torch.zeros((n, 4, H), dtype=torch.float64).index_add_(
+        0, dst, alpha[:, :, None] * X[col][:, None, :]).reshape(n, 4 * H)
+    asum = torch.zeros((n, 4), dtype=torch.float64).index_add_(0, dst, alpha)
+    aggm = torch.zeros((n, 4, H), dtype=torch.float64).index_add_(
+        0, dst, alpha[:, :, None] * X[col].abs()[:, None, :]).reshape(n, 4 * H)
+    W = wout.double().cpu()
+    c = torch.cat([agg, asum, X], 1) @ W.T
+    cm = torch.cat([aggm, asum, X.abs()], 1) @ W.T.abs()
+    ref, mag = _epi64(c, cm, X, bout.cpu(), sc.cpu(), sh.cpu(), flags)
+    # the scores carry the Q~K transform's split-fp16 error into the softmax:
+    # bound scaled by 4 (|score| <~ 10 here)
+    err_f = ((got[rb:re].double() - ref[rb:re]).abs() / (mag[rb:re] + 1e-30)).max().item()
+    err_l = ((launches[rb:re].double() - ref[rb:re]).abs() / (mag[rb:re] + 1e-30)).max().item()
+    assert err_f <= 1.6e-5 and err_l <= 1.6e-5, (err_f, err_l)
+    d = (got[rb:re] - launches[rb:re]).abs().max().item()
+    assert d <= 2e-5 * max(1.0, ref[rb:re].abs().max().item()), d
+
+
+def test_transformer_fused_prep_rejects():
+    L = _lib.lib()
+    assert L.mignn_transformer_fused_prep_bytes(128, 4) == 0
+    assert L.mignn_transformer_fused_prep_bytes(256, 4) == 41 * 16 * 2 * 1024 + 1024
+    img = torch.empty(16, dtype=torch.uint8, device=DEV)
+    w = torch.zeros(H, 4 * H + 4 + H, device=DEV)
+    assert L.mignn_transformer_fused_prep(_lib.ptr(w), 128, 4, _lib.ptr(img), 16, None) == 1
+    assert L.mignn_transformer_fused_prep(_lib.ptr(w), 256, 4, _lib.ptr(img), 16, None) == 1
