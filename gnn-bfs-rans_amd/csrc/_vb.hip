@@ -1146,7 +1146,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
         for (int h = 0; h < TF_HEADS; ++h)
 #pragma unroll
             for (int t = 0; t < 8; ++t) sc[h][t] = 0.f;
-#pragma unroll 1
+#pragma unroll 2
         for (int kc = 0; kc < AKP; ++kc) {
             f32x4 q0[TF_HEADS], q1[TF_HEADS];
 #pragma unroll
@@ -1161,7 +1161,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
                 const f32x4 v1 = *reinterpret_cast<const f32x4*>(xp + 4);
 #pragma unroll
                 for (int h = 0; h < TF_HEADS; ++h) sc[h][t] = dot8(q0[h], q1[h], v0, v1, sc[h][t]);
-                if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
         }
 #pragma unroll
@@ -1325,7 +1324,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
                     a0[h][i] = fmaf(av[h], v0[i], a0[h][i]);
                     a1[h][i] = fmaf(av[h], v1[i], a1[h][i]);
                 }
-            if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         if (any_slow && slow) {
             for (int e = 8; e < deg; ++e) {
@@ -1560,11 +1558,10 @@ int tf_fused(const int32_t* row_ptr, const int32_t* col, const float* qt, int64_
     const int64_t ntiles = (re - rb + BM - 1) / BM;
     const int64_t nb = (ntiles + 7) / 8 * 8;
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "transformer_layer: too many rows");
-    const auto* im = static_cast<const unsigned char*>(img);
-    flags |= g_fused_diag_flags;
-hipLaunchKernelGGL(tf_fused_kernel, dim3(static_cast<unsigned>(nb)), dim3(512), 0,
-                       as_stream(stream), row_ptr, col, qt, ldq, x, ldx, rb, re, score_scale, im,
-                       bias, scale, shift, flags, out, ldo);
+    hipLaunchKernelGGL(tf_fused_kernel, dim3(static_cast<unsigned>(nb)), dim3(512), 0,
+                       as_stream(stream), row_ptr, col, qt, ldq, x, ldx, rb, re, score_scale,
+                       static_cast<const unsigned char*>(img), bias, scale, shift,
+                       flags | g_fused_diag_flags, out, ldo);
     return launch_status("tf_fused_kernel");
 }
 }  // namespace mignn

@@ -65,6 +65,7 @@ cases = {"fused": fused, "launches": launches, "qk_gemm": qk_gemm}
 # ablations (wrong results; timing only): 4096 no pass 1, 256 no weighted sums, 512 no MFMA
 for dflag in [int(v) for v in os.environ.get("TB_ABLATE", "").split(",") if v]:
     cases[f"fused_ablate_{dflag}"] = (lambda d: (lambda Y: fused(Y, d)))(dflag)
+
 outs = {k: torch.full_like(X, float("nan")) for k in ("fused", "launches")}
 for k in outs:
     cases[k](outs[k])
