@@ -1133,12 +1133,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
     auto xrow = [&](int c) -> const float* {   // lane's columns of row c (the zero row for c < 0)
         return c >= 0 ? x + static_cast<int64_t>(c) * ldx + 8 * g : g_zero_row_ag + 8 * g;
     };
+    // 8-term dot as a pairwise tree (the score's rounding: short chains, as
+    // transformer_aggregate's per-lane dots + tree reduction)
     auto dot8 = [](const f32x4& a0, const f32x4& a1, const f32x4& b0, const f32x4& b1, float d) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) d = fmaf(a0[i], b0[i], d);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) d = fmaf(a1[i], b1[i], d);
-        return d;
+        const float p0 = fmaf(a0[1], b0[1], a0[0] * b0[0]);
+        const float p1 = fmaf(a0[3], b0[3], a0[2] * b0[2]);
+        const float p2 = fmaf(a1[1], b1[1], a1[0] * b1[0]);
+        const float p3 = fmaf(a1[3], b1[3], a1[2] * b1[2]);
+        return d + ((p0 + p1) + (p2 + p3));
     };
     // scores of 8 entries (columns cj, -1 = none), 4 heads
     auto scores8 = [&](const int (&cj)[8], float (&sc)[TF_HEADS][8]) {
@@ -1160,7 +1162,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
                 const f32x4 v0 = *reinterpret_cast<const f32x4*>(xp);
                 const f32x4 v1 = *reinterpret_cast<const f32x4*>(xp + 4);
 #pragma unroll
-                for (int h = 0; h < TF_HEADS; ++h) sc[h][t] = dot8(q0[h], q1[h], v0, v1, sc[h][t]);
+                for (int h = 0; h < TF_HEADS; ++h) sc[h][t] += dot8(q0[h], q1[h], v0, v1, 0.f);
                 if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -1179,8 +1181,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
             const f32x4 v1 = *reinterpret_cast<const f32x4*>(xp0 + 32 * kc + 4);
 #pragma unroll
             for (int h = 0; h < TF_HEADS; ++h)
-                d[h] = dot8(*reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc),
-                            *reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc + 4), v0, v1, d[h]);
+                d[h] += dot8(*reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc),
+                             *reinterpret_cast<const f32x4*>(qrow + h * AH + 32 * kc + 4), v0, v1, 0.f);
         }
 #pragma unroll
         for (int h = 0; h < TF_HEADS; ++h) r4[h] = rowsum4(d[h]) * score_scale;

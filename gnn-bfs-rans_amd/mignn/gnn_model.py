@@ -685,11 +685,15 @@ class FlowGNN(nn.Module):
             return self._cached(tag, i, srcs, lambda: f16x3_image(w))
         return None
 
-    def _fused256(self) -> bool:
-        """H = 256 GIN / GCN layers as one fused kernel (mignn_gin_layer_fused /
-        mignn_gcn_layer_fused; split-fp16 arithmetic) -- the default in f16x3
-        precision; MIGNN_FUSED256=0 runs the aggregate + GEMM launches instead."""
-        return self.precision == "f16x3" and os.environ.get("MIGNN_FUSED256", "1") != "0"
+    def _fused256(self, part: str = "layer") -> bool:
+        """The H = 256 fused kernels (split-fp16 arithmetic) -- the default in
+        f16x3 precision: GIN / GCN / TransformerConv layers (mignn_gin_layer_fused,
+        mignn_gcn_layer_fused, mignn_transformer_layer_fused; part "layer") and
+        the output head (mignn_mlp_head at h = 256; part "head").
+        MIGNN_FUSED256=0 runs the aggregate + GEMM launches for both, "layer" /
+        "head" keeps only that part fused."""
+        v = os.environ.get("MIGNN_FUSED256", "1")
+        return self.precision == "f16x3" and (v == "1" or v == part)
 
     def _mm(self, tag, i, srcs, w, a, bias=None, **kw):
         """Node transform by W = w: split-fp16 GEMM (mignn_linear_f16x3) or
@@ -854,7 +858,7 @@ class FlowGNN(nn.Module):
         l0, l3, l6, l8 = (self.output_proj[i] for i in (0, 3, 6, 8))
         H = self.hidden_dim
         if (self.precision == "f16x3" and self.output_dim <= 8
-                and (H in (64, 128) or (H == 256 and self._fused256()))):
+                and (H in (64, 128) or (H == 256 and self._fused256("head")))):
             L = _lib.lib()
             P = _lib.ptr
             ts = (l0.weight, l0.bias, l3.weight, l3.bias, l6.weight, l6.bias, l8.weight,
