@@ -119,18 +119,22 @@ __device__ __forceinline__ float rowsum4(float v) {
 // the wave stores whole rows (the accumulator layout would store 16 rows x
 // 64 B per instruction).  EV = [q (int) | bias | scale | shift][NCB*16] in LDS,
 // written by the caller before the call.
-template <int NCB>
+// CRES: the residual is not read but computed, x_i[n] = TB[n] . (c0, c1, c2, 1)
+// (GIN layer 0 from the coordinates: x = input_proj(pos), TB = [W_in | b_in])
+template <int NCB, bool CRES = false>
 __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float* EV,
                                                 const f32x4 (&acc)[NCB], int p, int flags,
                                                 const float* __restrict__ x, int64_t ldx,
                                                 float* __restrict__ out, int64_t ldo, int64_t t0,
-                                                int64_t re, int wave, int lane, int lself, int g) {
+                                                int64_t re, int wave, int lane, int lself, int g,
+                                                const float* TB = nullptr, float c0 = 0.f,
+                                                float c1 = 0.f, float c2 = 0.f) {
     constexpr int N = NCB * 16, CPR = NCB * 4, ROWB = NCB * 64, RPI = 64 / CPR, NI = 16 / RPI;
     const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
     int l = lane;
     asm volatile("" : "+v"(l));
     const int ci = l % CPR, ri = l / CPR;
-    if (res) {
+    if (res && !CRES) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int li = 16 * wave + RPI * i + ri;
@@ -146,7 +150,18 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
     for (int cb = 0; cb < NCB; ++cb) {
         const int n = 16 * cb + 4 * g;
         f32x4* const slot = reinterpret_cast<f32x4*>(srow + 16 * ((4 * cb + g) ^ (lself & 15)));
-        const f32x4 xv = res ? *slot : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (CRES) {
+            if (res) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const f32x4 t = *reinterpret_cast<const f32x4*>(TB + 4 * (n + i));
+                    xv[i] = fmaf(t[2], c2, fmaf(t[1], c1, fmaf(t[0], c0, t[3])));
+                }
+            }
+        } else if (res) {
+            xv = *slot;
+        }
         const int4 q = *reinterpret_cast<const int4*>(EQ + n);
         const f32x4 bo = *reinterpret_cast<const f32x4*>(EV + N + n);
         const f32x4 so = *reinterpret_cast<const f32x4*>(EV + 2 * N + n);
@@ -498,6 +513,183 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
         EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
     }
     staged_epilogue<ACB>(lds, EV, acc, p, flags, x, ldx, out, ldo, t0, re, wave, lane, lself, g);
+}
+
+// GIN layer 0 at H = 256 from the coordinates (input_proj composed into the
+// aggregate, as gcn_layer0.hip does for GCN): with x = pos W_in^T + b_in,
+//   a_i = sum_j x_j + (1 + eps) x_i = W_in P_i + c_i b_in,
+//   P_i = sum_j pos_j + (1 + eps) pos_i,  c_i = deg_i + 1 + eps,
+// so the layer reads 12 B of coordinates per CSR entry instead of a 1-KB row,
+// and input_proj's [N, 256] output is never written.  The chain (nn.0, ReLU,
+// nn.2) and the epilogue are agg_gemm_kernel<AGG_GIN, true>'s; the residual
+// x_i is recomputed from pos_i.  LDS: W ring [2][32 KB] | (epilogue: staging
+// rows [128][1 KB] | q bias scale shift) | [W_in | b_in] table [256][4].
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void gin0_fused_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ pos, int64_t ldp, int D, int64_t rb, int64_t re, float self_scale,
+    const float* __restrict__ w_in, const float* __restrict__ b_in,
+    const unsigned char* __restrict__ img1, const float* __restrict__ b1,
+    const unsigned char* __restrict__ img2, const float* __restrict__ b2,
+    const float* __restrict__ scale, const float* __restrict__ shift, int flags,
+    float* __restrict__ out, int64_t ldo) {
+    constexpr int AW = 8, BM = 16 * AW;
+    constexpr int WPC = ACHUNK / 1024 / AW;
+    constexpr size_t FB = static_cast<size_t>(AKP) * ACB * 2 * AFRAG;
+    constexpr int OFF_EV = BM * 1024;
+    constexpr int OFF_TB = OFF_EV + 4 * AH * 4;
+    constexpr int LDS_BYTES = OFF_TB + AH * 16;
+    static_assert(LDS_BYTES <= 160 * 1024, "gin0 LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t ntiles = (re - rb + BM - 1) / BM;
+    const int64_t per_xcd = gridDim.x >> 3;
+    const int64_t tile = static_cast<int64_t>(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;
+    const int64_t t0 = rb + tile * BM;
+    const int64_t row = t0 + 16 * wave + r;
+    const bool rv = row < re;
+    const int64_t rowc = rv ? row : re - 1;
+    const int lself = 16 * wave + r;
+
+    // [W_in | b_in] -> LDS (ordinary loads, before the DMAs)
+    float* const TB = reinterpret_cast<float*>(lds + OFF_TB);
+    if (tid < AH) {
+        f32x4 t;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) t[d] = d < D ? w_in[tid * D + d] : 0.f;
+        t[3] = b_in[tid];
+        *reinterpret_cast<f32x4*>(TB + 4 * tid) = t;
+    }
+    auto w_dma = [&](int c) {                  // W1's chunks, then W2's -> buffer c & 1
+        if (c >= 2 * AKP) return;
+        const unsigned char* src = c < AKP ? img1 + static_cast<size_t>(c) * ACHUNK
+                                           : img2 + static_cast<size_t>(c - AKP) * ACHUNK;
+        unsigned char* dst = lds + (c & 1) * ACHUNK;
+#pragma unroll
+        for (int pc = 0; pc < WPC; ++pc) {
+            const int piece = wave + pc * AW;
+            glds16_ag(src + piece * 1024 + lane * 16, lds_addr_ag(dst + piece * 1024));
+        }
+    };
+    w_dma(0);
+
+    // P_i (CSR order, then the self term) and c_i
+    float pi[3], P[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) pi[d] = d < D ? pos[rowc * ldp + d] : 0.f;
+    const int e0 = row_ptr[rowc];
+    const int deg = rv ? row_ptr[rowc + 1] - e0 : 0;
+    P[0] = P[1] = P[2] = 0.f;
+    for (int e = 0; e < deg; ++e) {
+        const int64_t j = col[e0 + e];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) P[d] += d < D ? pos[j * ldp + d] : 0.f;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) P[d] = fmaf(self_scale, pi[d], P[d]);
+    const float cnt = static_cast<float>(deg) + self_scale;
+
+    f32x4 acc[ACB];
+#pragma unroll
+    for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int p = 100;
+    const unsigned char* const wl0 = lds + lane * 16;
+    auto mfma3 = [&](const unsigned char* wb, const f16x8& bh, const f16x8& bl) {
+#pragma unroll
+        for (int cb = 0; cb < ACB; ++cb) {
+            const f16x8 wh = *reinterpret_cast<const f16x8*>(wb + (2 * cb) * AFRAG);
+            const f16x8 wl = *reinterpret_cast<const f16x8*>(wb + (2 * cb + 1) * AFRAG);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bl, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, bh, acc[cb], 0, 0, 0);
+        }
+    };
+    // ---- nn.0 over a = W_in P + c b_in, formed chunk by chunk in the B layout
+#pragma unroll 1
+    for (int kc = 0; kc < AKP; ++kc) {
+        vm_barrier<0>();                       // W1 chunk kc landed (and the table, kc = 0)
+        w_dma(kc + 1);
+        float a[8];
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const f32x4 t = *reinterpret_cast<const f32x4*>(TB + 4 * (32 * kc + 8 * g + j));
+            a[j] = fmaf(t[3], cnt, fmaf(t[2], P[2], fmaf(t[1], P[1], t[0] * P[0])));
+            m = max(m, __float_as_uint(fabsf(a[j])));
+        }
+        const int pc = sexp_ag(rowmax4(m));
+        if (pc < p) {
+#pragma unroll
+            for (int cb = 0; cb < ACB; ++cb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
+            p = pc;
+        }
+        const float spv = p2_ag(p);
+        f16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float v = a[j] * spv;
+            const _Float16 hh = static_cast<_Float16>(v);
+            bh[j] = hh;
+            bl[j] = static_cast<_Float16>(v - static_cast<float>(hh));
+        }
+        mfma3(wl0 + (kc & 1) * ACHUNK, bh, bl);
+    }
+    // ---- nn.2 over h = relu(acc 2^-(p + q1) + b1) from the accumulators (k-permuted W2)
+    {
+        const int32_t* const q1 = reinterpret_cast<const int32_t*>(img1 + FB);
+        uint32_t m = 0;
+#pragma unroll
+        for (int cb = 0; cb < ACB; ++cb) {
+            const int4 q = *reinterpret_cast<const int4*>(q1 + 16 * cb + 4 * g);
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(b1 + 16 * cb + 4 * g);
+            const int qn[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float h = ldexpf(acc[cb][i], -(p + qn[i])) + bb[i];
+                h = h < 0.f ? 0.f : h;
+                acc[cb][i] = h;
+                m = max(m, __float_as_uint(fabsf(h)));
+            }
+        }
+        p = sexp_ag(rowmax4(m));
+        const float spv = p2_ag(p);
+        f16x8 hh[AKP], hl[AKP];
+#pragma unroll
+        for (int kc = 0; kc < AKP; ++kc)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = acc[2 * kc + (j >> 2)][j & 3] * spv;
+                const _Float16 t = static_cast<_Float16>(v);
+                hh[kc][j] = t;
+                hl[kc][j] = static_cast<_Float16>(v - static_cast<float>(t));
+            }
+#pragma unroll
+        for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < AKP; ++kc) {
+            vm_barrier<0>();                   // W2 chunk kc landed
+            w_dma(AKP + kc + 1);
+            mfma3(wl0 + ((AKP + kc) & 1) * ACHUNK, hh[kc], hl[kc]);
+        }
+    }
+    // ---- epilogue (staged; the residual x_i = W_in pos_i + b_in recomputed)
+    vm_barrier<0>();
+    const bool hb = (flags & MIGNN_EPI_BIAS) != 0, ha = (flags & MIGNN_EPI_AFFINE) != 0;
+    float* const EV = reinterpret_cast<float*>(lds + OFF_EV);
+    if (tid < AH) {
+        reinterpret_cast<int32_t*>(EV)[tid] = reinterpret_cast<const int32_t*>(img2 + FB)[tid];
+        EV[AH + tid] = hb ? b2[tid] : 0.f;
+        EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
+        EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
+    }
+    staged_epilogue<ACB, true>(lds, EV, acc, p, flags, nullptr, 0, out, ldo, t0, re, wave, lane,
+                               lself, g, TB, pi[0], pi[1], pi[2]);
 }
 
 int g_fused_diag_flags = 0;   // mignn_diag_set_fused_flags (timing ablations; wrong results)
@@ -1570,3 +1762,31 @@ hipLaunchKernelGGL(tf_fused_kernel, dim3(static_cast<unsigned>(nb)), dim3(512), 
     return launch_status("tf_fused_kernel");
 }
 }  // namespace mignn
+
+extern "C" int mignn_gin_layer0_fused(const int32_t* row_ptr, const int32_t* col, const float* pos,
+                                      int64_t ldp, int d, int64_t rb, int64_t re, int h, float eps,
+                                      const float* w_in, const float* b_in, const void* img1,
+                                      const float* b1, const void* img2, const float* b2,
+                                      const float* scale, const float* shift, int flags,
+                                      float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gin_layer0_fused: unknown flags 0x%x", flags);
+    MIGNN_REQUIRE(row_ptr && col && pos && w_in && b_in && img1 && b1 && img2 && out,
+                  "gin_layer0_fused: null pointer");
+    MIGNN_REQUIRE(h == AH, "gin_layer0_fused: h must be 256 (got %d)", h);
+    MIGNN_REQUIRE(d >= 1 && d <= 3 && ldp >= d, "gin_layer0_fused: 1..3 coordinates per node");
+    MIGNN_REQUIRE(aligned16(out) && aligned16(img1) && aligned16(img2) && ldo % 4 == 0 && ldo >= h,
+                  "gin_layer0_fused: unaligned");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gin_layer0_fused: bad row range");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gin_layer0_fused: affine");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || b2, "gin_layer0_fused: bias");
+    if (re == rb) return MIGNN_OK;
+    constexpr int BM = 128;
+    const int64_t ntiles = (re - rb + BM - 1) / BM;
+    const int64_t nb = (ntiles + 7) / 8 * 8;
+    MIGNN_REQUIRE(nb < (int64_t(1) << 31), "gin_layer0_fused: too many rows");
+    hipLaunchKernelGGL(gin0_fused_kernel, dim3(static_cast<unsigned>(nb)), dim3(512), 0,
+                       as_stream(stream), row_ptr, col, pos, ldp, d, rb, re, 1.0f + eps, w_in, b_in,
+                       static_cast<const unsigned char*>(img1), b1,
+                       static_cast<const unsigned char*>(img2), b2, scale, shift, flags, out, ldo);
+    return launch_status("gin0_fused_kernel");
+}

@@ -441,6 +441,13 @@ class FlowGNN(nn.Module):
             except RuntimeError as e:
                 raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
             first = 1
+        elif self._fuse_gin_layer0():
+            # input_proj + GIN layer 0 at H = 256 from the coordinates (mignn_gin_layer0_fused)
+            try:
+                self._gin_layer0(xin, csr, cur)
+            except RuntimeError as e:
+                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
+            first = 1
         else:
             # input_proj (gnn_model.py:159), gathered into the CSR's node order
             self._input_proj(xin, cur, rows=csr.perm)
@@ -593,6 +600,29 @@ class FlowGNN(nn.Module):
         return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GCN"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 4
                 and self.hidden_dim in (4, 8, 16, 32, 64, 128, 256))
+
+    def _fuse_gin_layer0(self) -> bool:
+        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GIN"
+                and self.num_layers > 0 and 1 <= self.input_dim <= 3 and self.hidden_dim == 256
+                and self._fused256())
+
+    def _gin_layer0(self, x, csr: Csr, out):
+        """input_proj + GIN layer 0 + residual + BN + ReLU in one kernel:
+        a_i = W_in (sum_j pos_j + (1+eps) pos_i) + (deg_i + 1 + eps) b_in."""
+        layer = self.gnn_layers[0]
+        nn0, nn2 = layer.nn[0], layer.nn[2]
+        eps = self._cached("eps", 0, (layer.eps,), lambda: float(layer.eps.reshape(-1)[0]))
+        img1 = self._cached("w_gin0", 0, (nn0.weight,), lambda: f16x3_image(nn0.weight))
+        img2 = self._cached("w_gin2p", 0, (nn2.weight,), lambda: gin_fused_image(nn2.weight))
+        scale, shift = self._bn(0)
+        epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
+        pos = self._coords(x, csr)
+        P = _lib.ptr
+        _lib.check(_lib.lib().mignn_gin_layer0_fused(
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), self.input_dim, 0, x.shape[0],
+            256, eps, P(self.input_proj.weight), P(self.input_proj.bias), P(img1), P(nn0.bias),
+            P(img2), P(nn2.bias), P(scale), P(shift), epi, P(out), out.stride(0), _stream(x)),
+            "mignn_gin_layer0_fused")
 
     def _layer0_coef(self):
         """A = diag(sc) W_in, B = diag(sc) W W_in, d = sc*(W b_in), e = sc*(b_in + b) + sh

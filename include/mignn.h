@@ -331,6 +331,18 @@ int mignn_gin_layer_fused(const int32_t* row_ptr, const int32_t* col, const floa
                           const void* img1, const float* b1, const void* img2, const float* b2,
                           const float* scale, const float* shift, int flags, float* out,
                           int64_t ldo, void* stream);
+/* GIN layer 0 at h = 256 from the node coordinates (input_proj composed
+ * into the aggregate: a_i = W_in (sum_j pos_j + (1+eps) pos_i) + (deg_i + 1 +
+ * eps) b_in; the residual x_i = W_in pos_i + b_in recomputed in the
+ * epilogue): input_proj's [N, 256] output is never written and the layer
+ * gathers 12 B per CSR entry instead of a 1-KB row.  pos [N, d] (d <= 3,
+ * stride ldp) in the CSR's node order; w_in [256, d], b_in [256] =
+ * input_proj; the rest as mignn_gin_layer_fused. */
+int mignn_gin_layer0_fused(const int32_t* row_ptr, const int32_t* col, const float* pos,
+                           int64_t ldp, int d, int64_t row_begin, int64_t row_end, int h, float eps,
+                           const float* w_in, const float* b_in, const void* img1, const float* b1,
+                           const void* img2, const float* b2, const float* scale,
+                           const float* shift, int flags, float* out, int64_t ldo, void* stream);
 int mignn_gcn_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* ew,
                           const float* x, int64_t ldx, int64_t row_begin, int64_t row_end, int h,
                           const void* img, const float* bias, const float* scale,

@@ -341,3 +341,50 @@ def test_transformer_fused_prep_rejects():
     w = torch.zeros(H, 4 * H + 4 + H, device=DEV)
     assert L.mignn_transformer_fused_prep(_lib.ptr(w), 128, 4, _lib.ptr(img), 16, None) == 1
     assert L.mignn_transformer_fused_prep(_lib.ptr(w), 256, 4, _lib.ptr(img), 16, None) == 1
+
+
+@pytest.mark.parametrize("flags", [15, 1 | 2])
+def test_gin_layer0_fused_vs_fp64_and_two_step(flags):
+    """mignn_gin_layer0_fused (input_proj composed into GIN layer 0's
+    aggregate: a_i = W_in (sum_j pos_j + (1+eps) pos_i) + (deg_i+1+eps) b_in,
+    residual recomputed from pos_i) against a float64 restatement of
+    input_proj -> GINConv -> epilogue, and against the two-step route it
+    replaces (input_proj, then mignn_gin_layer_fused); hub rows, empty rows,
+    a row range."""
+    n = 3000
+    rb, re = 77, 2950
+    ei = _graph(n, 51)
+    csr = build_csr(ei, n, _lib.CSR_VERBATIM)
+    g = torch.Generator(device=DEV).manual_seed(flags + 3)
+    pos = torch.rand(n, 3, device=DEV, generator=g) * 10
+    w_in = torch.randn(H, 3, device=DEV, generator=g) / 3 ** 0.5
+    b_in = torch.randn(H, device=DEV, generator=g) * 0.1
+    _, w1, w2, b1, b2, sc, sh = _params(9, scaled_rows=False)
+    eps = 0.2
+    L = _lib.lib()
+    P = _lib.ptr
+    img1, img2 = f16x3_image(w1), gin_fused_image(w2)
+    got = torch.full((n, H), float("nan"), device=DEV)
+    _lib.check(L.mignn_gin_layer0_fused(P(csr.row_ptr), P(csr.col), P(pos), 3, 3, rb, re, H, eps,
+                                        P(w_in), P(b_in), P(img1), P(b1), P(img2), P(b2), P(sc),
+                                        P(sh), flags, P(got), H, _lib.stream()), "gin0_fused")
+    x0 = (pos @ w_in.T + b_in).contiguous()
+    two = torch.full((n, H), float("nan"), device=DEV)
+    _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(x0), H, rb, re, H, eps,
+                                       P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), flags, P(two),
+                                       H, _lib.stream()), "gin_fused")
+    torch.cuda.synchronize()
+    col, dst = _csr_edges(csr, n)
+    X = pos.double().cpu() @ w_in.double().cpu().T + b_in.double().cpu()
+    a = torch.zeros(n, H, dtype=torch.float64).index_add_(0, dst, X[col]) + (1 + eps) * X
+    am = torch.zeros(n, H, dtype=torch.float64).index_add_(0, dst, X[col].abs()) + (1 + eps) * X.abs()
+    W1, W2 = w1.double().cpu(), w2.double().cpu()
+    h = (a @ W1.T + b1.double().cpu()).clamp_min(0)
+    hm = am @ W1.T.abs() + b1.double().cpu().abs()
+    ref, mag = _epi64(h @ W2.T, hm @ W2.T.abs(), X, b2.cpu(), sc.cpu(), sh.cpu(), flags)
+    g_cpu, t_cpu = got.cpu(), two.cpu()
+    _check(g_cpu[rb:re], ref[rb:re], mag[rb:re], f"gin0 flags={flags}")
+    _check(t_cpu[rb:re], ref[rb:re], mag[rb:re], f"gin two-step flags={flags}")
+    assert torch.isnan(g_cpu[:rb]).all() and torch.isnan(g_cpu[re:]).all()
+    d = (g_cpu[rb:re] - t_cpu[rb:re]).abs().max().item()
+    assert d <= 4e-6 * max(1.0, ref[rb:re].abs().max().item()), d
