@@ -991,17 +991,29 @@ struct GatCfg {
     static constexpr int OFF_AL = 2 * STEPW;           // alphas [AW][16][4][8]
     static constexpr int OFF_ST = OFF_AL + AW * 16 * 4 * 8 * 4;   // (max, sum) [AW][16][4]
     static constexpr int OFF_EPI = OFF_ST + AW * 16 * 4 * 8;       // QF | BF | SC | SH [H]
-    static constexpr int LDS_BYTES = OFF_EPI + 4 * H * 4;
+    static constexpr int OFF_TB = OFF_EPI + 4 * H * 4;  // (layer 0) [W_in | b_in] [H][4]
+    static constexpr int LDS_BYTES = OFF_TB + H * 16;
     static_assert(LDS_BYTES <= 160 * 1024, "gat_fused LDS");
 };
 
-template <int H>
+// L0 (layer 0 from the coordinates, x = pos W_in^T + b_in never formed): the
+// logits come from pos through the composed [wlog W_in | wlog b_in] (lw [8][4]),
+// every lane forms its row's 4 heads' P = sum_j alpha_j pos_j and S = sum_j
+// alpha_j in registers, and every chunk's weighted sums are W_in[c] . P +
+// S b_in[c] -- no row gathers; the residual is recomputed from pos_i in the
+// epilogue.  (A first form had lane g compute head g only and pass P, S to
+// the row's other lanes through LDS: it gave wrong rows in waves 4-7 of some
+// tiles, run to run, with or without extra barriers; the register form is
+// exact and deterministic.)
+template <int H, bool L0 = false>
 __global__ __launch_bounds__(GatCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void
 gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                  const float* __restrict__ logits, const float* __restrict__ x, int64_t ldx,
                  int64_t rb, int64_t re, float slope, const unsigned char* __restrict__ img,
                  const float* __restrict__ bias, const float* __restrict__ scale,
-                 const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+                 const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo,
+                 const float* __restrict__ w_in = nullptr, const float* __restrict__ b_in = nullptr,
+                 const float* __restrict__ lw = nullptr, int D = 0) {
     using C = GatCfg<H>;
     constexpr int HEADS = 4;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
@@ -1044,6 +1056,16 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         SC[tid] = (flags & MIGNN_EPI_AFFINE) ? scale[tid] : 1.f;
         SH[tid] = (flags & MIGNN_EPI_AFFINE) ? shift[tid] : 0.f;
     }
+    float* const TB = reinterpret_cast<float*>(lds + C::OFF_TB);
+    if constexpr (L0) {
+        if (tid < H) {
+            f32x4 t;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) t[d] = d < D ? w_in[tid * D + d] : 0.f;
+            t[3] = b_in[tid];
+            *reinterpret_cast<f32x4*>(TB + 4 * tid) = t;
+        }
+    }
 
     // ---- CSR slots, scores of head g, softmax statistics, alphas
     const int e0 = row_ptr[rowc];
@@ -1053,28 +1075,97 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     for (int e = 0; e < AS; ++e) cj[e] = e < deg ? col[e0 + e] : -1;
     const bool extra = __builtin_amdgcn_ballot_w64(deg > AS) != 0ull;
     auto leaky = [&](float v) { return v > 0.f ? v : v * slope; };
-    const float ad = logits[rowc * (2 * HEADS) + HEADS + g];
+    float* const AL = reinterpret_cast<float*>(lds + C::OFF_AL) + ((wave * 16 + r) * 4) * 8;
+    float pi[3] = {0.f, 0.f, 0.f};
+    f32x4 PSK[HEADS];                          // (L0) per head: P = sum alpha pos_j | S = sum alpha
+    if constexpr (L0) {
+        // logits from the coordinates; every lane forms all 4 heads' P and S
+#pragma unroll
+        for (int d = 0; d < 3; ++d) pi[d] = d < D ? x[rowc * ldx + d] : 0.f;
+        auto posj = [&](int j, float (&pj)[3]) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) pj[d] = d < D ? x[static_cast<int64_t>(j) * ldx + d] : 0.f;
+        };
+        float pj[AS][3];
+#pragma unroll
+        for (int e = 0; e < AS; ++e) posj(cj[e] >= 0 ? cj[e] : 0, pj[e]);
+#pragma unroll
+        for (int k = 0; k < HEADS; ++k) {
+            const f32x4 ls = *reinterpret_cast<const f32x4*>(lw + 4 * k);
+            const f32x4 ld = *reinterpret_cast<const f32x4*>(lw + 4 * (HEADS + k));
+            const float ad0 = fmaf(ld[2], pi[2], fmaf(ld[1], pi[1], fmaf(ld[0], pi[0], ld[3])));
+            auto score = [&](const float (&q)[3]) {
+                return leaky(fmaf(ls[2], q[2], fmaf(ls[1], q[1], fmaf(ls[0], q[0], ls[3]))) + ad0);
+            };
+            float sc0[AS];
+            float mx0 = -INFINITY;
+#pragma unroll
+            for (int e = 0; e < AS; ++e) {
+                sc0[e] = cj[e] >= 0 ? score(pj[e]) : -INFINITY;
+                mx0 = fmaxf(mx0, sc0[e]);
+            }
+            if (extra)
+                for (int e = AS; e < deg; ++e) {
+                    float q[3];
+                    posj(col[e0 + e], q);
+                    mx0 = fmaxf(mx0, score(q));
+                }
+            float sm0 = 0.f;
+#pragma unroll
+            for (int e = 0; e < AS; ++e)
+                if (cj[e] >= 0) sm0 += expf(sc0[e] - mx0);
+            if (extra)
+                for (int e = AS; e < deg; ++e) {
+                    float q[3];
+                    posj(col[e0 + e], q);
+                    sm0 += expf(score(q) - mx0);
+                }
+            sm0 += 1e-16f;
+            f32x4 PS = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < AS; ++e) {
+                if (cj[e] < 0) continue;
+                const float a = expf(sc0[e] - mx0) / sm0;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) PS[d] = fmaf(a, pj[e][d], PS[d]);
+                PS[3] += a;
+            }
+            if (extra)
+                for (int e = AS; e < deg; ++e) {
+                    float q[3];
+                    posj(col[e0 + e], q);
+                    const float a = expf(score(q) - mx0) / sm0;
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) PS[d] = fmaf(a, q[d], PS[d]);
+                    PS[3] += a;
+                }
+            PSK[k] = PS;
+        }
+    }
+    const float ad = L0 ? 0.f : logits[rowc * (2 * HEADS) + HEADS + g];
     float sc[AS];
     float mx = -INFINITY;
 #pragma unroll
     for (int e = 0; e < AS; ++e) {
+        if constexpr (L0) break;
         sc[e] = cj[e] >= 0 ? leaky(logits[static_cast<int64_t>(cj[e]) * (2 * HEADS) + g] + ad) : -INFINITY;
         mx = fmaxf(mx, sc[e]);
     }
-    if (extra)
+    if (extra && !L0)
         for (int e = AS; e < deg; ++e)
             mx = fmaxf(mx, leaky(logits[static_cast<int64_t>(col[e0 + e]) * (2 * HEADS) + g] + ad));
     float sm = 0.f;
 #pragma unroll
-    for (int e = 0; e < AS; ++e)
+    for (int e = 0; e < AS; ++e) {
+        if constexpr (L0) break;
         if (cj[e] >= 0) sm += expf(sc[e] - mx);
-    if (extra)
+    }
+    if (extra && !L0)
         for (int e = AS; e < deg; ++e)
             sm += expf(leaky(logits[static_cast<int64_t>(col[e0 + e]) * (2 * HEADS) + g] + ad) - mx);
     sm += 1e-16f;
-    float* const AL = reinterpret_cast<float*>(lds + C::OFF_AL) + ((wave * 16 + r) * 4) * 8;
     float* const ST = reinterpret_cast<float*>(lds + C::OFF_ST) + ((wave * 16 + r) * 4) * 2;
-    {
+    if constexpr (!L0) {
         f32x4 a0, a1;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1090,6 +1181,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     // (row addresses recomputed per chunk from the 32-bit columns: 64-bit
     // pointers held across the loop cost 16 registers)
     auto gather = [&](int t) {
+        if constexpr (L0) return;
 #pragma unroll
         for (int e = 0; e < AS; ++e) {
             const float* sp = cj[e] >= 0 ? x + static_cast<int64_t>(cj[e]) * ldx + 8 * g + 32 * t
@@ -1115,6 +1207,16 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         for (int k = 0; k < HEADS; ++k) {
             a[k][0] = f32x4{0.f, 0.f, 0.f, 0.f};
             a[k][1] = a[k][0];
+            if constexpr (L0) {                // W_in[c] . P_k + S_k b_in[c]
+                const f32x4 PS = PSK[k];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const f32x4 tb = *reinterpret_cast<const f32x4*>(TB + 4 * (32 * t + 8 * g + j));
+                    a[k][j >> 2][j & 3] =
+                        fmaf(tb[3], PS[3], fmaf(tb[2], PS[2], fmaf(tb[1], PS[1], tb[0] * PS[0])));
+                }
+                continue;
+            }
             // the row's alphas of head k (LDS, written by this wave: in order)
             const f32x4 w0 = *reinterpret_cast<const f32x4*>(AL + k * 8);
             const f32x4 w1 = *reinterpret_cast<const f32x4*>(AL + k * 8 + 4);
@@ -1128,7 +1230,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
                 }
             }
         }
-        if (extra) {
+        if (extra && !L0) {
             // entries past the register slots: alphas from the saved statistics
             for (int e = AS; e < deg; ++e) {
                 const int j = col[e0 + e];
@@ -1205,8 +1307,8 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         EV2[2 * H + tid] = SC[tid];
         EV2[3 * H + tid] = SH[tid];
     }
-    staged_epilogue<C::NCB>(lds, EV2, acc, p, flags, x, ldx, out, ldo, rb + tile * C::BM, re, wave,
-                            lane, 16 * wave + r, g);
+    staged_epilogue<C::NCB, L0>(lds, EV2, acc, p, flags, x, ldx, out, ldo, rb + tile * C::BM, re,
+                                wave, lane, 16 * wave + r, g, TB, pi[0], pi[1], pi[2]);
 }
 
 // ------------------------------------------------------------------ TransformerConv
@@ -1591,18 +1693,21 @@ int launch_agg_gemm(const int32_t* row_ptr, const int32_t* col, const float* ew,
 }
 
 
-template <int H>
+template <int H, bool L0 = false>
 int launch_gat_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
                      const float* x, int64_t ldx, int64_t rb, int64_t re, float slope,
                      const void* img, const float* bias, const float* scale, const float* shift,
-                     int flags, float* out, int64_t ldo, hipStream_t st) {
+                     int flags, float* out, int64_t ldo, hipStream_t st,
+                     const float* w_in = nullptr, const float* b_in = nullptr,
+                     const float* lw = nullptr, int d = 0) {
     using C = GatCfg<H>;
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     const int64_t nb = (ntiles + 7) / 8 * 8;
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "gat_fused: too many rows");
-    hipLaunchKernelGGL((gat_fused_kernel<H>), dim3(static_cast<unsigned>(nb)), dim3(C::NT), 0, st,
-                       row_ptr, col, logits, x, ldx, rb, re, slope,
-                       static_cast<const unsigned char*>(img), bias, scale, shift, flags, out, ldo);
+    hipLaunchKernelGGL((gat_fused_kernel<H, L0>), dim3(static_cast<unsigned>(nb)), dim3(C::NT), 0,
+                       st, row_ptr, col, logits, x, ldx, rb, re, slope,
+                       static_cast<const unsigned char*>(img), bias, scale, shift, flags, out, ldo,
+                       w_in, b_in, lw, d);
     return launch_status("gat_fused_kernel");
 }
 
@@ -1789,4 +1894,31 @@ extern "C" int mignn_gin_layer0_fused(const int32_t* row_ptr, const int32_t* col
                        static_cast<const unsigned char*>(img1), b1,
                        static_cast<const unsigned char*>(img2), b2, scale, shift, flags, out, ldo);
     return launch_status("gin0_fused_kernel");
+}
+
+extern "C" int mignn_gat_layer0_fused(const int32_t* row_ptr, const int32_t* col, const float* pos,
+                                      int64_t ldp, int d, int64_t rb, int64_t re, int h,
+                                      float negative_slope, const float* w_in, const float* b_in,
+                                      const float* lw, const void* wcat_img, const float* bias,
+                                      const float* scale, const float* shift, int flags,
+                                      float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gat_layer0_fused: unknown flags 0x%x", flags);
+    MIGNN_REQUIRE(row_ptr && col && pos && w_in && b_in && lw && wcat_img && out,
+                  "gat_layer0_fused: null pointer");
+    MIGNN_REQUIRE(h == 64 || h == 128, "gat_layer0_fused: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(d >= 1 && d <= 3 && ldp >= d, "gat_layer0_fused: 1..3 coordinates per node");
+    MIGNN_REQUIRE(aligned16(out) && aligned16(wcat_img) && aligned16(lw) && ldo % 4 == 0 && ldo >= h,
+                  "gat_layer0_fused: unaligned");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gat_layer0_fused: bad row range");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gat_layer0_fused: affine");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bias, "gat_layer0_fused: bias");
+    if (re == rb) return MIGNN_OK;
+    hipStream_t st = as_stream(stream);
+    flags |= g_fused_diag_flags;
+    return h == 128 ? launch_gat_fused<128, true>(row_ptr, col, nullptr, pos, ldp, rb, re,
+                                                  negative_slope, wcat_img, bias, scale, shift,
+                                                  flags, out, ldo, st, w_in, b_in, lw, d)
+                    : launch_gat_fused<64, true>(row_ptr, col, nullptr, pos, ldp, rb, re,
+                                                 negative_slope, wcat_img, bias, scale, shift,
+                                                 flags, out, ldo, st, w_in, b_in, lw, d);
 }

@@ -441,6 +441,13 @@ class FlowGNN(nn.Module):
             except RuntimeError as e:
                 raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
             first = 1
+        elif self._fuse_gat_layer0():
+            # input_proj + GAT layer 0 from the coordinates (mignn_gat_layer0_fused)
+            try:
+                self._gat_layer0(xin, csr, cur)
+            except RuntimeError as e:
+                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
+            first = 1
         elif self._fuse_gin_layer0():
             # input_proj + GIN layer 0 at H = 256 from the coordinates (mignn_gin_layer0_fused)
             try:
@@ -600,6 +607,44 @@ class FlowGNN(nn.Module):
         return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GCN"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 4
                 and self.hidden_dim in (4, 8, 16, 32, 64, 128, 256))
+
+    def _fuse_gat_layer0(self) -> bool:
+        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GAT"
+                and self.num_layers > 0 and 1 <= self.input_dim <= 3
+                and self.hidden_dim in (64, 128) and self.precision == "f16x3")
+
+    def _gat_layer0(self, x, csr: Csr, out):
+        """input_proj + GAT layer 0 + residual + BN + ReLU in one kernel: logits
+        through [wlog W_in | wlog b_in], per head P = sum alpha pos_j and S =
+        sum alpha, weighted sums W_in P + S b_in (fp64-composed weights)."""
+        layer = self.gnn_layers[0]
+        H, D = self.hidden_dim, self.input_dim
+        ts = (layer.lin.weight, layer.att_src, layer.att_dst, self.input_proj.weight,
+              self.input_proj.bias)
+
+        def make():
+            heads, C = layer.heads, layer.out_channels
+            W = layer.lin.weight.detach().double().view(heads, C, -1)
+            vs = torch.einsum("hck,hc->hk", W, layer.att_src.detach().double().view(heads, C))
+            vd = torch.einsum("hck,hc->hk", W, layer.att_dst.detach().double().view(heads, C))
+            wlog = torch.cat([vs, vd], 0)                                   # [8, H]
+            lw = torch.zeros(2 * heads, 4, dtype=torch.float64, device=W.device)
+            lw[:, :D] = wlog @ self.input_proj.weight.detach().double()
+            lw[:, 3] = wlog @ self.input_proj.bias.detach().double()
+            return lw.float().contiguous()
+        lw = self._cached("gat0", 0, ts, make)
+        _, wcat = self._cached("gat", 0, (layer.lin.weight, layer.att_src, layer.att_dst),
+                               lambda: self._gat_weights(layer))
+        img = self._img("w_gat", 0, (layer.lin.weight,), wcat)
+        scale, shift = self._bn(0)
+        epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
+        pos = self._coords(x, csr)
+        P = _lib.ptr
+        _lib.check(_lib.lib().mignn_gat_layer0_fused(
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, 0, x.shape[0], H,
+            float(layer.negative_slope), P(self.input_proj.weight), P(self.input_proj.bias), P(lw),
+            P(img), P(layer.bias), P(scale), P(shift), epi, P(out), out.stride(0), _stream(x)),
+            "mignn_gat_layer0_fused")
 
     def _fuse_gin_layer0(self) -> bool:
         return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GIN"

@@ -331,6 +331,20 @@ int mignn_gin_layer_fused(const int32_t* row_ptr, const int32_t* col, const floa
                           const void* img1, const float* b1, const void* img2, const float* b2,
                           const float* scale, const float* shift, int flags, float* out,
                           int64_t ldo, void* stream);
+/* GAT layer 0 (4 heads, h in {64, 128}) from the node coordinates
+ * (input_proj composed in: with x = pos W_in^T + b_in, the logits are
+ * pos . lw[:, :3] + lw[:, 3] for lw = [wlog W_in | wlog b_in] ([8][4], rows
+ * as mignn_gat_layer's wlog), head k's weighted sum is W_in P_k + S_k b_in
+ * with P_k = sum_j alpha_jk pos_j and S_k = sum_j alpha_jk, and the residual
+ * x_i is recomputed): neither input_proj's [N, h] output nor the logits are
+ * written, and no feature row is gathered.  pos [N, d] (d <= 3, stride ldp)
+ * in the CSR's node order; wcat_img as mignn_gat_layer. */
+int mignn_gat_layer0_fused(const int32_t* row_ptr, const int32_t* col, const float* pos,
+                           int64_t ldp, int d, int64_t row_begin, int64_t row_end, int h,
+                           float negative_slope, const float* w_in, const float* b_in,
+                           const float* lw, const void* wcat_img, const float* bias,
+                           const float* scale, const float* shift, int flags, float* out,
+                           int64_t ldo, void* stream);
 /* GIN layer 0 at h = 256 from the node coordinates (input_proj composed
  * into the aggregate: a_i = W_in (sum_j pos_j + (1+eps) pos_i) + (deg_i + 1 +
  * eps) b_in; the residual x_i = W_in pos_i + b_in recomputed in the

@@ -388,3 +388,61 @@ def test_gin_layer0_fused_vs_fp64_and_two_step(flags):
     assert torch.isnan(g_cpu[:rb]).all() and torch.isnan(g_cpu[re:]).all()
     d = (g_cpu[rb:re] - t_cpu[rb:re]).abs().max().item()
     assert d <= 4e-6 * max(1.0, ref[rb:re].abs().max().item()), d
+
+
+@pytest.mark.parametrize("h", [64, 128])
+@pytest.mark.parametrize("flags", [15, 1 | 2])
+def test_gat_layer0_fused_vs_fp64_and_two_step(h, flags):
+    """mignn_gat_layer0_fused (input_proj composed into GAT layer 0: logits
+    through [wlog W_in | wlog b_in], weighted sums W_in P + S b_in, residual
+    recomputed) against a float64 restatement of input_proj -> GATConv ->
+    epilogue and against the two-step route (input_proj, then
+    mignn_gat_layer's fused kernel); hub rows, empty rows, a row range."""
+    n = 4000
+    rb, re = 29, 3981
+    ei = _graph(n, 61)
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
+    g = torch.Generator(device=DEV).manual_seed(h + flags + 5)
+    pos = torch.rand(n, 3, device=DEV, generator=g) * 4
+    w_in = torch.randn(h, 3, device=DEV, generator=g) / 3 ** 0.5
+    b_in = torch.randn(h, device=DEV, generator=g) * 0.1
+    wlog = torch.randn(8, h, device=DEV, generator=g) / h ** 0.5
+    wcat = torch.randn(h, 4 * h, device=DEV, generator=g) / (2 * h) ** 0.5
+    bias = torch.randn(h, device=DEV, generator=g) * 0.1
+    sc = torch.rand(h, device=DEV, generator=g) + 0.5
+    sh = torch.randn(h, device=DEV, generator=g) * 0.1
+    img = f16x3_image(wcat)
+    lw = torch.zeros(8, 4, dtype=torch.float64, device=DEV)
+    lw[:, :3] = wlog.double() @ w_in.double()
+    lw[:, 3] = wlog.double() @ b_in.double()
+    lw = lw.float().contiguous()
+    L = _lib.lib()
+    P = _lib.ptr
+    got = torch.full((n, h), float("nan"), device=DEV)
+    _lib.check(L.mignn_gat_layer0_fused(P(csr.row_ptr), P(csr.col), P(pos), 3, 3, rb, re, h, 0.2,
+                                        P(w_in), P(b_in), P(lw), P(img), P(bias), P(sc), P(sh),
+                                        flags, P(got), h, _lib.stream()), "gat0_fused")
+    x0 = (pos @ w_in.T + b_in).contiguous()
+    two = torch.full((n, h), float("nan"), device=DEV)
+    _gat_layer(csr, x0, n, rb, re, h, wlog, wcat, img, bias, sc, sh, flags, two)
+    torch.cuda.synchronize()
+    col, dst = _csr_edges(csr, n)
+    X = pos.double().cpu() @ w_in.double().cpu().T + b_in.double().cpu()
+    lg = X @ wlog.double().cpu().T
+    s = lg[col, :4] + lg[dst, 4:]
+    s = torch.where(s > 0, s, 0.2 * s)
+    mx = torch.full((n, 4), -float("inf"), dtype=torch.float64).scatter_reduce(
+        0, dst[:, None].expand_as(s), s, "amax", include_self=True)
+    pexp = torch.exp(s - mx[dst])
+    sm = torch.zeros((n, 4), dtype=torch.float64).index_add_(0, dst, pexp) + 1e-16
+    alpha = pexp / sm[dst]
+    agg = torch.zeros((n, 4, h), dtype=torch.float64).index_add_(
+        0, dst, alpha[:, :, None] * X[col][:, None, :]).reshape(n, 4 * h)
+    aggm = torch.zeros((n, 4, h), dtype=torch.float64).index_add_(
+        0, dst, alpha[:, :, None] * X[col].abs()[:, None, :]).reshape(n, 4 * h)
+    W = wcat.double().cpu()
+    ref, mag = _epi64(agg @ W.T, aggm @ W.T.abs(), X, bias.cpu(), sc.cpu(), sh.cpu(), flags)
+    g_cpu, t_cpu = got.cpu(), two.cpu()
+    _check(g_cpu[rb:re], ref[rb:re], mag[rb:re], f"gat0 h={h}")
+    _check(t_cpu[rb:re], ref[rb:re], mag[rb:re], f"gat two-step h={h}")
+    assert torch.isnan(g_cpu[:rb]).all() and torch.isnan(g_cpu[re:]).all()
