@@ -692,6 +692,127 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
                                lself, g, TB, pi[0], pi[1], pi[2]);
 }
 
+// TransformerConv layer 0 from the coordinates (heads = 4, any H = 64 CPL):
+// with x = pos W_in^T + b_in the whole layer collapses to 3-vectors.  The
+// score's row term cancels in the softmax, so
+//   s_ij^h = (G_h pos_i + g_h) . pos_j / sqrt(C)      (G_h = W_in^T M_h W_in, 3x3)
+//   P_h = sum_j a_ij^h pos_j,  S_h = sum_j a_ij^h      (softmax + 1e-16)
+//   out_i = relu( sum_h (A_h P_h + S_h e_h) + B pos_i + d )
+// where A_h = Wv_h/heads W_in, e_h = Wv_h/heads b_in + bv_h/heads, B = W_skip
+// W_in and d = W_skip b_in + b_skip, with the residual (+ W_in pos_i + b_in)
+// and the BN affine folded in (host, fp64): 20 numbers per output column
+// (T [H][20]), 12 per head (GT [4][12] = G_h | g_h).  No [N, H] input, no
+// Q~K transform, no gathered feature row: ~26 FMAs per output value.
+// Block: 4 waves; a wave takes 64 rows at a time -- lane l forms row l's
+// P, S (online softmax over its CSR entries) into LDS, then the wave writes
+// the 64 rows one by one, lane l owning columns CPL l .. CPL l + CPL - 1
+// (table in registers).
+template <int CPL>
+__global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ row_ptr,
+                                                  const int32_t* __restrict__ col,
+                                                  const float* __restrict__ pos, int64_t ldp,
+                                                  int D, int64_t rb, int64_t re, float score_scale,
+                                                  const float* __restrict__ T,
+                                                  const float* __restrict__ GT, int relu,
+                                                  float* __restrict__ out, int64_t ldo) {
+    constexpr int HEADS = 4, NW = 4, SL = 20;
+    __shared__ __attribute__((aligned(16))) float slot[NW][64][SL];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    float tb[CPL][SL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+#pragma unroll
+        for (int i = 0; i < SL; ++i) tb[k][i] = T[(lane * CPL + k) * SL + i];
+    const int64_t nb = (re - rb + 63) / 64;
+    const int64_t groups = (nb + NW - 1) / NW;
+    for (int64_t b = static_cast<int64_t>(blockIdx.x); b < groups; b += gridDim.x) {
+        // (b indexes groups of NW batches: every wave of the block runs the
+        // same number of iterations -- the __syncthreads below are uniform)
+        const int64_t batch = b * NW + wave;
+        const int64_t row = rb + batch * 64 + lane;
+        // ---- lane = row: P_h, S_h
+        if (row < re) {
+            float pi[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) pi[d] = d < D ? pos[row * ldp + d] : 0.f;
+            float u[HEADS][3];
+#pragma unroll
+            for (int h = 0; h < HEADS; ++h)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const float* gr = GT + h * 12 + 3 * a;
+                    u[h][a] = (fmaf(gr[2], pi[2], fmaf(gr[1], pi[1], fmaf(gr[0], pi[0], GT[h * 12 + 9 + a])))) * score_scale;
+                }
+            float m[HEADS], l[HEADS], P[HEADS][3];
+#pragma unroll
+            for (int h = 0; h < HEADS; ++h) {
+                m[h] = -INFINITY;
+                l[h] = 0.f;
+                P[h][0] = P[h][1] = P[h][2] = 0.f;
+            }
+            const int e0 = row_ptr[row], e1 = row_ptr[row + 1];
+            // (scores and sums on pos_j - pos_i: the softmax is shift-invariant and
+            // the neighbour offsets are small, so neither loses precision to the
+            // coordinates' magnitude; P_h = sum a (pos_j - pos_i) + S_h pos_i)
+            for (int e = e0; e < e1; ++e) {
+                const int64_t j = col[e];
+                float pj[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) pj[d] = d < D ? pos[j * ldp + d] - pi[d] : 0.f;
+#pragma unroll
+                for (int h = 0; h < HEADS; ++h) {
+                    const float sc = fmaf(u[h][2], pj[2], fmaf(u[h][1], pj[1], u[h][0] * pj[0]));
+                    const float mn = fmaxf(m[h], sc);
+                    const float corr = m[h] == -INFINITY ? 0.f : expf(m[h] - mn);
+                    const float w = expf(sc - mn);
+                    l[h] = fmaf(l[h], corr, w);
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) P[h][d] = fmaf(P[h][d], corr, w * pj[d]);
+                    m[h] = mn;
+                }
+            }
+            float* const sl = slot[wave][lane];
+#pragma unroll
+            for (int h = 0; h < HEADS; ++h) {
+                const float inv = 1.f / (l[h] + 1e-16f);
+                const float S = l[h] * inv;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) sl[3 * h + d] = fmaf(S, pi[d], P[h][d] * inv);
+                sl[12 + h] = S;
+            }
+#pragma unroll
+            for (int d = 0; d < 3; ++d) sl[16 + d] = pi[d];
+        }
+        __syncthreads();
+        // ---- the wave's 64 rows, lane = CPL columns
+        const int64_t rows = re - (rb + batch * 64) < 64 ? re - (rb + batch * 64) : 64;
+        for (int rr = 0; rr < rows; ++rr) {
+            const float* const sl = slot[wave][rr];
+            float v[SL - 1];
+#pragma unroll
+            for (int i = 0; i < SL - 1; ++i) v[i] = sl[i];
+            float o[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                float acc = tb[k][19];
+#pragma unroll
+                for (int i = 0; i < 19; ++i) acc = fmaf(tb[k][i], v[i], acc);
+                o[k] = relu ? fmaxf(acc, 0.f) : acc;
+            }
+            float* const dst = out + (rb + batch * 64 + rr) * ldo + lane * CPL;
+            if constexpr (CPL == 4) {
+                __builtin_nontemporal_store(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(dst));
+            } else {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) dst[k] = o[k];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 int g_fused_diag_flags = 0;   // mignn_diag_set_fused_flags (timing ablations; wrong results)
 
 // k-permuted split image of W2 [256, 256] for the chained transform: element
@@ -1921,4 +2042,30 @@ extern "C" int mignn_gat_layer0_fused(const int32_t* row_ptr, const int32_t* col
                     : launch_gat_fused<64, true>(row_ptr, col, nullptr, pos, ldp, rb, re,
                                                  negative_slope, wcat_img, bias, scale, shift,
                                                  flags, out, ldo, st, w_in, b_in, lw, d);
+}
+
+extern "C" int mignn_transformer_layer0_coords(const int32_t* row_ptr, const int32_t* col,
+                                               const float* pos, int64_t ldp, int d,
+                                               int64_t rb, int64_t re, int h, int heads,
+                                               float score_scale, const float* table,
+                                               const float* gt, int relu, float* out,
+                                               int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(row_ptr && col && pos && table && gt && out, "transformer_layer0_coords: null pointer");
+    MIGNN_REQUIRE(heads == 4 && (h == 64 || h == 128 || h == 256),
+                  "transformer_layer0_coords: heads = 4, h in {64, 128, 256}");
+    MIGNN_REQUIRE(d >= 1 && d <= 3 && ldp >= d, "transformer_layer0_coords: 1..3 coordinates per node");
+    MIGNN_REQUIRE(ldo >= h && (h != 256 || (aligned16(out) && ldo % 4 == 0)),
+                  "transformer_layer0_coords: bad output");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "transformer_layer0_coords: bad row range");
+    if (re == rb) return MIGNN_OK;
+    const int64_t nb = (re - rb + 63) / 64;
+    const int64_t groups = (nb + 3) / 4;
+    const unsigned grid = static_cast<unsigned>(groups < 256 * 16 ? groups : 256 * 16);
+    hipStream_t st = as_stream(stream);
+    switch (h) {
+        case 256: hipLaunchKernelGGL(tf0_kernel<4>, dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, score_scale, table, gt, relu, out, ldo); break;
+        case 128: hipLaunchKernelGGL(tf0_kernel<2>, dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, score_scale, table, gt, relu, out, ldo); break;
+        default: hipLaunchKernelGGL(tf0_kernel<1>, dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, score_scale, table, gt, relu, out, ldo); break;
+    }
+    return launch_status("tf0_kernel");
 }

@@ -441,6 +441,13 @@ class FlowGNN(nn.Module):
             except RuntimeError as e:
                 raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
             first = 1
+        elif self._fuse_tf_layer0(edge_attr):
+            # input_proj + TransformerConv layer 0 from the coordinates
+            try:
+                self._tf_layer0(xin, csr, cur)
+            except RuntimeError as e:
+                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
+            first = 1
         elif self._fuse_gat_layer0():
             # input_proj + GAT layer 0 from the coordinates (mignn_gat_layer0_fused)
             try:
@@ -607,6 +614,67 @@ class FlowGNN(nn.Module):
         return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GCN"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 4
                 and self.hidden_dim in (4, 8, 16, 32, 64, 128, 256))
+
+    def _fuse_tf_layer0(self, edge_attr) -> bool:
+        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "Transformer"
+                and edge_attr is None and self.num_layers > 0 and 1 <= self.input_dim <= 3
+                and self.hidden_dim in (64, 128, 256) and self.precision == "f16x3")
+
+    def _tf_layer0_tables(self):
+        """fp64 composition of input_proj into TransformerConv layer 0
+        (mignn_transformer_layer0_coords): GT [4][12] = G_h | g_h and T [H][20]
+        = A_0..A_3 | e_0..e_3 | B | d, bias, residual and BN folded in."""
+        layer = self.gnn_layers[0]
+        ts = [layer.lin_query.weight, layer.lin_query.bias, layer.lin_key.weight,
+              layer.lin_key.bias, layer.lin_value.weight, layer.lin_value.bias,
+              layer.lin_skip.weight, layer.lin_skip.bias, self.input_proj.weight,
+              self.input_proj.bias]
+        if self.use_batch_norm:
+            bn = self.batch_norms[0].module
+            ts += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
+
+        def make():
+            d64 = lambda t: t.detach().double()  # noqa: E731
+            heads, C = layer.heads, layer.out_channels
+            H, D = self.hidden_dim, self.input_dim
+            Wq = d64(layer.lin_query.weight).view(heads, C, -1)
+            Wk = d64(layer.lin_key.weight).view(heads, C, -1)
+            Wv = d64(layer.lin_value.weight).view(heads, C, -1)
+            bq = d64(layer.lin_query.bias).view(heads, C)
+            bv = d64(layer.lin_value.bias).view(heads, C)
+            M = torch.einsum("hck,hcq->hkq", Wk, Wq)                    # qt_h = M_h x + m_h
+            mb = torch.einsum("hck,hc->hk", Wk, bq)
+            Win = torch.zeros(H, 3, dtype=torch.float64, device=Wq.device)
+            Win[:, :D] = d64(self.input_proj.weight)
+            bin_ = d64(self.input_proj.bias)
+            G = torch.einsum("ka,hkq,qb->hab", Win, M, Win)               # [h, 3, 3]
+            g = torch.einsum("ka,hk->ha", Win, torch.einsum("hkq,q->hk", M, bin_) + mb)
+            gt = torch.cat([G.reshape(heads, 9), g], 1)                    # [4, 12]
+            A = torch.einsum("chk,ka->hca", Wv.permute(1, 0, 2), Win) / heads   # [h, C, 3]
+            e = (torch.einsum("chk,k->hc", Wv.permute(1, 0, 2), bin_) + bv) / heads
+            Ws = d64(layer.lin_skip.weight)
+            B = Ws @ Win + Win
+            dd = Ws @ bin_ + d64(layer.lin_skip.bias) + bin_
+            if self.use_batch_norm:
+                bn = self.batch_norms[0].module
+                sc = d64(bn.weight) / torch.sqrt(d64(bn.running_var) + bn.eps)
+                sh = d64(bn.bias) - d64(bn.running_mean) * sc
+                A = A * sc[None, :, None]
+                e = e * sc[None, :]
+                B = B * sc[:, None]
+                dd = dd * sc + sh
+            T = torch.cat([A.permute(1, 0, 2).reshape(C, 3 * heads), e.t(), B, dd[:, None]], 1)
+            return T.float().contiguous(), gt.float().contiguous()
+        return self._cached("tf0", 0, ts, make)
+
+    def _tf_layer0(self, x, csr: Csr, out):
+        T, gt = self._tf_layer0_tables()
+        pos = self._coords(x, csr)
+        P = _lib.ptr
+        _lib.check(_lib.lib().mignn_transformer_layer0_coords(
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), self.input_dim, 0, x.shape[0],
+            self.hidden_dim, HEADS, 1.0 / math.sqrt(self.hidden_dim), P(T), P(gt), 1, P(out),
+            out.stride(0), _stream(x)), "mignn_transformer_layer0_coords")
 
     def _fuse_gat_layer0(self) -> bool:
         return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GAT"

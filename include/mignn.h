@@ -331,6 +331,20 @@ int mignn_gin_layer_fused(const int32_t* row_ptr, const int32_t* col, const floa
                           const void* img1, const float* b1, const void* img2, const float* b2,
                           const float* scale, const float* shift, int flags, float* out,
                           int64_t ldo, void* stream);
+/* TransformerConv layer 0 (4 heads, h in {64, 128, 256}) from the node
+ * coordinates: with x = pos W_in^T + b_in the layer reduces to 3-vectors --
+ * scores (G_h pos_i + g_h) . pos_j * score_scale (the row term q_i . b_in
+ * cancels in the softmax), per head P_h = sum_j a_ij pos_j and S_h = sum_j
+ * a_ij, out_i = relu?( sum_h (A_h P_h + S_h e_h) + B pos_i + d ).  gt [4][12]
+ * = G_h (3x3, row-major) | g_h; table [h][20] per output column = A_0..A_3
+ * (3 each) | e_0..e_3 | B (3) | d, with the bias, residual and BN affine
+ * folded in by the caller (fp64 composition: FlowGNN._tf_layer0_tables).
+ * No [N, h] input, no Q~K transform, no gathered feature row. */
+int mignn_transformer_layer0_coords(const int32_t* row_ptr, const int32_t* col, const float* pos,
+                                    int64_t ldp, int d, int64_t row_begin, int64_t row_end, int h,
+                                    int heads, float score_scale, const float* table,
+                                    const float* gt, int relu, float* out, int64_t ldo,
+                                    void* stream);
 /* GAT layer 0 (4 heads, h in {64, 128}) from the node coordinates
  * (input_proj composed in: with x = pos W_in^T + b_in, the logits are
  * pos . lw[:, :3] + lw[:, 3] for lw = [wlog W_in | wlog b_in] ([8][4], rows

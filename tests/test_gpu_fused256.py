@@ -446,3 +446,34 @@ def test_gat_layer0_fused_vs_fp64_and_two_step(h, flags):
     _check(g_cpu[rb:re], ref[rb:re], mag[rb:re], f"gat0 h={h}")
     _check(t_cpu[rb:re], ref[rb:re], mag[rb:re], f"gat two-step h={h}")
     assert torch.isnan(g_cpu[:rb]).all() and torch.isnan(g_cpu[re:]).all()
+
+
+@pytest.mark.parametrize("hidden", [64, 128, 256])
+def test_transformer_layer0_coords_matches_two_step(hidden, monkeypatch):
+    """TransformerConv layer 0 collapsed to 3-vectors (mignn_transformer_layer0_coords:
+    input_proj, Q~K, softmax, value / skip transforms, residual and BN composed
+    in fp64) against the model's own two-step route (input_proj, then the
+    layer) on a graph with empty and hub rows, 2-layer model with BN; and the
+    whole model against the fp64 oracle."""
+    from mignn import FlowGNN
+    from mignn.synthetic import seeded_state_dict
+    from oracle import flowgnn_oracle as orc
+    n = 3000
+    ei = _graph(n, 71)
+    g = torch.Generator(device=DEV).manual_seed(hidden)
+    x = torch.rand(n, 3, device=DEV, generator=g) * 2 - 1
+    cfg = dict(hidden_dim=hidden, num_layers=2, layer_type="Transformer")
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    sd = seeded_state_dict(m.state_dict(), seed=hidden)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "1")
+        y1 = m(x, ei)
+        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "0")
+        y0 = m(x, ei)
+    scale = max(1.0, y0.abs().max().item())
+    assert (y1 - y0).abs().max().item() <= 2e-5 * scale
+    r64 = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
+    err = (y1.cpu().double() - r64).abs().max().item()
+    assert err <= 2e-5 * max(1.0, r64.abs().max().item()), err
