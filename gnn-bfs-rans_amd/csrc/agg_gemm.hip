@@ -707,7 +707,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
 // P, S (online softmax over its CSR entries) into LDS, then the wave writes
 // the 64 rows one by one, lane l owning columns CPL l .. CPL l + CPL - 1
 // (table in registers).
-template <int CPL>
+// GAT = true: GATConv layer 0 in the same form -- scores LeakyReLU(ls_h .
+// (pos_j, 1) + ld_h . (pos_i, 1)) from the composed logit weights (GT = lw
+// [8][4] = [wlog W_in | wlog b_in]), A_h = Wcat_h W_in, e_h = Wcat_h b_in.
+template <int CPL, bool GAT = false>
 __global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ row_ptr,
                                                   const int32_t* __restrict__ col,
                                                   const float* __restrict__ pos, int64_t ldp,
@@ -737,14 +740,26 @@ __global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ ro
             float pi[3];
 #pragma unroll
             for (int d = 0; d < 3; ++d) pi[d] = d < D ? pos[row * ldp + d] : 0.f;
-            float u[HEADS][3];
+            float u[HEADS][3], ub[HEADS];           // score = u . dpos (+ ub: GAT)
 #pragma unroll
-            for (int h = 0; h < HEADS; ++h)
+            for (int h = 0; h < HEADS; ++h) {
+                if constexpr (GAT) {
+                    // a_s[j] + a_d[i] = ls . dpos + (ls + ld) . (pos_i, 1)
+                    const float* ls = GT + 4 * h;
+                    const float* ld = GT + 4 * (HEADS + h);
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    const float* gr = GT + h * 12 + 3 * a;
-                    u[h][a] = (fmaf(gr[2], pi[2], fmaf(gr[1], pi[1], fmaf(gr[0], pi[0], GT[h * 12 + 9 + a])))) * score_scale;
+                    for (int a = 0; a < 3; ++a) u[h][a] = ls[a];
+                    ub[h] = fmaf(ls[2] + ld[2], pi[2], fmaf(ls[1] + ld[1], pi[1],
+                                 fmaf(ls[0] + ld[0], pi[0], ls[3] + ld[3])));
+                } else {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        const float* gr = GT + h * 12 + 3 * a;
+                        u[h][a] = (fmaf(gr[2], pi[2], fmaf(gr[1], pi[1], fmaf(gr[0], pi[0], GT[h * 12 + 9 + a])))) * score_scale;
+                    }
+                    ub[h] = 0.f;
                 }
+            }
             float m[HEADS], l[HEADS], P[HEADS][3];
 #pragma unroll
             for (int h = 0; h < HEADS; ++h) {
@@ -763,7 +778,8 @@ __global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ ro
                 for (int d = 0; d < 3; ++d) pj[d] = d < D ? pos[j * ldp + d] - pi[d] : 0.f;
 #pragma unroll
                 for (int h = 0; h < HEADS; ++h) {
-                    const float sc = fmaf(u[h][2], pj[2], fmaf(u[h][1], pj[1], u[h][0] * pj[0]));
+                    float sc = fmaf(u[h][2], pj[2], fmaf(u[h][1], pj[1], fmaf(u[h][0], pj[0], ub[h])));
+                    if constexpr (GAT) sc = sc > 0.f ? sc : sc * score_scale;   // LeakyReLU(slope)
                     const float mn = fmaxf(m[h], sc);
                     const float corr = m[h] == -INFINITY ? 0.f : expf(m[h] - mn);
                     const float w = expf(sc - mn);
@@ -2068,4 +2084,29 @@ extern "C" int mignn_transformer_layer0_coords(const int32_t* row_ptr, const int
         default: hipLaunchKernelGGL(tf0_kernel<1>, dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, score_scale, table, gt, relu, out, ldo); break;
     }
     return launch_status("tf0_kernel");
+}
+
+extern "C" int mignn_gat_layer0_coords(const int32_t* row_ptr, const int32_t* col, const float* pos,
+                                       int64_t ldp, int d, int64_t rb, int64_t re, int h,
+                                       int heads, float negative_slope, const float* table,
+                                       const float* lw, int relu, float* out, int64_t ldo,
+                                       void* stream) {
+    MIGNN_REQUIRE(row_ptr && col && pos && table && lw && out, "gat_layer0_coords: null pointer");
+    MIGNN_REQUIRE(heads == 4 && (h == 64 || h == 128 || h == 256),
+                  "gat_layer0_coords: heads = 4, h in {64, 128, 256}");
+    MIGNN_REQUIRE(d >= 1 && d <= 3 && ldp >= d, "gat_layer0_coords: 1..3 coordinates per node");
+    MIGNN_REQUIRE(ldo >= h && (h != 256 || (aligned16(out) && ldo % 4 == 0)),
+                  "gat_layer0_coords: bad output");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gat_layer0_coords: bad row range");
+    if (re == rb) return MIGNN_OK;
+    const int64_t nb = (re - rb + 63) / 64;
+    const int64_t groups = (nb + 3) / 4;
+    const unsigned grid = static_cast<unsigned>(groups < 256 * 16 ? groups : 256 * 16);
+    hipStream_t st = as_stream(stream);
+    switch (h) {
+        case 256: hipLaunchKernelGGL((tf0_kernel<4, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo); break;
+        case 128: hipLaunchKernelGGL((tf0_kernel<2, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo); break;
+        default: hipLaunchKernelGGL((tf0_kernel<1, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo); break;
+    }
+    return launch_status("tf0_kernel<gat>");
 }

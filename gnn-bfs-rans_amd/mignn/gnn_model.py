@@ -449,9 +449,12 @@ class FlowGNN(nn.Module):
                 raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
             first = 1
         elif self._fuse_gat_layer0():
-            # input_proj + GAT layer 0 from the coordinates (mignn_gat_layer0_fused)
+            # input_proj + GAT layer 0 from the coordinates
             try:
-                self._gat_layer0(xin, csr, cur)
+                if os.environ.get("MIGNN_GAT_COORDS", "0") == "1":
+                    self._gat_layer0(xin, csr, cur)        # collapsed (mignn_gat_layer0_coords)
+                else:
+                    self._gat_layer0_mfma(xin, csr, cur)   # mignn_gat_layer0_fused
             except RuntimeError as e:
                 raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
             first = 1
@@ -679,9 +682,58 @@ class FlowGNN(nn.Module):
     def _fuse_gat_layer0(self) -> bool:
         return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GAT"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 3
-                and self.hidden_dim in (64, 128) and self.precision == "f16x3")
+                and self.hidden_dim in (64, 128, 256) and self.precision == "f16x3")
 
     def _gat_layer0(self, x, csr: Csr, out):
+        """input_proj + GAT layer 0 + residual + BN + ReLU collapsed to
+        3-vectors (mignn_gat_layer0_coords): logits through lw = [wlog W_in |
+        wlog b_in], per head P = sum alpha pos_j and S = sum alpha, output
+        sum_k (Wcat_k W_in P_k + S_k Wcat_k b_in) + bias + x_i, BN folded
+        (fp64 composition)."""
+        layer = self.gnn_layers[0]
+        H, D = self.hidden_dim, self.input_dim
+        ts = [layer.lin.weight, layer.att_src, layer.att_dst, layer.bias,
+              self.input_proj.weight, self.input_proj.bias]
+        if self.use_batch_norm:
+            bn = self.batch_norms[0].module
+            ts += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
+
+        def make():
+            d64 = lambda t: t.detach().double()  # noqa: E731
+            heads, C = layer.heads, layer.out_channels
+            W = d64(layer.lin.weight).view(heads, C, -1)                    # [h, c, k]
+            vs = torch.einsum("hck,hc->hk", W, d64(layer.att_src).view(heads, C))
+            vd = torch.einsum("hck,hc->hk", W, d64(layer.att_dst).view(heads, C))
+            wlog = torch.cat([vs, vd], 0)                                   # [8, H]
+            Win = torch.zeros(H, 3, dtype=torch.float64, device=W.device)
+            Win[:, :D] = d64(self.input_proj.weight)
+            bin_ = d64(self.input_proj.bias)
+            lw = torch.zeros(2 * heads, 4, dtype=torch.float64, device=W.device)
+            lw[:, :3] = wlog @ Win
+            lw[:, 3] = wlog @ bin_
+            A = torch.einsum("hck,ka->hca", W, Win) / heads                 # [h, C, 3]
+            e = torch.einsum("hck,k->hc", W, bin_) / heads                   # [h, C]
+            B = Win.clone()                                                 # residual x_i
+            dd = d64(layer.bias) + bin_
+            if self.use_batch_norm:
+                bn = self.batch_norms[0].module
+                sc = d64(bn.weight) / torch.sqrt(d64(bn.running_var) + bn.eps)
+                sh = d64(bn.bias) - d64(bn.running_mean) * sc
+                A = A * sc[None, :, None]
+                e = e * sc[None, :]
+                B = B * sc[:, None]
+                dd = dd * sc + sh
+            T = torch.cat([A.permute(1, 0, 2).reshape(C, 3 * heads), e.t(), B, dd[:, None]], 1)
+            return T.float().contiguous(), lw.float().contiguous()
+        T, lw = self._cached("gat0c", 0, ts, make)
+        pos = self._coords(x, csr)
+        P = _lib.ptr
+        _lib.check(_lib.lib().mignn_gat_layer0_coords(
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, 0, x.shape[0], H, HEADS,
+            float(layer.negative_slope), P(T), P(lw), 1, P(out), out.stride(0), _stream(x)),
+            "mignn_gat_layer0_coords")
+
+    def _gat_layer0_mfma(self, x, csr: Csr, out):
         """input_proj + GAT layer 0 + residual + BN + ReLU in one kernel: logits
         through [wlog W_in | wlog b_in], per head P = sum alpha pos_j and S =
         sum alpha, weighted sums W_in P + S b_in (fp64-composed weights)."""

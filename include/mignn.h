@@ -345,6 +345,15 @@ int mignn_transformer_layer0_coords(const int32_t* row_ptr, const int32_t* col, 
                                     int heads, float score_scale, const float* table,
                                     const float* gt, int relu, float* out, int64_t ldo,
                                     void* stream);
+/* GATConv layer 0 collapsed the same way (what FlowGNN runs): scores
+ * LeakyReLU(lw[h] . (pos_j, 1) + lw[4 + h] . (pos_i, 1)) (lw as
+ * mignn_gat_layer0_fused's), table [h][20] = A_0..A_3 | e_0..e_3 | B | d with
+ * A_h = Wcat_h W_in, e_h = Wcat_h b_in and the bias, residual and BN affine
+ * folded in.  No MFMA transform, no gathered feature row. */
+int mignn_gat_layer0_coords(const int32_t* row_ptr, const int32_t* col, const float* pos,
+                            int64_t ldp, int d, int64_t row_begin, int64_t row_end, int h,
+                            int heads, float negative_slope, const float* table, const float* lw,
+                            int relu, float* out, int64_t ldo, void* stream);
 /* GAT layer 0 (4 heads, h in {64, 128}) from the node coordinates
  * (input_proj composed in: with x = pos W_in^T + b_in, the logits are
  * pos . lw[:, :3] + lw[:, 3] for lw = [wlog W_in | wlog b_in] ([8][4], rows

@@ -477,3 +477,33 @@ def test_transformer_layer0_coords_matches_two_step(hidden, monkeypatch):
     r64 = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
     err = (y1.cpu().double() - r64).abs().max().item()
     assert err <= 2e-5 * max(1.0, r64.abs().max().item()), err
+
+
+@pytest.mark.parametrize("hidden", [64, 128])
+def test_gat_layer0_coords_matches_two_step(hidden, monkeypatch):
+    """GATConv layer 0 collapsed to 3-vectors (mignn_gat_layer0_coords) against
+    the model's two-step route (input_proj, then the fused layer) on a graph
+    with empty and hub rows, and the model against the fp64 oracle."""
+    from mignn import FlowGNN
+    from mignn.synthetic import seeded_state_dict
+    from oracle import flowgnn_oracle as orc
+    n = 3000
+    ei = _graph(n, 81)
+    g = torch.Generator(device=DEV).manual_seed(hidden + 1)
+    x = torch.rand(n, 3, device=DEV, generator=g) * 2 - 1
+    cfg = dict(hidden_dim=hidden, num_layers=2, layer_type="GAT")
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    sd = seeded_state_dict(m.state_dict(), seed=hidden + 1)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    monkeypatch.setenv("MIGNN_GAT_COORDS", "1")
+    with torch.no_grad():
+        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "1")
+        y1 = m(x, ei)
+        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "0")
+        y0 = m(x, ei)
+    scale = max(1.0, y0.abs().max().item())
+    assert (y1 - y0).abs().max().item() <= 2e-5 * scale
+    r64 = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
+    err = (y1.cpu().double() - r64).abs().max().item()
+    assert err <= 2e-5 * max(1.0, r64.abs().max().item()), err
