@@ -121,14 +121,18 @@ __device__ __forceinline__ float rowsum4(float v) {
 // written by the caller before the call.
 // CRES: the residual is not read but computed, x_i[n] = TB[n] . (c0, c1, c2, 1)
 // (GIN layer 0 from the coordinates: x = input_proj(pos), TB = [W_in | b_in])
-template <int NCB, bool CRES = false>
+// LG: also the next GAT layer's logits of each finished row, x_out . WLN^T
+// (WLN [8][N] in LDS) -> lgn[row][8] (the row's 4 lanes summed)
+template <int NCB, bool CRES = false, bool LG = false>
 __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float* EV,
                                                 const f32x4 (&acc)[NCB], int p, int flags,
                                                 const float* __restrict__ x, int64_t ldx,
                                                 float* __restrict__ out, int64_t ldo, int64_t t0,
                                                 int64_t re, int wave, int lane, int lself, int g,
                                                 const float* TB = nullptr, float c0 = 0.f,
-                                                float c1 = 0.f, float c2 = 0.f) {
+                                                float c1 = 0.f, float c2 = 0.f,
+                                                const float* WLN = nullptr,
+                                                float* __restrict__ lgn = nullptr) {
     constexpr int N = NCB * 16, CPR = NCB * 4, ROWB = NCB * 64, RPI = 64 / CPR, NI = 16 / RPI;
     const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
     int l = lane;
@@ -146,6 +150,7 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
     vm_barrier<0>();                           // (EV of every wave; this wave's rows landed)
     unsigned char* const srow = STG + lself * ROWB;
     const int32_t* const EQ = reinterpret_cast<const int32_t*>(EV);
+    float lp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
         const int n = 16 * cb + 4 * g;
@@ -172,6 +177,28 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
         for (int i = 0; i < 4; ++i)
             o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
         *slot = o;
+    }
+    if constexpr (LG) {
+        // (a second pass over this lane's own staged values: the accumulators
+        // are dead by now, which keeps the registers below the spill line)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+            const int n = 16 * cb + 4 * g;
+            const f32x4 o = *reinterpret_cast<const f32x4*>(srow + 16 * ((4 * cb + g) ^ (lself & 15)));
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(WLN + q * N + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lp[q] = fmaf(o[i], w[i], lp[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) lp[q] = rowsum4(lp[q]);
+        if (g == 0 && t0 + lself < re) {
+            f32x4* const dst = reinterpret_cast<f32x4*>(lgn + (t0 + lself) * 8);
+            dst[0] = f32x4{lp[0], lp[1], lp[2], lp[3]};
+            dst[1] = f32x4{lp[4], lp[5], lp[6], lp[7]};
+        }
     }
     // this wave's rows out (its own staging rows: in-order LDS)
 #pragma unroll
@@ -1142,7 +1169,7 @@ struct GatCfg {
 // the row's other lanes through LDS: it gave wrong rows in waves 4-7 of some
 // tiles, run to run, with or without extra barriers; the register form is
 // exact and deterministic.)
-template <int H, bool L0 = false>
+template <int H, bool L0 = false, bool LG = false>
 __global__ __launch_bounds__(GatCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void
 gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                  const float* __restrict__ logits, const float* __restrict__ x, int64_t ldx,
@@ -1150,7 +1177,8 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
                  const float* __restrict__ bias, const float* __restrict__ scale,
                  const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo,
                  const float* __restrict__ w_in = nullptr, const float* __restrict__ b_in = nullptr,
-                 const float* __restrict__ lw = nullptr, int D = 0) {
+                 const float* __restrict__ lw = nullptr, int D = 0,
+                 const float* __restrict__ wlog_next = nullptr, float* __restrict__ lg_next = nullptr) {
     using C = GatCfg<H>;
     constexpr int HEADS = 4;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
@@ -1444,8 +1472,12 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         EV2[2 * H + tid] = SC[tid];
         EV2[3 * H + tid] = SH[tid];
     }
-    staged_epilogue<C::NCB, L0>(lds, EV2, acc, p, flags, x, ldx, out, ldo, rb + tile * C::BM, re,
-                                wave, lane, 16 * wave + r, g, TB, pi[0], pi[1], pi[2]);
+    float* const WLN = EV2 + 4 * H;                // (LG) the next layer's logit weights [8][H]
+    if constexpr (LG)
+        for (int i = tid; i < 8 * H; i += C::NT) WLN[i] = wlog_next[i];
+    staged_epilogue<C::NCB, L0, LG>(lds, EV2, acc, p, flags, x, ldx, out, ldo, rb + tile * C::BM,
+                                    re, wave, lane, 16 * wave + r, g, TB, pi[0], pi[1], pi[2], WLN,
+                                    lg_next);
 }
 
 // ------------------------------------------------------------------ TransformerConv
@@ -1836,15 +1868,22 @@ int launch_gat_fused(const int32_t* row_ptr, const int32_t* col, const float* lo
                      const void* img, const float* bias, const float* scale, const float* shift,
                      int flags, float* out, int64_t ldo, hipStream_t st,
                      const float* w_in = nullptr, const float* b_in = nullptr,
-                     const float* lw = nullptr, int d = 0) {
+                     const float* lw = nullptr, int d = 0, const float* wlog_next = nullptr,
+                     float* lg_next = nullptr) {
     using C = GatCfg<H>;
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     const int64_t nb = (ntiles + 7) / 8 * 8;
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "gat_fused: too many rows");
-    hipLaunchKernelGGL((gat_fused_kernel<H, L0>), dim3(static_cast<unsigned>(nb)), dim3(C::NT), 0,
-                       st, row_ptr, col, logits, x, ldx, rb, re, slope,
-                       static_cast<const unsigned char*>(img), bias, scale, shift, flags, out, ldo,
-                       w_in, b_in, lw, d);
+    if (!L0 && lg_next != nullptr)
+        hipLaunchKernelGGL((gat_fused_kernel<H, false, true>), dim3(static_cast<unsigned>(nb)),
+                           dim3(C::NT), 0, st, row_ptr, col, logits, x, ldx, rb, re, slope,
+                           static_cast<const unsigned char*>(img), bias, scale, shift, flags, out,
+                           ldo, w_in, b_in, lw, d, wlog_next, lg_next);
+    else
+        hipLaunchKernelGGL((gat_fused_kernel<H, L0>), dim3(static_cast<unsigned>(nb)), dim3(C::NT),
+                           0, st, row_ptr, col, logits, x, ldx, rb, re, slope,
+                           static_cast<const unsigned char*>(img), bias, scale, shift, flags, out,
+                           ldo, w_in, b_in, lw, d, nullptr, nullptr);
     return launch_status("gat_fused_kernel");
 }
 
@@ -1922,16 +1961,19 @@ namespace mignn {
 int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
                     const float* x, int64_t ldx, int64_t rb, int64_t re, int h, float slope,
                     const void* img, const float* bias, const float* scale, const float* shift,
-                    int flags, float* out, int64_t ldo, void* stream) {
+                    int flags, float* out, int64_t ldo, void* stream, const float* wlog_next,
+                    float* lg_next) {
     MIGNN_REQUIRE(aligned16(x) && aligned16(out) && aligned16(img) && ldx % 4 == 0 && ldo % 4 == 0,
                   "gat_layer: fused path needs 16-B aligned rows");
     MIGNN_REQUIRE(x != out, "gat_layer: in-place not supported (neighbours read x)");
     hipStream_t st = as_stream(stream);
     flags |= g_fused_diag_flags;
     return h == 128 ? launch_gat_fused<128>(row_ptr, col, logits, x, ldx, rb, re, slope, img, bias,
-                                            scale, shift, flags, out, ldo, st)
+                                            scale, shift, flags, out, ldo, st, nullptr, nullptr,
+                                            nullptr, 0, wlog_next, lg_next)
                     : launch_gat_fused<64>(row_ptr, col, logits, x, ldx, rb, re, slope, img, bias,
-                                           scale, shift, flags, out, ldo, st);
+                                           scale, shift, flags, out, ldo, st, nullptr, nullptr,
+                                           nullptr, 0, wlog_next, lg_next);
 }
 }  // namespace mignn
 

@@ -51,13 +51,13 @@ extern "C" size_t mignn_gat_layer_scratch_bytes(int64_t n_x, int64_t rows, int h
            align256(static_cast<size_t>(rows) * heads * h * 4);
 }
 
-extern "C" int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const float* x,
-                               int64_t ldx, int64_t n_x, int64_t row_begin, int64_t row_end, int h,
-                               int heads, float negative_slope, const float* wlog,
-                               const float* logits, int64_t ldl, const float* wcat,
-                               const void* wcat_img, const float* bias, const float* scale,
-                               const float* shift, int flags, void* scratch, size_t scratch_bytes,
-                               float* out, int64_t ldo, void* stream) {
+static int gat_layer_impl(const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx,
+                          int64_t n_x, int64_t row_begin, int64_t row_end, int h, int heads,
+                          float negative_slope, const float* wlog, const float* logits,
+                          int64_t ldl, const float* wcat, const void* wcat_img, const float* bias,
+                          const float* scale, const float* shift, int flags, void* scratch,
+                          size_t scratch_bytes, float* out, int64_t ldo, void* stream,
+                          const float* wlog_next, float* logits_next) {
     MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gat_layer: unknown flags 0x%x", flags);
     MIGNN_REQUIRE(row_ptr && col && x && out && (logits || wlog) && (wcat || wcat_img),
                   "gat_layer: null pointer");
@@ -87,16 +87,50 @@ extern "C" int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const
     // never reaches memory
     if (wcat_img != nullptr && heads == 4 && (h == 64 || h == 128) && g_gat_fused)
         return gat_layer_fused(row_ptr, col, lg, x, ldx, row_begin, row_end, h, negative_slope,
-                               wcat_img, bias, scale, shift, flags, out, ldo, stream);
+                               wcat_img, bias, scale, shift, flags, out, ldo, stream, wlog_next,
+                               logits_next);
     float* agg = reinterpret_cast<float*>(base);
     const int64_t lda = static_cast<int64_t>(heads) * h;
     // the aggregation writes row r at agg + r * lda for r in [row_begin, row_end)
     if (int rc = mignn_gat_aggregate(row_ptr, col, lg, x, ldx, row_begin, row_end, h, heads,
                                      negative_slope, agg - row_begin * lda, lda, stream))
         return rc;
-    return transform(agg, lda, rows, heads * h, nullptr, 0, 0, wcat, wcat_img, h, bias,
-                     x + row_begin * ldx, ldx, scale, shift, flags, out + row_begin * ldo, ldo,
-                     stream);
+    if (int rc = transform(agg, lda, rows, heads * h, nullptr, 0, 0, wcat, wcat_img, h, bias,
+                           x + row_begin * ldx, ldx, scale, shift, flags, out + row_begin * ldo,
+                           ldo, stream))
+        return rc;
+    if (logits_next == nullptr) return MIGNN_OK;
+    // the next layer's logits of the rows just written
+    return mignn_linear(out + row_begin * ldo, ldo, rows, h, nullptr, 0, 0, wlog_next, 2 * heads,
+                        nullptr, nullptr, 0, nullptr, nullptr, 0, logits_next + row_begin * 2 * heads,
+                        2 * heads, stream);
+}
+
+extern "C" int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const float* x,
+                               int64_t ldx, int64_t n_x, int64_t row_begin, int64_t row_end, int h,
+                               int heads, float negative_slope, const float* wlog,
+                               const float* logits, int64_t ldl, const float* wcat,
+                               const void* wcat_img, const float* bias, const float* scale,
+                               const float* shift, int flags, void* scratch, size_t scratch_bytes,
+                               float* out, int64_t ldo, void* stream) {
+    return gat_layer_impl(row_ptr, col, x, ldx, n_x, row_begin, row_end, h, heads, negative_slope,
+                          wlog, logits, ldl, wcat, wcat_img, bias, scale, shift, flags, scratch,
+                          scratch_bytes, out, ldo, stream, nullptr, nullptr);
+}
+
+extern "C" int mignn_gat_layer_next(const int32_t* row_ptr, const int32_t* col, const float* x,
+                                    int64_t ldx, int64_t n_x, int64_t row_begin, int64_t row_end,
+                                    int h, int heads, float negative_slope, const float* wlog,
+                                    const float* logits, int64_t ldl, const float* wcat,
+                                    const void* wcat_img, const float* bias, const float* scale,
+                                    const float* shift, int flags, void* scratch,
+                                    size_t scratch_bytes, float* out, int64_t ldo,
+                                    const float* wlog_next, float* logits_next, void* stream) {
+    MIGNN_REQUIRE(wlog_next && logits_next && aligned16(logits_next),
+                  "gat_layer_next: wlog_next / 16-B aligned logits_next");
+    return gat_layer_impl(row_ptr, col, x, ldx, n_x, row_begin, row_end, h, heads, negative_slope,
+                          wlog, logits, ldl, wcat, wcat_img, bias, scale, shift, flags, scratch,
+                          scratch_bytes, out, ldo, stream, wlog_next, logits_next);
 }
 
 extern "C" size_t mignn_transformer_layer_scratch_bytes(int64_t rows, int h, int heads) {

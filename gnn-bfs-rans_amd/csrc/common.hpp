@@ -164,7 +164,8 @@ int transformer_aggregate_rows(const int32_t* row_ptr, const int32_t* col, const
 int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* logits,
                     const float* x, int64_t ldx, int64_t rb, int64_t re, int h, float slope,
                     const void* img, const float* bias, const float* scale, const float* shift,
-                    int flags, float* out, int64_t ldo, void* stream);
+                    int flags, float* out, int64_t ldo, void* stream,
+                    const float* wlog_next = nullptr, float* lg_next = nullptr);
 // the fused TransformerConv (H = 256, 4 heads; agg_gemm.hip): image of wout
 // in the fused k order, and the aggregate + output transform kernel over qt
 size_t tf_fused_prep_bytes();

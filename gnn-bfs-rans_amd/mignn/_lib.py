@@ -47,6 +47,9 @@ SIGNATURES = {
     "mignn_gat_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int64, c_int, c_int,
                                 c_float, _P, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P,
                                 c_size_t, _P, c_int64, _P]),
+    "mignn_gat_layer_next": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int64, c_int, c_int,
+                                     c_float, _P, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P,
+                                     c_size_t, _P, c_int64, _P, _P, _P]),
     "mignn_transformer_layer_scratch_bytes": (c_size_t, [c_int64, c_int, c_int]),
     "mignn_transformer_layer": (c_int, [_P, _P, _P, c_int64, c_int64, c_int64, c_int, c_int,
                                         c_float, _P, _P, _P, _P, _P, _P, _P, _P, c_int, _P,

@@ -468,6 +468,10 @@ class FlowGNN(nn.Module):
         else:
             # input_proj (gnn_model.py:159), gathered into the CSR's node order
             self._input_proj(xin, cur, rows=csr.perm)
+        # GAT: a layer's epilogue forms the next layer's logits (no logit GEMV launch)
+        chain = (self.layer_type == "GAT" and self.precision == "f16x3"
+                 and os.environ.get("MIGNN_GAT_NEXT_LOGITS", "0") == "1")
+        lg_cur = None
         for i, layer in enumerate(self.gnn_layers):
             if i < first:
                 continue
@@ -476,7 +480,13 @@ class FlowGNN(nn.Module):
                     # PyG TransformerConv.message adds a non-None edge_attr to value_j
                     # ([E, heads, C] + [E, d]); reproduce the resulting torch error.
                     _value_plus_edge_attr_check((E, HEADS, H), tuple(edge_attr.shape))
-                self._layer(i, layer, csr, cur, nxt, 0, num_nodes)
+                lg_next = None
+                if chain and i + 1 < len(self.gnn_layers):
+                    lg_next = torch.empty((num_nodes, 2 * HEADS), dtype=torch.float32,
+                                          device=x.device)
+                self._layer(i, layer, csr, cur, nxt, 0, num_nodes, logits=lg_cur,
+                            logits_next=lg_next)
+                lg_cur = lg_next
             except RuntimeError as e:
                 raise self._layer_error(i, e, num_nodes, edge_index, cur, edge_attr) from e
             cur, nxt = nxt, cur
@@ -898,7 +908,8 @@ class FlowGNN(nn.Module):
             return linear_f16x3(a, img, w.shape[0], bias, **kw)
         return linear(a, w, bias, **kw)
 
-    def _layer(self, i, layer, csr: Csr, x, out, rb: int, re: int, logits=None):
+    def _layer(self, i, layer, csr: Csr, x, out, rb: int, re: int, logits=None,
+               logits_next=None):
         """One conv + residual + BN + ReLU (gnn_model.py:162-192) for rows [rb, re).
         `x` holds every row the CSR references (own rows + halo rows).  GAT:
         `logits` [rows, 2*heads] of every referenced row, precomputed by a
@@ -973,6 +984,17 @@ class FlowGNN(nn.Module):
             n_x = x.shape[0]
             nb = L.mignn_gat_layer_scratch_bytes(0 if logits is not None else n_x, n, H, HEADS)
             scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=x.device)
+            if logits_next is not None:
+                # this layer's epilogue also forms the next GAT layer's logits
+                nl = self.gnn_layers[i + 1]
+                wlog_n, _ = self._cached("gat", i + 1, (nl.lin.weight, nl.att_src, nl.att_dst),
+                                         lambda: self._gat_weights(nl))
+                _lib.check(L.mignn_gat_layer_next(
+                    P(csr.row_ptr), P(csr.col), P(x), x.stride(0), n_x, rb, re, H, HEADS,
+                    float(layer.negative_slope), P(wlog), P(logits), 2 * HEADS, P(wcat), P(img),
+                    P(layer.bias), P(scale), P(shift), epi, P(scratch), nb, P(out), out.stride(0),
+                    P(wlog_n), P(logits_next), st), "mignn_gat_layer_next")
+                return
             _lib.check(L.mignn_gat_layer(
                 P(csr.row_ptr), P(csr.col), P(x), x.stride(0), n_x, rb, re, H, HEADS,
                 float(layer.negative_slope), P(wlog), P(logits), 2 * HEADS, P(wcat), P(img),

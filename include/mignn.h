@@ -207,6 +207,17 @@ int mignn_gat_layer(const int32_t* row_ptr, const int32_t* col, const float* x, 
                     const float* wcat, const void* wcat_img, const float* bias,
                     const float* scale, const float* shift, int flags, void* scratch,
                     size_t scratch_bytes, float* out, int64_t ldo, void* stream);
+/* mignn_gat_layer that also writes the NEXT GAT layer's logits of its rows,
+ * logits_next[r][2*heads] = out[r] . wlog_next^T (wlog_next: the next layer's
+ * wlog), from the fused kernel's epilogue (the [rows, 2*heads] logit GEMV of
+ * the next call is then skipped by passing logits_next as its `logits`). */
+int mignn_gat_layer_next(const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx,
+                         int64_t n_x, int64_t row_begin, int64_t row_end, int h, int heads,
+                         float negative_slope, const float* wlog, const float* logits,
+                         int64_t ldl, const float* wcat, const void* wcat_img, const float* bias,
+                         const float* scale, const float* shift, int flags, void* scratch,
+                         size_t scratch_bytes, float* out, int64_t ldo, const float* wlog_next,
+                         float* logits_next, void* stream);
 size_t mignn_transformer_layer_scratch_bytes(int64_t rows, int h, int heads);
 int mignn_transformer_layer(const int32_t* row_ptr, const int32_t* col, const float* x,
                             int64_t ldx, int64_t row_begin, int64_t row_end, int h, int heads,

@@ -507,3 +507,46 @@ def test_gat_layer0_coords_matches_two_step(hidden, monkeypatch):
     r64 = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
     err = (y1.cpu().double() - r64).abs().max().item()
     assert err <= 2e-5 * max(1.0, r64.abs().max().item()), err
+
+
+@pytest.mark.parametrize("h", [64, 128])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_gat_layer_next_logits(h, fused):
+    """mignn_gat_layer_next: the same output rows as mignn_gat_layer, plus the
+    next layer's logits of those rows (out . wlog_next^T), from the fused
+    kernel's epilogue (fused) or a GEMV after the launch sequence (0)."""
+    n = 3000
+    rb, re = 40, 2960
+    ei = _graph(n, 91)
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
+    g = torch.Generator(device=DEV).manual_seed(h + 3 * fused)
+    x = torch.randn(n, h, device=DEV, generator=g)
+    wlog = torch.randn(8, h, device=DEV, generator=g) / h ** 0.5
+    wnext = torch.randn(8, h, device=DEV, generator=g) / h ** 0.5
+    wcat = torch.randn(h, 4 * h, device=DEV, generator=g) / (2 * h) ** 0.5
+    bias = torch.randn(h, device=DEV, generator=g) * 0.1
+    sc = torch.rand(h, device=DEV, generator=g) + 0.5
+    sh = torch.randn(h, device=DEV, generator=g) * 0.1
+    img = f16x3_image(wcat)
+    L = _lib.lib()
+    P = _lib.ptr
+    _lib.check(L.mignn_diag_set_gat_fused(fused), "gat_fused")
+    try:
+        ref = torch.full((n, h), float("nan"), device=DEV)
+        _gat_layer(csr, x, n, rb, re, h, wlog, wcat, img, bias, sc, sh, 15, ref)
+        out = torch.full((n, h), float("nan"), device=DEV)
+        lg = torch.full((n, 8), float("nan"), device=DEV)
+        nb = L.mignn_gat_layer_scratch_bytes(n, re - rb, h, 4)
+        scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=DEV)
+        _lib.check(L.mignn_gat_layer_next(P(csr.row_ptr), P(csr.col), P(x), h, n, rb, re, h, 4, 0.2,
+                                          P(wlog), None, 8, P(wcat), P(img), P(bias), P(sc), P(sh),
+                                          15, P(scratch), nb, P(out), h, P(wnext), P(lg),
+                                          _lib.stream()), "gat_layer_next")
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(L.mignn_diag_set_gat_fused(1), "gat_fused")
+    assert torch.equal(out[rb:re], ref[rb:re])
+    want = out[rb:re].double() @ wnext.double().T
+    err = (lg[rb:re].double() - want).abs().max().item()
+    assert err <= 1e-5 * max(1.0, want.abs().max().item()), err
+    assert torch.isnan(lg[:rb]).all() and torch.isnan(lg[re:]).all()
