@@ -451,7 +451,7 @@ class FlowGNN(nn.Module):
         elif self._fuse_gat_layer0():
             # input_proj + GAT layer 0 from the coordinates
             try:
-                if os.environ.get("MIGNN_GAT_COORDS", "0") == "1":
+                if os.environ.get("MIGNN_GAT_COORDS", "1") == "1":
                     self._gat_layer0(xin, csr, cur)        # collapsed (mignn_gat_layer0_coords)
                 else:
                     self._gat_layer0_mfma(xin, csr, cur)   # mignn_gat_layer0_fused
@@ -470,7 +470,7 @@ class FlowGNN(nn.Module):
             self._input_proj(xin, cur, rows=csr.perm)
         # GAT: a layer's epilogue forms the next layer's logits (no logit GEMV launch)
         chain = (self.layer_type == "GAT" and self.precision == "f16x3"
-                 and os.environ.get("MIGNN_GAT_NEXT_LOGITS", "0") == "1")
+                 and os.environ.get("MIGNN_GAT_NEXT_LOGITS", "1") == "1")
         lg_cur = None
         for i, layer in enumerate(self.gnn_layers):
             if i < first:
