@@ -21,7 +21,8 @@ for f in glob.glob("gpurun_out/pmcl/p*/*counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
         for k in ("sum_rows_kernel", "tf_rows_kernel", "gat_rows_kernel", "gemm_f16x3_kernel",
-                  "agg_gemm_kernel", "gat_fused_kernel"):
+                  "agg_gemm_kernel", "gat_fused_kernel", "tf_fused_kernel", "head256_kernel",
+                  "gin0_fused_kernel", "tf0_kernel"):
             if k in n:
                 vals[(k, r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in sorted(vals.items()):
