@@ -744,8 +744,13 @@ __global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ ro
                                                   int D, int64_t rb, int64_t re, float score_scale,
                                                   const float* __restrict__ T,
                                                   const float* __restrict__ GT, int relu,
-                                                  float* __restrict__ out, int64_t ldo) {
+                                                  float* __restrict__ out, int64_t ldo,
+                                                  const float* __restrict__ wlog_next = nullptr,
+                                                  float* __restrict__ lg_next = nullptr) {
     constexpr int HEADS = 4, NW = 4, SL = 20;
+    // (GAT, lg_next given: each written row's next-layer logits, out . wlog_next^T,
+    // summed over the wave's 64 lanes)
+    const bool lgn = GAT && lg_next != nullptr;
     __shared__ __attribute__((aligned(16))) float slot[NW][64][SL];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -755,6 +760,11 @@ __global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ ro
     for (int k = 0; k < CPL; ++k)
 #pragma unroll
         for (int i = 0; i < SL; ++i) tb[k][i] = T[(lane * CPL + k) * SL + i];
+    float wn[8][CPL];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) wn[q][k] = lgn ? wlog_next[q * (64 * CPL) + lane * CPL + k] : 0.f;
     const int64_t nb = (re - rb + 63) / 64;
     const int64_t groups = (nb + NW - 1) / NW;
     for (int64_t b = static_cast<int64_t>(blockIdx.x); b < groups; b += gridDim.x) {
@@ -850,6 +860,23 @@ __global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ ro
             } else {
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) dst[k] = o[k];
+            }
+            if (lgn) {
+                float lq[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int k = 0; k < CPL; ++k) a = fmaf(o[k], wn[q][k], a);
+#pragma unroll
+                    for (int sh = 32; sh > 0; sh >>= 1) a += __shfl_xor(a, sh);
+                    lq[q] = a;
+                }
+                if (lane == 0) {
+                    f32x4* const ld = reinterpret_cast<f32x4*>(lg_next + (rb + batch * 64 + rr) * 8);
+                    ld[0] = f32x4{lq[0], lq[1], lq[2], lq[3]};
+                    ld[1] = f32x4{lq[4], lq[5], lq[6], lq[7]};
+                }
             }
         }
         __syncthreads();
@@ -2132,7 +2159,10 @@ extern "C" int mignn_gat_layer0_coords(const int32_t* row_ptr, const int32_t* co
                                        int64_t ldp, int d, int64_t rb, int64_t re, int h,
                                        int heads, float negative_slope, const float* table,
                                        const float* lw, int relu, float* out, int64_t ldo,
-                                       void* stream) {
+                                       const float* wlog_next, float* logits_next, void* stream) {
+    MIGNN_REQUIRE((wlog_next == nullptr) == (logits_next == nullptr) &&
+                      (logits_next == nullptr || aligned16(logits_next)),
+                  "gat_layer0_coords: wlog_next and 16-B aligned logits_next go together");
     MIGNN_REQUIRE(row_ptr && col && pos && table && lw && out, "gat_layer0_coords: null pointer");
     MIGNN_REQUIRE(heads == 4 && (h == 64 || h == 128 || h == 256),
                   "gat_layer0_coords: heads = 4, h in {64, 128, 256}");
@@ -2146,9 +2176,9 @@ extern "C" int mignn_gat_layer0_coords(const int32_t* row_ptr, const int32_t* co
     const unsigned grid = static_cast<unsigned>(groups < 256 * 16 ? groups : 256 * 16);
     hipStream_t st = as_stream(stream);
     switch (h) {
-        case 256: hipLaunchKernelGGL((tf0_kernel<4, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo); break;
-        case 128: hipLaunchKernelGGL((tf0_kernel<2, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo); break;
-        default: hipLaunchKernelGGL((tf0_kernel<1, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo); break;
+        case 256: hipLaunchKernelGGL((tf0_kernel<4, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo, wlog_next, logits_next); break;
+        case 128: hipLaunchKernelGGL((tf0_kernel<2, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo, wlog_next, logits_next); break;
+        default: hipLaunchKernelGGL((tf0_kernel<1, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, pos, ldp, d, rb, re, negative_slope, table, lw, relu, out, ldo, wlog_next, logits_next); break;
     }
     return launch_status("tf0_kernel<gat>");
 }

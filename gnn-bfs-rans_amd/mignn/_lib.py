@@ -135,7 +135,7 @@ SIGNATURES = {
     "mignn_transformer_layer0_coords": (c_int, [_P, _P, _P, c_int64, c_int, c_int64, c_int64, c_int,
                                                 c_int, c_float, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gat_layer0_coords": (c_int, [_P, _P, _P, c_int64, c_int, c_int64, c_int64, c_int, c_int,
-                                        c_float, _P, _P, c_int, _P, c_int64, _P]),
+                                        c_float, _P, _P, c_int, _P, c_int64, _P, _P, _P]),
     "mignn_gat_layer0_fused": (c_int, [_P, _P, _P, c_int64, c_int, c_int64, c_int64, c_int, c_float,
                                        _P, _P, _P, _P, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gin_layer0_fused": (c_int, [_P, _P, _P, c_int64, c_int, c_int64, c_int64, c_int, c_float,

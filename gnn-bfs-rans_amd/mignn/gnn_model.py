@@ -434,6 +434,7 @@ class FlowGNN(nn.Module):
         csr = self._csr.get(edge_index, num_nodes, mode, pos)
         cur, nxt = buf_a, buf_b
         first = 0
+        lg0 = None                                   # (GAT) layer 1's logits from layer 0
         if self._fuse_layer0():
             # input_proj + GCN layer 0 from the coordinates (mignn_gcn_layer0_coords)
             try:
@@ -452,7 +453,11 @@ class FlowGNN(nn.Module):
             # input_proj + GAT layer 0 from the coordinates
             try:
                 if os.environ.get("MIGNN_GAT_COORDS", "1") == "1":
-                    self._gat_layer0(xin, csr, cur)        # collapsed (mignn_gat_layer0_coords)
+                    if (self.num_layers > 1 and os.environ.get("MIGNN_GAT_NEXT_LOGITS", "1") == "1"
+                            and os.environ.get("MIGNN_GAT_L0_LOGITS", "0") == "1"):
+                        lg0 = torch.empty((num_nodes, 2 * HEADS), dtype=torch.float32,
+                                          device=x.device)
+                    self._gat_layer0(xin, csr, cur, logits_next=lg0)  # collapsed
                 else:
                     self._gat_layer0_mfma(xin, csr, cur)   # mignn_gat_layer0_fused
             except RuntimeError as e:
@@ -471,7 +476,7 @@ class FlowGNN(nn.Module):
         # GAT: a layer's epilogue forms the next layer's logits (no logit GEMV launch)
         chain = (self.layer_type == "GAT" and self.precision == "f16x3"
                  and os.environ.get("MIGNN_GAT_NEXT_LOGITS", "1") == "1")
-        lg_cur = None
+        lg_cur = lg0
         for i, layer in enumerate(self.gnn_layers):
             if i < first:
                 continue
@@ -694,7 +699,7 @@ class FlowGNN(nn.Module):
                 and self.num_layers > 0 and 1 <= self.input_dim <= 3
                 and self.hidden_dim in (64, 128, 256) and self.precision == "f16x3")
 
-    def _gat_layer0(self, x, csr: Csr, out):
+    def _gat_layer0(self, x, csr: Csr, out, logits_next=None):
         """input_proj + GAT layer 0 + residual + BN + ReLU collapsed to
         3-vectors (mignn_gat_layer0_coords): logits through lw = [wlog W_in |
         wlog b_in], per head P = sum alpha pos_j and S = sum alpha, output
@@ -738,10 +743,15 @@ class FlowGNN(nn.Module):
         T, lw = self._cached("gat0c", 0, ts, make)
         pos = self._coords(x, csr)
         P = _lib.ptr
+        wlog_n = None
+        if logits_next is not None:
+            nl = self.gnn_layers[1]
+            wlog_n, _ = self._cached("gat", 1, (nl.lin.weight, nl.att_src, nl.att_dst),
+                                     lambda: self._gat_weights(nl))
         _lib.check(_lib.lib().mignn_gat_layer0_coords(
             P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, 0, x.shape[0], H, HEADS,
-            float(layer.negative_slope), P(T), P(lw), 1, P(out), out.stride(0), _stream(x)),
-            "mignn_gat_layer0_coords")
+            float(layer.negative_slope), P(T), P(lw), 1, P(out), out.stride(0), P(wlog_n),
+            P(logits_next), _stream(x)), "mignn_gat_layer0_coords")
 
     def _gat_layer0_mfma(self, x, csr: Csr, out):
         """input_proj + GAT layer 0 + residual + BN + ReLU in one kernel: logits

@@ -360,11 +360,14 @@ int mignn_transformer_layer0_coords(const int32_t* row_ptr, const int32_t* col, 
  * LeakyReLU(lw[h] . (pos_j, 1) + lw[4 + h] . (pos_i, 1)) (lw as
  * mignn_gat_layer0_fused's), table [h][20] = A_0..A_3 | e_0..e_3 | B | d with
  * A_h = Wcat_h W_in, e_h = Wcat_h b_in and the bias, residual and BN affine
- * folded in.  No MFMA transform, no gathered feature row. */
+ * folded in.  No MFMA transform, no gathered feature row.  wlog_next /
+ * logits_next (both or neither): also the next GAT layer's logits of the
+ * written rows, as mignn_gat_layer_next. */
 int mignn_gat_layer0_coords(const int32_t* row_ptr, const int32_t* col, const float* pos,
                             int64_t ldp, int d, int64_t row_begin, int64_t row_end, int h,
                             int heads, float negative_slope, const float* table, const float* lw,
-                            int relu, float* out, int64_t ldo, void* stream);
+                            int relu, float* out, int64_t ldo, const float* wlog_next,
+                            float* logits_next, void* stream);
 /* GAT layer 0 (4 heads, h in {64, 128}) from the node coordinates
  * (input_proj composed in: with x = pos W_in^T + b_in, the logits are
  * pos . lw[:, :3] + lw[:, 3] for lw = [wlog W_in | wlog b_in] ([8][4], rows

@@ -550,3 +550,26 @@ def test_gat_layer_next_logits(h, fused):
     err = (lg[rb:re].double() - want).abs().max().item()
     assert err <= 1e-5 * max(1.0, want.abs().max().item()), err
     assert torch.isnan(lg[:rb]).all() and torch.isnan(lg[re:]).all()
+
+
+@pytest.mark.parametrize("hidden", [64, 128])
+def test_gat_layer0_next_logits(hidden, monkeypatch):
+    """The collapsed GAT layer 0 also forming layer 1's logits (summed over
+    the wave's lanes in mignn_gat_layer0_coords) gives the same model output
+    as layer 1 computing them itself."""
+    from mignn import FlowGNN
+    from mignn.synthetic import seeded_state_dict
+    n = 3000
+    ei = _graph(n, 83)
+    g = torch.Generator(device=DEV).manual_seed(hidden + 7)
+    x = torch.rand(n, 3, device=DEV, generator=g) * 2 - 1
+    cfg = dict(hidden_dim=hidden, num_layers=3, layer_type="GAT")
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=hidden + 7))
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        monkeypatch.setenv("MIGNN_GAT_L0_LOGITS", "1")
+        y1 = m(x, ei)
+        monkeypatch.setenv("MIGNN_GAT_L0_LOGITS", "0")
+        y0 = m(x, ei)
+    assert (y1 - y0).abs().max().item() <= 1e-5 * max(1.0, y0.abs().max().item())
