@@ -883,7 +883,11 @@ __global__ __launch_bounds__(256) void tf0_kernel(const int32_t* __restrict__ ro
     }
 }
 
+#ifdef MIGNN_DIAG
 int g_fused_diag_flags = 0;   // mignn_diag_set_fused_flags (timing ablations; wrong results)
+#else
+constexpr int g_fused_diag_flags = 0;   // the product library has no ablation state
+#endif
 
 // k-permuted split image of W2 [256, 256] for the chained transform: element
 // j of lane (m, g) in fragment (kc, cb) = W2[16 cb + m][16 (2 kc + j / 4) +
@@ -2004,12 +2008,14 @@ int gat_layer_fused(const int32_t* row_ptr, const int32_t* col, const float* log
 }
 }  // namespace mignn
 
+#ifdef MIGNN_DIAG
 extern "C" int mignn_diag_set_fused_flags(int flags) {
     g_fused_diag_flags = flags & (MIGNN_DIAG_NO_PRODUCE | MIGNN_DIAG_NO_MFMA | MIGNN_DIAG_NO_EXT |
                                   MIGNN_DIAG_NO_TABLES | MIGNN_DIAG_NO_LOCAL |
                                   MIGNN_SCHED_INTERLEAVED);
     return MIGNN_OK;
 }
+#endif
 
 namespace mignn {
 size_t head256_prep_bytes() { return HEAD256_BYTES; }

@@ -27,7 +27,11 @@ namespace {
 
 inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
+#ifdef MIGNN_DIAG
 bool g_gat_fused = true;     // mignn_diag_set_gat_fused (A/B timing against the launch sequence)
+#else
+constexpr bool g_gat_fused = true;
+#endif
 
 // the transform of either arithmetic: img != NULL -> split fp16, else fp32 w
 int transform(const float* a, int64_t lda, int64_t m, int k1, const float* a2, int64_t lda2,
@@ -58,7 +62,10 @@ static int gat_layer_impl(const int32_t* row_ptr, const int32_t* col, const floa
                           const float* scale, const float* shift, int flags, void* scratch,
                           size_t scratch_bytes, float* out, int64_t ldo, void* stream,
                           const float* wlog_next, float* logits_next) {
-    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gat_layer: unknown flags 0x%x", flags);
+    MIGNN_REQUIRE((flags & ~(MIGNN_EPI_MASK | MIGNN_GAT_LAUNCHES)) == 0,
+                  "gat_layer: unknown flags 0x%x", flags);
+    const bool launches = (flags & MIGNN_GAT_LAUNCHES) != 0 || !g_gat_fused;
+    flags &= MIGNN_EPI_MASK;
     MIGNN_REQUIRE(row_ptr && col && x && out && (logits || wlog) && (wcat || wcat_img),
                   "gat_layer: null pointer");
     MIGNN_REQUIRE(row_begin >= 0 && row_end >= row_begin && n_x >= row_end,
@@ -85,7 +92,7 @@ static int gat_layer_impl(const int32_t* row_ptr, const int32_t* col, const floa
     // split-fp16 transform, 4 heads, h in {64, 128}: aggregation and head-mean
     // transform in one kernel (agg_gemm.hip) -- the [rows, heads h] aggregate
     // never reaches memory
-    if (wcat_img != nullptr && heads == 4 && (h == 64 || h == 128) && g_gat_fused)
+    if (wcat_img != nullptr && heads == 4 && (h == 64 || h == 128) && !launches)
         return gat_layer_fused(row_ptr, col, lg, x, ldx, row_begin, row_end, h, negative_slope,
                                wcat_img, bias, scale, shift, flags, out, ldo, stream, wlog_next,
                                logits_next);
@@ -219,7 +226,9 @@ extern "C" int mignn_transformer_layer_fused(
                     score_scale, wout_fimg, bout, scale, shift, flags, out, ldo, stream);
 }
 
+#ifdef MIGNN_DIAG
 extern "C" int mignn_diag_set_gat_fused(int on) {
     g_gat_fused = on != 0;
     return MIGNN_OK;
 }
+#endif

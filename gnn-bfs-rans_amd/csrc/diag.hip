@@ -15,6 +15,8 @@
 //   | 8     non-temporal output stores
 #include "common.hpp"
 
+#ifdef MIGNN_DIAG   // diagnostic library only (libmignn_diag.so)
+
 namespace mignn {
 namespace {
 
@@ -285,3 +287,5 @@ extern "C" int mignn_diag_clock(int blocks, int iters, int64_t* out, void* strea
                        out);
     return launch_status("clock_probe_kernel");
 }
+
+#endif  // MIGNN_DIAG

@@ -255,7 +255,11 @@ __device__ __forceinline__ void stamp(unsigned long long* trace, int lane, int64
     if (trace != nullptr && blockIdx.x < 8 && s >= 0 && s < 64 && lane == 0)
         trace[(blockIdx.x * 64 + s) * 8 + slot] = __builtin_amdgcn_s_memtime();
 }
+#ifdef MIGNN_DIAG
 unsigned long long* g_trace16_host = nullptr;   // set by mignn_diag_set_trace_f16x3
+#else
+constexpr unsigned long long* g_trace16_host = nullptr;
+#endif
 
 // zeros read by the empty out-of-tile slots (a valid, always-cached address)
 __device__ __attribute__((aligned(16))) float g_zero_row[256];
@@ -901,10 +905,19 @@ int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, co
 
 using namespace mignn;
 
+static int gcn_f16x3_impl(const int32_t* row_ptr, const int32_t* col,
+                                          const float* ew, const float* x, int64_t ldx,
+                                          int64_t rb, int64_t re, int h, const float* w,
+                                          const float* bias, const float* scale,
+                                          const float* shift, int flags, float* out, int64_t ldo,
+                                          void* stream);
+
+#ifdef MIGNN_DIAG
 extern "C" int mignn_diag_set_trace_f16x3(void* buf) {
     g_trace16_host = static_cast<unsigned long long*>(buf);
     return MIGNN_OK;
 }
+#endif
 
 extern "C" int mignn_device_errors(unsigned int* out, int clear) {
     MIGNN_REQUIRE(out, "device_errors: null pointer");
@@ -925,11 +938,11 @@ extern "C" int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col,
                                      const float* shift, int flags, float* out, int64_t ldo,
                                      void* stream) {
     MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer_f16x3: unknown flags 0x%x", flags);
-    return mignn_diag_gcn_layer_f16x3(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift,
+    return gcn_f16x3_impl(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift,
                                       flags, out, ldo, stream);
 }
 
-extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col,
+static int gcn_f16x3_impl(const int32_t* row_ptr, const int32_t* col,
                                           const float* ew, const float* x, int64_t ldx,
                                           int64_t rb, int64_t re, int h, const float* w,
                                           const float* bias, const float* scale,
@@ -956,3 +969,14 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
                     : launch_f16x3<64, 4>(row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift,
                                           flags, out, ldo, st);
 }
+
+#ifdef MIGNN_DIAG
+extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col,
+                                          const float* ew, const float* x, int64_t ldx,
+                                          int64_t rb, int64_t re, int h, const float* w,
+                                          const float* bias, const float* scale,
+                                          const float* shift, int flags, float* out, int64_t ldo,
+                                          void* stream) {
+    return gcn_f16x3_impl(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift, flags, out, ldo, stream);
+}
+#endif

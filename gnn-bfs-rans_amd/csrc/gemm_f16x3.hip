@@ -424,6 +424,12 @@ __global__ __launch_bounds__(GNT, RPW == 1 ? 2 : 1) void gemm_f16x3_kernel(
 
 using namespace mignn;
 
+static int linear_f16x3_impl(const float* a, int64_t lda, int64_t m, int k1,
+                                       const float* a2, int64_t lda2, int k2, const void* img,
+                                       int n, const float* bias, const float* residual,
+                                       int64_t ldr, const float* scale, const float* shift,
+                                       int flags, float* c, int64_t ldc, void* stream);
+
 extern "C" size_t mignn_linear_f16x3_prep_bytes(int n, int k) {
     if (n <= 0 || k <= 0) return 0;
     const int kp = (k + 31) / 32;
@@ -456,11 +462,11 @@ extern "C" int mignn_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1
                                   const float* shift, int flags, float* c, int64_t ldc,
                                   void* stream) {
     MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "linear_f16x3: unknown flags 0x%x", flags);
-    return mignn_diag_linear_f16x3(a, lda, m, k1, a2, lda2, k2, img, n, bias, residual, ldr, scale,
+    return linear_f16x3_impl(a, lda, m, k1, a2, lda2, k2, img, n, bias, residual, ldr, scale,
                                    shift, flags, c, ldc, stream);
 }
 
-extern "C" int mignn_diag_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1,
+static int linear_f16x3_impl(const float* a, int64_t lda, int64_t m, int k1,
                                        const float* a2, int64_t lda2, int k2, const void* img,
                                        int n, const float* bias, const float* residual,
                                        int64_t ldr, const float* scale, const float* shift,
@@ -487,3 +493,13 @@ extern "C" int mignn_diag_linear_f16x3(const float* a, int64_t lda, int64_t m, i
                        scale, shift, flags, c, ldc, tmr, tnr);
     return launch_status("gemm_f16x3_kernel");
 }
+
+#ifdef MIGNN_DIAG
+extern "C" int mignn_diag_linear_f16x3(const float* a, int64_t lda, int64_t m, int k1,
+                                       const float* a2, int64_t lda2, int k2, const void* img,
+                                       int n, const float* bias, const float* residual,
+                                       int64_t ldr, const float* scale, const float* shift,
+                                       int flags, float* c, int64_t ldc, void* stream) {
+    return linear_f16x3_impl(a, lda, m, k1, a2, lda2, k2, img, n, bias, residual, ldr, scale, shift, flags, c, ldc, stream);
+}
+#endif

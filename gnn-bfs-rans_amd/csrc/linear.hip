@@ -185,16 +185,22 @@ __global__ __launch_bounds__(256) void narrow_linear_kernel(const float* __restr
 
 using namespace mignn;
 
+static int linear_impl(const float* a, int64_t lda, int64_t m, int k, const float* a2,
+                                 int64_t lda2, int k2, const float* w, int n, const float* bias,
+                                 const float* residual, int64_t ldr, const float* scale,
+                                 const float* shift, int flags, float* c, int64_t ldc,
+                                 void* stream);
+
 extern "C" int mignn_linear(const float* a, int64_t lda, int64_t m, int k, const float* a2,
                             int64_t lda2, int k2, const float* w, int n, const float* bias,
                             const float* residual, int64_t ldr, const float* scale,
                             const float* shift, int flags, float* c, int64_t ldc, void* stream) {
     MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "linear: unknown flags 0x%x", flags);
-    return mignn_diag_linear(a, lda, m, k, a2, lda2, k2, w, n, bias, residual, ldr, scale, shift,
+    return linear_impl(a, lda, m, k, a2, lda2, k2, w, n, bias, residual, ldr, scale, shift,
                              flags, c, ldc, stream);
 }
 
-extern "C" int mignn_diag_linear(const float* a, int64_t lda, int64_t m, int k, const float* a2,
+static int linear_impl(const float* a, int64_t lda, int64_t m, int k, const float* a2,
                                  int64_t lda2, int k2, const float* w, int n, const float* bias,
                                  const float* residual, int64_t ldr, const float* scale,
                                  const float* shift, int flags, float* c, int64_t ldc,
@@ -255,3 +261,13 @@ extern "C" int mignn_input_proj_rows(const float* x, int64_t n, int in_dim, cons
                        dim3(block), 0, as_stream(stream), x, n, in_dim, rows, w, b, h, out, ldo);
     return launch_status("input_proj_kernel");
 }
+
+#ifdef MIGNN_DIAG
+extern "C" int mignn_diag_linear(const float* a, int64_t lda, int64_t m, int k, const float* a2,
+                                 int64_t lda2, int k2, const float* w, int n, const float* bias,
+                                 const float* residual, int64_t ldr, const float* scale,
+                                 const float* shift, int flags, float* c, int64_t ldc,
+                                 void* stream) {
+    return linear_impl(a, lda, m, k, a2, lda2, k2, w, n, bias, residual, ldr, scale, shift, flags, c, ldc, stream);
+}
+#endif

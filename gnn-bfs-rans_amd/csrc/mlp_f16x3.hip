@@ -413,6 +413,7 @@ extern "C" int mignn_mlp_head(const float* x, int64_t ldx, int64_t n, int h, con
     return launch_status("mlp_head_kernel");
 }
 
+#ifdef MIGNN_DIAG
 extern "C" int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img,
                                    float* out, void* stream) {
     MIGNN_REQUIRE(x && img && out && n > 0 && mode >= 0 && mode <= 5, "diag_mlp_head: bad args");
@@ -438,3 +439,4 @@ extern "C" int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const vo
     }
     return launch_status("mlp_head_kernel(diag)");
 }
+#endif

@@ -605,10 +605,18 @@ int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, i
 
 using namespace mignn;
 
+static int gcn_layer_impl(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                                    const float* x, int64_t ldx, int64_t rb, int64_t re, int h,
+                                    const float* w, const float* bias, const float* scale,
+                                    const float* shift, int flags, float* out, int64_t ldo,
+                                    void* stream);
+
+#ifdef MIGNN_DIAG
 extern "C" int mignn_diag_set_trace(void* buf) {
     MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf)));
     return MIGNN_OK;
 }
+#endif
 
 extern "C" int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
                                const float* x, int64_t ldx, int64_t rb, int64_t re, int h,
@@ -616,11 +624,11 @@ extern "C" int mignn_gcn_layer(const int32_t* row_ptr, const int32_t* col, const
                                const float* shift, int flags, float* out, int64_t ldo,
                                void* stream) {
     MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer: unknown flags 0x%x", flags);
-    return mignn_diag_gcn_layer(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift, flags,
+    return gcn_layer_impl(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift, flags,
                                 out, ldo, stream);
 }
 
-extern "C" int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
+static int gcn_layer_impl(const int32_t* row_ptr, const int32_t* col, const float* ew,
                                     const float* x, int64_t ldx, int64_t rb, int64_t re, int h,
                                     const float* w, const float* bias, const float* scale,
                                     const float* shift, int flags, float* out, int64_t ldo,
@@ -672,3 +680,13 @@ extern "C" int mignn_gin_layer(const int32_t* row_ptr, const int32_t* col, const
                 scale, shift, flags, h, out, ldo};
     return dispatch_tile<ROWS>(h, h, t2, st);
 }
+
+#ifdef MIGNN_DIAG
+extern "C" int mignn_diag_gcn_layer(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                                    const float* x, int64_t ldx, int64_t rb, int64_t re, int h,
+                                    const float* w, const float* bias, const float* scale,
+                                    const float* shift, int flags, float* out, int64_t ldo,
+                                    void* stream) {
+    return gcn_layer_impl(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift, flags, out, ldo, stream);
+}
+#endif

@@ -65,6 +65,16 @@ SIGNATURES = {
                                 c_int, _P, c_int64, _P]),
     "mignn_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                       _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_plan_bytes": (c_size_t, [c_int64, c_int64]),
+    "mignn_gcn_plan": (c_int, [_P, _P, _P, c_int64, c_int64, c_int, _P, c_size_t, _P]),
+    "mignn_gcn_layer_planned": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
+                                        _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_aggregate_planned": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int,
+                                            _P, c_int64, _P]),
+    "mignn_gcn_ring_plan_bytes": (c_size_t, [c_int64, c_int64, c_int]),
+    "mignn_gcn_ring_plan": (c_int, [_P, _P, _P, c_int64, c_int64, c_int, _P, c_size_t, _P, _P]),
+    "mignn_gcn_layer_ring": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
+                                     _P, _P, c_int, _P, c_int64, _P]),
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
     "mignn_mlp_head_prep": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int, c_int, _P, c_size_t,
                                     _P]),
@@ -161,6 +171,9 @@ DIAG_SIGNATURES = {
                                      _P, c_int, _P, c_int64, _P]),
     "mignn_diag_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                            _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_diag_gcn_tile": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64,
+                                    c_int, _P, _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_diag_ring_trace": (c_int, [_P]),
     "mignn_diag_set_gat_fused": (c_int, [c_int]),
     "mignn_diag_set_fused_flags": (c_int, [c_int]),
     "mignn_diag_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,
@@ -168,30 +181,48 @@ DIAG_SIGNATURES = {
 }
 
 _lib = None
+_diag = None
+DIAG_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmignn_diag.so")
 
 
 class MignnError(RuntimeError):
     pass
 
 
+def _load(path, sigs):
+    if not os.path.exists(path):
+        raise MignnError(
+            f"{os.path.basename(path)} not found at {path}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+            "There is no CPU fallback.")
+    h = ctypes.CDLL(path)
+    for name, (res, args) in sigs.items():
+        fn = getattr(h, name)
+        fn.restype = res
+        fn.argtypes = args
+    if h.mignn_abi_version() != 1:
+        raise MignnError("libmignn ABI mismatch")
+    return h
+
+
 def lib():
-    """Load (once) and return the ctypes handle; raise if the .so is missing."""
+    """Load (once) and return the ctypes handle of the product library
+    (libmignn.so: the C ABI of include/mignn.h, nothing else); raise if the
+    .so is missing."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise MignnError(
-                f"{LIB_NAME} not found at {LIB_PATH}: build it with "
-                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
-                "There is no CPU fallback.")
-        h = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in {**SIGNATURES, **DIAG_SIGNATURES}.items():
-            fn = getattr(h, name)
-            fn.restype = res
-            fn.argtypes = args
-        if h.mignn_abi_version() != 1:
-            raise MignnError("libmignn ABI mismatch")
-        _lib = h
+        _lib = _load(LIB_PATH, SIGNATURES)
     return _lib
+
+
+def diag_lib():
+    """The diagnostic build (libmignn_diag.so: the product entry points plus
+    the timing-study entries of include/mignn_diag.h).  Used by scripts/ only;
+    the product path and the tests never load it."""
+    global _diag
+    if _diag is None:
+        _diag = _load(DIAG_LIB_PATH, {**SIGNATURES, **DIAG_SIGNATURES})
+    return _diag
 
 
 def ptr(t) -> int | None:

@@ -128,7 +128,7 @@ class Csr:
     ids inside the CSR are the internal ids: internal row p is caller node
     perm[p], caller node v is internal row inv[v]."""
     __slots__ = ("row_ptr", "col", "dinv", "ew", "info", "num_nodes", "num_edges", "edge_index",
-                 "perm", "inv", "pos", "key_tensor")
+                 "perm", "inv", "pos", "key_tensor", "plans")
 
     def __init__(self, row_ptr, col, dinv, info, num_nodes, num_edges, edge_index, ew=None):
         self.row_ptr, self.col, self.dinv, self.info = row_ptr, col, dinv, info
@@ -136,6 +136,23 @@ class Csr:
         self.ew = ew
         self.perm = self.inv = self.pos = None
         self.key_tensor = None   # the caller's edge_index the cache key was made from
+        self.plans: Dict[Tuple[int, int, int], torch.Tensor] = {}
+
+    def gcn_plan(self, h: int, row_begin: int, row_end: int) -> torch.Tensor:
+        """The tile plan of rows [row_begin, row_end) for hidden width h
+        (mignn_gcn_plan), built on first use and kept with the CSR (it copies
+        the ew weights: rebuilt after compute_gcn_weights)."""
+        key = (h, row_begin, row_end)
+        plan = self.plans.get(key)
+        if plan is None:
+            L = _lib.lib()
+            nb = L.mignn_gcn_plan_bytes(row_begin, row_end)
+            plan = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.col.device)
+            _lib.check(L.mignn_gcn_plan(_lib.ptr(self.row_ptr), _lib.ptr(self.col),
+                                        _lib.ptr(self.ew), row_begin, row_end, h, _lib.ptr(plan),
+                                        nb, _lib.stream(self.col.device)), "mignn_gcn_plan")
+            self.plans[key] = plan
+        return plan
 
     def compute_gcn_weights(self, row_begin: int = 0, row_end: Optional[int] = None):
         """Per-entry PyG gcn_norm weights (mignn_gcn_norm); call again after the
@@ -143,6 +160,7 @@ class Csr:
         re = self.num_nodes if row_end is None else row_end
         if self.ew is None:
             self.ew = torch.empty_like(self.col, dtype=torch.float32)
+        self.plans.clear()
         _lib.check(_lib.lib().mignn_gcn_norm(_lib.ptr(self.row_ptr), _lib.ptr(self.col),
                                              _lib.ptr(self.dinv), row_begin, re, _lib.ptr(self.ew),
                                              _lib.stream(self.col.device)), "mignn_gcn_norm")
@@ -389,6 +407,13 @@ class FlowGNN(nn.Module):
         # internal locality order of the nodes: "auto" (meshes of >= 2^20
         # nodes with 3-D cell-centre features), "1" always, "0" never
         self.reorder = os.environ.get("MIGNN_REORDER", "auto")
+        # split-fp16 GCN layer kernel at H in {64, 128}: "tile" (the tile-plan
+        # kernel, csrc/gcn_tile.hip), "pc" (the producer / consumer kernel,
+        # csrc/gcn_f16x3.hip) or "auto" (the faster one measured per H: tile at
+        # H = 64, pc at H = 128); read once here, not per forward
+        self.gcn_kernel = os.environ.get("MIGNN_GCN_KERNEL", "auto")
+        if self.gcn_kernel not in ("tile", "pc", "auto"):
+            raise ValueError(f"MIGNN_GCN_KERNEL must be auto, tile or pc, got {self.gcn_kernel!r}")
         self._csr = _CsrCache()
         self._prep: Dict[Tuple, object] = {}
         self._dtypes_checked = False
@@ -935,7 +960,15 @@ class FlowGNN(nn.Module):
             return
         if self.layer_type == "GCN":
             w, b = layer.lin.weight, layer.bias
-            if H in (64, 128):
+            kern = self.gcn_kernel if self.gcn_kernel != "auto" else ("tile" if H == 64 else "pc")
+            if H in (64, 128) and self.precision == "f16x3" and kern == "tile":
+                # the hot kernel: split-fp16 GCN layer over the CSR's tile plan
+                plan = csr.gcn_plan(H, rb, re)
+                _lib.check(L.mignn_gcn_layer_planned(
+                    P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
+                    P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),
+                    "mignn_gcn_layer_planned")
+            elif H in (64, 128):
                 fn = L.mignn_gcn_layer_f16x3 if self.precision == "f16x3" else L.mignn_gcn_layer
                 _lib.check(fn(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
                               P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),

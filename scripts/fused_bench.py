@@ -40,11 +40,11 @@ if mode == "gat":
     WLOG = torch.randn(8, H, device=dev, generator=g) / H ** 0.5
     WCAT = torch.randn(H, 4 * H, device=dev, generator=g) / (2 * H) ** 0.5
     img1 = f16x3_image(WCAT)
-    GSCR = torch.empty(max(_lib.lib().mignn_gat_layer_scratch_bytes(n, n, H, 4), 1), dtype=torch.uint8,
+    GSCR = torch.empty(max(_lib.diag_lib().mignn_gat_layer_scratch_bytes(n, n, H, 4), 1), dtype=torch.uint8,
                        device=dev)
 else:
     img1, img2, img2s = f16x3_image(W1), gin_fused_image(W2), f16x3_image(W2)
-L = _lib.lib()
+L = _lib.diag_lib()
 P = _lib.ptr
 st = _lib.stream()
 

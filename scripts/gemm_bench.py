@@ -13,7 +13,7 @@ if os.environ.get("GB_LIB"):                       # an alternative build (exper
     _lib.LIB_PATH = os.environ["GB_LIB"]
 from mignn.gnn_model import f16x3_image, linear, linear_f16x3  # noqa: E402
 
-L, P = _lib.lib(), _lib.ptr
+L, P = _lib.diag_lib(), _lib.ptr
 
 M = int(os.environ.get("GB_M", 2_000_000))
 SHAPES = [  # (name, k1, k2, n, residual)

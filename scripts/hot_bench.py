@@ -37,7 +37,7 @@ W = torch.randn(H, H, device=dev, generator=g) * 0.05
 b = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
-L = _lib.lib()
+L = _lib.diag_lib()
 P = _lib.ptr
 st = _lib.stream()
 FL = 15

@@ -82,7 +82,7 @@ b = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
 csum0 = [float(t.double().sum()) for t in (X, W, csr.ew, csr.col, csr.row_ptr)]
-L = _lib.lib()
+L = _lib.diag_lib()
 P = _lib.ptr
 st = _lib.stream()
 

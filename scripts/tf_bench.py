@@ -33,7 +33,7 @@ WOUT = torch.randn(H, HEADS * H + HEADS + H, device=dev, generator=g) / 36
 BOUT = torch.randn(H, device=dev, generator=g) * 0.1
 SC = torch.rand(H, device=dev, generator=g) + 0.5
 SH = torch.randn(H, device=dev, generator=g) * 0.1
-L = _lib.lib()
+L = _lib.diag_lib()
 P = _lib.ptr
 st = _lib.stream()
 IMG_Q, IMG_O = f16x3_image(WQK), f16x3_image(WOUT)

@@ -16,6 +16,7 @@ import torch
 from mignn import _lib
 from mignn.gnn_model import build_csr, f16x3_image, gin_fused_image, linear_f16x3
 
+GAT_LAUNCHES = 64   # include/mignn.h MIGNN_GAT_LAUNCHES
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 H = 256
@@ -207,7 +208,7 @@ def _gat_layer(csr, x, n_x, rb, re, h, wlog, wcat, img, bias, sc, sh, flags, out
 @pytest.mark.parametrize("flags", [15, 1 | 2])
 def test_gat_fused_vs_launches_and_fp64(h, flags):
     """mignn_gat_layer's fused kernel (split-fp16 image given, 4 heads) against
-    its aggregate + transform launch sequence (mignn_diag_set_gat_fused(0))
+    its aggregate + transform launch sequence (flag MIGNN_GAT_LAUNCHES)
     and against a float64 restatement (PyG GATConv semantics on the CSR:
     LeakyReLU(0.2) logits, softmax + 1e-16, head mean, bias) on a graph with
     hub rows (the kernel's past-the-slots path) and a row sub-range."""
@@ -225,11 +226,10 @@ def test_gat_fused_vs_launches_and_fp64(h, flags):
     img = f16x3_image(wcat)
     outs = []
     for fused in (1, 0):
-        _lib.check(_lib.lib().mignn_diag_set_gat_fused(fused), "gat_fused")
         o = torch.full((n, h), float("nan"), device=DEV)
-        _gat_layer(csr, x, n, rb, re, h, wlog, wcat, img, bias, sc, sh, flags, o)
+        _gat_layer(csr, x, n, rb, re, h, wlog, wcat, img, bias, sc, sh,
+                   flags | (0 if fused else GAT_LAUNCHES), o)
         outs.append(o)
-    _lib.check(_lib.lib().mignn_diag_set_gat_fused(1), "gat_fused")
     torch.cuda.synchronize()
     got, launches = outs[0].cpu(), outs[1].cpu()
     assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
@@ -530,21 +530,19 @@ def test_gat_layer_next_logits(h, fused):
     img = f16x3_image(wcat)
     L = _lib.lib()
     P = _lib.ptr
-    _lib.check(L.mignn_diag_set_gat_fused(fused), "gat_fused")
-    try:
+    lf = 0 if fused else GAT_LAUNCHES
+    if True:
         ref = torch.full((n, h), float("nan"), device=DEV)
-        _gat_layer(csr, x, n, rb, re, h, wlog, wcat, img, bias, sc, sh, 15, ref)
+        _gat_layer(csr, x, n, rb, re, h, wlog, wcat, img, bias, sc, sh, 15 | lf, ref)
         out = torch.full((n, h), float("nan"), device=DEV)
         lg = torch.full((n, 8), float("nan"), device=DEV)
         nb = L.mignn_gat_layer_scratch_bytes(n, re - rb, h, 4)
         scratch = torch.empty(max(nb, 1), dtype=torch.uint8, device=DEV)
         _lib.check(L.mignn_gat_layer_next(P(csr.row_ptr), P(csr.col), P(x), h, n, rb, re, h, 4, 0.2,
                                           P(wlog), None, 8, P(wcat), P(img), P(bias), P(sc), P(sh),
-                                          15, P(scratch), nb, P(out), h, P(wnext), P(lg),
+                                          15 | lf, P(scratch), nb, P(out), h, P(wnext), P(lg),
                                           _lib.stream()), "gat_layer_next")
         torch.cuda.synchronize()
-    finally:
-        _lib.check(L.mignn_diag_set_gat_fused(1), "gat_fused")
     assert torch.equal(out[rb:re], ref[rb:re])
     want = out[rb:re].double() @ wnext.double().T
     err = (lg[rb:re].double() - want).abs().max().item()

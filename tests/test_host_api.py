@@ -38,6 +38,25 @@ def test_library_exports_every_header_symbol():
     assert _lib.lib().mignn_abi_version() == 1
 
 
+def _dynamic_symbols(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True,
+                         text=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def test_product_library_has_no_diagnostic_state():
+    """libmignn.so (what the product path loads) exports no timing-study entry
+    (mignn_diag_*) and exactly the C functions of include/mignn.h: ablation
+    switches and traces live only in libmignn_diag.so (built from the same
+    sources with -DMIGNN_DIAG), so no call can change a later product launch."""
+    syms = {s for s in _dynamic_symbols(_lib.LIB_PATH) if s.startswith("mignn_")}
+    assert not {s for s in syms if s.startswith("mignn_diag")}, sorted(syms)
+    assert syms == set(header_functions()), sorted(syms ^ set(header_functions()))
+    diag = {s for s in _dynamic_symbols(_lib.DIAG_LIB_PATH) if s.startswith("mignn_diag")}
+    assert diag == set(_lib.DIAG_SIGNATURES), sorted(diag ^ set(_lib.DIAG_SIGNATURES))
+
+
 @pytest.mark.parametrize("name", model_names())
 def test_state_dict_layout_matches_reference(name):
     cfg, sd, _, _ = model_fixture(name)
