@@ -76,6 +76,10 @@ class RangeLayout:
         self.lo, self.hi, self.n_own = lo, hi, hi - lo
         src, dst = edge_index[0].long(), edge_index[1].long()
         E = int(src.numel())
+        if self.n_own <= 0 and E > 0:
+            # (checked before any device indexing: a rank that owns no rows
+            # cannot own a destination either)
+            raise ValueError("edge_index holds an edge whose destination this rank does not own")
         own_src = (src >= lo) & (src < hi)
         # ghost marks over the global ids (+1 dummy slot for owned sources)
         mark = torch.zeros(N + 1, dtype=torch.int32, device=dev)

@@ -414,15 +414,23 @@ class FlowGNN(nn.Module):
         self.gcn_kernel = os.environ.get("MIGNN_GCN_KERNEL", "auto")
         if self.gcn_kernel not in ("tile", "pc", "auto"):
             raise ValueError(f"MIGNN_GCN_KERNEL must be auto, tile or pc, got {self.gcn_kernel!r}")
+        # kernel-route switches (A/B studies; the defaults are the measured
+        # fastest routes), read once at construction -- plain attributes after
+        # that, never environment lookups inside forward:
+        #   fuse_layer0     input_proj composed into layer 0 (MIGNN_FUSE_LAYER0)
+        #   gat_coords      GAT layer 0 collapsed to 3-vectors (MIGNN_GAT_COORDS)
+        #   gat_next_logits a GAT layer's epilogue forms the next layer's
+        #                   logits (MIGNN_GAT_NEXT_LOGITS)
+        #   fused256        H = 256 fused layer / head kernels: "1", "0",
+        #                   "layer" or "head" (MIGNN_FUSED256)
+        self.fuse_layer0 = os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1"
+        self.gat_coords = os.environ.get("MIGNN_GAT_COORDS", "1") == "1"
+        self.gat_next_logits = os.environ.get("MIGNN_GAT_NEXT_LOGITS", "1") == "1"
+        self.fused256 = os.environ.get("MIGNN_FUSED256", "1")
+        if self.fused256 not in ("0", "1", "layer", "head"):
+            raise ValueError(f"MIGNN_FUSED256 must be 0, 1, layer or head, got {self.fused256!r}")
         self._csr = _CsrCache()
         self._prep: Dict[Tuple, object] = {}
-        self._dtypes_checked = False
-
-    def _apply(self, fn, *args, **kwargs):
-        # every parameter conversion / move passes here: re-check the dtypes
-        # at the next forward
-        self._dtypes_checked = False
-        return super()._apply(fn, *args, **kwargs)
 
     # ------------------------------------------------------------------ API
     def predict_fields(self, output: torch.Tensor) -> dict:
@@ -459,7 +467,6 @@ class FlowGNN(nn.Module):
         csr = self._csr.get(edge_index, num_nodes, mode, pos)
         cur, nxt = buf_a, buf_b
         first = 0
-        lg0 = None                                   # (GAT) layer 1's logits from layer 0
         if self._fuse_layer0():
             # input_proj + GCN layer 0 from the coordinates (mignn_gcn_layer0_coords)
             try:
@@ -477,12 +484,8 @@ class FlowGNN(nn.Module):
         elif self._fuse_gat_layer0():
             # input_proj + GAT layer 0 from the coordinates
             try:
-                if os.environ.get("MIGNN_GAT_COORDS", "1") == "1":
-                    if (self.num_layers > 1 and os.environ.get("MIGNN_GAT_NEXT_LOGITS", "1") == "1"
-                            and os.environ.get("MIGNN_GAT_L0_LOGITS", "0") == "1"):
-                        lg0 = torch.empty((num_nodes, 2 * HEADS), dtype=torch.float32,
-                                          device=x.device)
-                    self._gat_layer0(xin, csr, cur, logits_next=lg0)  # collapsed
+                if self.gat_coords:
+                    self._gat_layer0(xin, csr, cur)   # collapsed (mignn_gat_layer0_coords)
                 else:
                     self._gat_layer0_mfma(xin, csr, cur)   # mignn_gat_layer0_fused
             except RuntimeError as e:
@@ -499,9 +502,8 @@ class FlowGNN(nn.Module):
             # input_proj (gnn_model.py:159), gathered into the CSR's node order
             self._input_proj(xin, cur, rows=csr.perm)
         # GAT: a layer's epilogue forms the next layer's logits (no logit GEMV launch)
-        chain = (self.layer_type == "GAT" and self.precision == "f16x3"
-                 and os.environ.get("MIGNN_GAT_NEXT_LOGITS", "1") == "1")
-        lg_cur = lg0
+        chain = self.layer_type == "GAT" and self.precision == "f16x3" and self.gat_next_logits
+        lg_cur = None
         for i, layer in enumerate(self.gnn_layers):
             if i < first:
                 continue
@@ -531,13 +533,11 @@ class FlowGNN(nn.Module):
                 "graph to 'cuda' (HIP).")
         if self.input_proj.weight.device != x.device:
             raise RuntimeError(f"model is on {self.input_proj.weight.device}, input on {x.device}")
-        if not self._dtypes_checked:
-            # once per .to() / .float() / .half() ... (nn.Module._apply below),
-            # not per forward
-            for p in self.parameters():
-                if p.dtype != torch.float32:
-                    raise RuntimeError("mignn FlowGNN computes in fp32; parameters must be float32")
-            self._dtypes_checked = True
+        # every forward (a few attribute reads): parameters swapped in by
+        # load_state_dict(assign=True) or direct assignment bypass _apply
+        for p in self.parameters():
+            if p.dtype != torch.float32:
+                raise RuntimeError("mignn FlowGNN computes in fp32; parameters must be float32")
         if self.hidden_dim % 8 != 0:
             raise RuntimeError("mignn FlowGNN requires hidden_dim % 8 == 0")
         if self.precision not in ("f32", "f16x3"):
@@ -654,12 +654,12 @@ class FlowGNN(nn.Module):
             f"{edge_attr.shape if edge_attr is not None else 'None'}")
 
     def _fuse_layer0(self) -> bool:
-        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GCN"
+        return (self.fuse_layer0 and self.layer_type == "GCN"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 4
                 and self.hidden_dim in (4, 8, 16, 32, 64, 128, 256))
 
     def _fuse_tf_layer0(self, edge_attr) -> bool:
-        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "Transformer"
+        return (self.fuse_layer0 and self.layer_type == "Transformer"
                 and edge_attr is None and self.num_layers > 0 and 1 <= self.input_dim <= 3
                 and self.hidden_dim in (64, 128, 256) and self.precision == "f16x3")
 
@@ -720,11 +720,14 @@ class FlowGNN(nn.Module):
             out.stride(0), _stream(x)), "mignn_transformer_layer0_coords")
 
     def _fuse_gat_layer0(self) -> bool:
-        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GAT"
+        # (the MFMA form, gat_coords off, has kernels for H in {64, 128} only;
+        # at H = 256 it is the two-step route then)
+        return (self.fuse_layer0 and self.layer_type == "GAT"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 3
-                and self.hidden_dim in (64, 128, 256) and self.precision == "f16x3")
+                and (self.hidden_dim in (64, 128) or (self.hidden_dim == 256 and self.gat_coords))
+                and self.precision == "f16x3")
 
-    def _gat_layer0(self, x, csr: Csr, out, logits_next=None):
+    def _gat_layer0(self, x, csr: Csr, out):
         """input_proj + GAT layer 0 + residual + BN + ReLU collapsed to
         3-vectors (mignn_gat_layer0_coords): logits through lw = [wlog W_in |
         wlog b_in], per head P = sum alpha pos_j and S = sum alpha, output
@@ -768,15 +771,10 @@ class FlowGNN(nn.Module):
         T, lw = self._cached("gat0c", 0, ts, make)
         pos = self._coords(x, csr)
         P = _lib.ptr
-        wlog_n = None
-        if logits_next is not None:
-            nl = self.gnn_layers[1]
-            wlog_n, _ = self._cached("gat", 1, (nl.lin.weight, nl.att_src, nl.att_dst),
-                                     lambda: self._gat_weights(nl))
         _lib.check(_lib.lib().mignn_gat_layer0_coords(
             P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, 0, x.shape[0], H, HEADS,
-            float(layer.negative_slope), P(T), P(lw), 1, P(out), out.stride(0), P(wlog_n),
-            P(logits_next), _stream(x)), "mignn_gat_layer0_coords")
+            float(layer.negative_slope), P(T), P(lw), 1, P(out), out.stride(0), None, None,
+            _stream(x)), "mignn_gat_layer0_coords")
 
     def _gat_layer0_mfma(self, x, csr: Csr, out):
         """input_proj + GAT layer 0 + residual + BN + ReLU in one kernel: logits
@@ -812,7 +810,7 @@ class FlowGNN(nn.Module):
             "mignn_gat_layer0_fused")
 
     def _fuse_gin_layer0(self) -> bool:
-        return (os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1" and self.layer_type == "GIN"
+        return (self.fuse_layer0 and self.layer_type == "GIN"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 3 and self.hidden_dim == 256
                 and self._fused256())
 
@@ -932,7 +930,7 @@ class FlowGNN(nn.Module):
         the output head (mignn_mlp_head at h = 256; part "head").
         MIGNN_FUSED256=0 runs the aggregate + GEMM launches for both, "layer" /
         "head" keeps only that part fused."""
-        v = os.environ.get("MIGNN_FUSED256", "1")
+        v = self.fused256
         return self.precision == "f16x3" and (v == "1" or v == part)
 
     def _mm(self, tag, i, srcs, w, a, bias=None, **kw):

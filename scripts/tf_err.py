@@ -29,7 +29,7 @@ seeds = torch.randperm(n, generator=g)[:48].to(dev)
 ys = {}
 with torch.no_grad():
     for mode in ("1", "layer", "head", "0"):
-        os.environ["MIGNN_FUSED256"] = mode
+        m.fused256 = mode
         ys[mode] = m(x, ei)[seeds].cpu().double()
 nodes, sub = khop_subgraph(ei, n, seeds, 6)
 xs, subc = x[nodes].cpu(), sub.cpu()

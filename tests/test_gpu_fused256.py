@@ -468,9 +468,9 @@ def test_transformer_layer0_coords_matches_two_step(hidden, monkeypatch):
     m.load_state_dict(sd)
     m = m.to(DEV).eval()
     with torch.no_grad():
-        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "1")
+        m.fuse_layer0 = True
         y1 = m(x, ei)
-        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "0")
+        m.fuse_layer0 = False
         y0 = m(x, ei)
     scale = max(1.0, y0.abs().max().item())
     assert (y1 - y0).abs().max().item() <= 2e-5 * scale
@@ -479,7 +479,7 @@ def test_transformer_layer0_coords_matches_two_step(hidden, monkeypatch):
     assert err <= 2e-5 * max(1.0, r64.abs().max().item()), err
 
 
-@pytest.mark.parametrize("hidden", [64, 128])
+@pytest.mark.parametrize("hidden", [64, 128, 256])
 def test_gat_layer0_coords_matches_two_step(hidden, monkeypatch):
     """GATConv layer 0 collapsed to 3-vectors (mignn_gat_layer0_coords) against
     the model's two-step route (input_proj, then the fused layer) on a graph
@@ -496,11 +496,11 @@ def test_gat_layer0_coords_matches_two_step(hidden, monkeypatch):
     sd = seeded_state_dict(m.state_dict(), seed=hidden + 1)
     m.load_state_dict(sd)
     m = m.to(DEV).eval()
-    monkeypatch.setenv("MIGNN_GAT_COORDS", "1")
+    m.gat_coords = True
     with torch.no_grad():
-        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "1")
+        m.fuse_layer0 = True
         y1 = m(x, ei)
-        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "0")
+        m.fuse_layer0 = False
         y0 = m(x, ei)
     scale = max(1.0, y0.abs().max().item())
     assert (y1 - y0).abs().max().item() <= 2e-5 * scale
@@ -509,7 +509,7 @@ def test_gat_layer0_coords_matches_two_step(hidden, monkeypatch):
     assert err <= 2e-5 * max(1.0, r64.abs().max().item()), err
 
 
-@pytest.mark.parametrize("h", [64, 128])
+@pytest.mark.parametrize("h", [64, 128, 256])
 @pytest.mark.parametrize("fused", [1, 0])
 def test_gat_layer_next_logits(h, fused):
     """mignn_gat_layer_next: the same output rows as mignn_gat_layer, plus the
@@ -550,24 +550,3 @@ def test_gat_layer_next_logits(h, fused):
     assert torch.isnan(lg[:rb]).all() and torch.isnan(lg[re:]).all()
 
 
-@pytest.mark.parametrize("hidden", [64, 128])
-def test_gat_layer0_next_logits(hidden, monkeypatch):
-    """The collapsed GAT layer 0 also forming layer 1's logits (summed over
-    the wave's lanes in mignn_gat_layer0_coords) gives the same model output
-    as layer 1 computing them itself."""
-    from mignn import FlowGNN
-    from mignn.synthetic import seeded_state_dict
-    n = 3000
-    ei = _graph(n, 83)
-    g = torch.Generator(device=DEV).manual_seed(hidden + 7)
-    x = torch.rand(n, 3, device=DEV, generator=g) * 2 - 1
-    cfg = dict(hidden_dim=hidden, num_layers=3, layer_type="GAT")
-    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
-    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=hidden + 7))
-    m = m.to(DEV).eval()
-    with torch.no_grad():
-        monkeypatch.setenv("MIGNN_GAT_L0_LOGITS", "1")
-        y1 = m(x, ei)
-        monkeypatch.setenv("MIGNN_GAT_L0_LOGITS", "0")
-        y0 = m(x, ei)
-    assert (y1 - y0).abs().max().item() <= 1e-5 * max(1.0, y0.abs().max().item())

@@ -410,9 +410,9 @@ def test_gcn_layer0_fusion_matches(H, bn, reorder, monkeypatch):
     m.reorder = reorder
     x, ei = grid_graph(13, 10, 9, device=DEV, permute_seed=2)
     with torch.no_grad():
-        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "0")
+        m.fuse_layer0 = False
         y0 = m(x, ei)
-        monkeypatch.setenv("MIGNN_FUSE_LAYER0", "1")
+        m.fuse_layer0 = True
         y1 = m(x, ei)
     assert (y0 - y1).abs().max().item() < 2e-6 * max(1.0, y0.abs().max().item())
 
