@@ -193,17 +193,28 @@ def main():
         bounds = [r * N_local for r in range(world + 1)]
         exch = DistExchange()
         order = (lambda p, e: locality_order(p, e)[0]) if model._use_reorder(x) else None
-        lay = RangeLayout(ei, bounds, rank, DistRequests(), pos=x, order_fn=order)
-        shard = FlowGNNShard(model, lay, x)
-        shard.setup(exch, [shard])
-        del ei
+        shard_box = [None]
+
+        def build_shard():
+            # the whole per-graph setup, as FlowGNN.forward does it at N = 1
+            # from edge_index: partition layout (ghost lists, interior-first
+            # locality order, request lists), rank-local CSR + GCN weights,
+            # ghost coordinates
+            lay = RangeLayout(ei, bounds, rank, DistRequests(), pos=x, order_fn=order)
+            sh = FlowGNNShard(model, lay, x)
+            sh.setup(exch, [sh])
+            shard_box[0] = sh
+
+        build_shard()
 
         def step():
             if model._csr.capacity <= 0:      # graph setup inside the step (see timed_loop)
-                shard.setup_graph(exch, [shard])
-            return sharded_forward([shard], exch, [x])[0]
+                build_shard()
+            return sharded_forward([shard_box[0]], exch, [x])[0]
 
     # ---- live per-launch timing of the dominant (GCN layer) kernel
+    from mignn import _lib
+    dev_errors = [0]
     launches = []   # (start_event, end_event, n_rows) of the headline loop
     launches32 = []  # the same in the exact-fp32 loop
     recording = [None]
@@ -233,10 +244,18 @@ def main():
             t1 = time.perf_counter()
             recording[0] = None
         el = t1 - t0
+        # in-kernel protocol failures during the timed steps (mignn_device_errors:
+        # a launch whose bounded LDS wait ran out wrote wrong rows) fail the run
+        dev_err = _lib.device_errors(clear=True)
         if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            t = torch.tensor([el, float(dev_err)], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = t.item()
+            el, dev_err = t[0].item(), int(t[1].item())
+        dev_errors[0] |= dev_err
+        if dev_err:
+            raise SystemExit(f"bench: device error word 0x{dev_err:x} after a timed loop "
+                             "(mignn_device_errors: an in-kernel bounded wait ran out): "
+                             "results invalid")
         return el
 
     progress(f"headline workload ready: {N_local} nodes, {E_local} edges per GPU")
@@ -306,7 +325,10 @@ def main():
         },
         "roofline": roofline,
         "exact_f32": exact,
+        "device_errors": dev_errors[0],
     }
+    if world == 1 and args.layer_type == "GCN" and H in (64, 128):
+        line["aggregate_alone"] = aggregate_roofline(model, x, H, args.steps)
     if world > 1:
         dist.barrier()
 
@@ -364,6 +386,49 @@ def time_layers(model, recording):
     def restore():
         model._layer = orig_layer
     return restore
+
+
+def aggregate_roofline(model, x, H, steps):
+    """SURVEY 8(d) target (i): the GCN aggregate kernel alone
+    (mignn_gcn_aggregate_planned: out = D^-1/2 (A + I) D^-1/2 x, fp32) over the
+    bench graph's CSR in the locality order (the model's cached CSR of the
+    graph-cached loop), HIP events on the launch stream; algorithmic bytes as
+    the layer's: read x and write the output once, the CSR arrays once."""
+    from mignn import _lib
+    csr = None
+    for c in model._csr.entries.values():
+        csr = c
+    if csr is None:
+        return None
+    n = csr.num_nodes
+    plan = csr.gcn_plan(H, 0, n)
+    X = torch.randn((n, H), device=x.device, generator=torch.Generator(device=x.device).manual_seed(3))
+    Y = torch.empty_like(X)
+    L = _lib.lib()
+    P = _lib.ptr
+    st = _lib.stream(x.device)
+
+    def run():
+        _lib.check(L.mignn_gcn_aggregate_planned(P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew),
+                                                 P(X), H, 0, n, H, P(Y), H, st),
+                   "mignn_gcn_aggregate_planned")
+    for _ in range(3):
+        run()
+    k = max(5, min(steps, 20))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(k):
+        run()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / k
+    nnz = int(csr.row_ptr[-1].item())
+    by = 4 * (2 * n * H + (n + 1) + nnz + n)
+    return {"kernel": "gcn_tile_kernel<%d, agg> (mignn_gcn_aggregate_planned)" % H,
+            "bound": "hbm", "achieved": round(by / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s", "frac": round(by / (ms * 1e-3) / HBM_PEAK, 4), "traffic": None,
+            "avg_launch_ms": round(ms, 4), "launches": k, "algorithmic_bytes_per_launch": by,
+            "H": H, "rows": n, "csr_entries": nnz}
 
 
 def gcn_roofline(launches, H, deg_plus_self, precision, traffic):

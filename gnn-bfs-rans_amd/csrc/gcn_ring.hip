@@ -78,7 +78,7 @@ struct RCfg {
     static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
     static constexpr int OFF_STG = OFF_AH;
     static constexpr int NQ = 2;                       // row quads per wave (8 rows)
-    static constexpr int UB = H == 128 ? 2 : 4;        // slots per LDS batch
+    static constexpr int UB = 4;                       // slots per LDS batch
     static constexpr int VPL = H / 64;
     static constexpr int WN = H / 16;                  // 16-column blocks
     static constexpr int WM = NW / WN;                 // row groups (1 or 2)
@@ -156,6 +156,29 @@ __device__ __forceinline__ void rdma(const void* src, uint32_t dst) {
         : "memory");
 }
 
+// a wave-uniform 64-bit address, in SGPRs
+__device__ __forceinline__ uint64_t runi(const void* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<int>(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// the same with an SGPR base address and a per-lane 32-bit offset (no
+// per-piece address arithmetic: the offsets are fixed per lane)
+__device__ __forceinline__ void rdma_s(const void* base, uint32_t voff, uint32_t dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(runi(base)), "s"(__builtin_amdgcn_readfirstlane(static_cast<int>(dst)))
+        : "memory");
+}
+
 __device__ __forceinline__ int rsplit_exp(uint32_t mbits) {
     const int eb = static_cast<int>((mbits >> 23) & 0xffu);
     return min(140 - eb, 50);
@@ -184,15 +207,26 @@ __device__ __attribute__((aligned(16))) float g_ring_zero_row[256];
 #ifdef MIGNN_DIAG
 __device__ unsigned long long* g_ring_trace = nullptr;
 #endif
-__device__ __forceinline__ void rstamp(int wave, int lane, int64_t s, int pt) {
-#ifdef MIGNN_DIAG
-    unsigned long long* tr = g_ring_trace;
-#else
-    constexpr unsigned long long* tr = nullptr;
-#endif
-    if (tr != nullptr && blockIdx.x < 8 && s < 64 && (wave == 0 || wave == 4) && lane == 0)
-        tr[((blockIdx.x * 64 + s) * 2 + (wave >> 2)) * 16 + pt] = __builtin_amdgcn_s_memtime();
-}
+// stamps of one step collect in lanes 0..7 of a VGPR pair (v_writelane: no
+// memory traffic); the previous step's are written by ONE store at the next
+// step's top, after its barrier
+struct RTrace {
+    unsigned long long* tr;   // null: tracing off (the product build)
+    uint32_t lo, hi;
+    int lane;
+    __device__ __forceinline__ void stamp(int pt) {
+        if (tr == nullptr) return;
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        lo = lane == pt ? static_cast<uint32_t>(t) : lo;
+        hi = lane == pt ? static_cast<uint32_t>(t >> 32) : hi;
+    }
+    __device__ __forceinline__ void flush(int wave, int lane, int64_t s) {
+        if (tr == nullptr || blockIdx.x >= 8 || s < 0 || s >= 64 || (wave != 0 && wave != 4)) return;
+        if (lane < 8)
+            tr[((blockIdx.x * 64 + s) * 2 + (wave >> 2)) * 16 + lane] =
+                (static_cast<unsigned long long>(hi) << 32) | lo;
+    }
+};
 
 // ------------------------------------------------------------------ plan
 // One 64-thread block per tile, a thread per row.  Ext slots are numbered in
@@ -214,7 +248,7 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
         const int64_t r = t0 + lr;
         const uint32_t nloc = static_cast<uint32_t>(re - t0 < 64 ? re - t0 : 64);
         const uint32_t xoff = ring_parity(t, ntiles, G) ? C::OFF_X1 : C::OFF_X0;
-        for (int i = lr; i < C::NW * C::XLW; i += 64) xl[i] = 0xffffffffu;
+        for (int i = lr; i < C::NW * C::XLW; i += 64) xl[i] = 0u;   // unused: row 0, never read
         int e0 = 0, deg = 0, next = 0;
         if (r < re) {
             e0 = row_ptr[r];
@@ -299,7 +333,12 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
 }
 
 // ---------------------------------------------------------------- layer
-template <int H>
+// MODE (timing ablations, mignn_diag_ring only; 0 in the product; every
+// variant keeps the DMA op counts): 1 ext rows from the zero row, 2 no
+// aggregation sums, 4 no MFMAs, 8 own rows DMA'd from the zero row
+// EPIF: the epilogue flags at compile time (15 = BIAS|RESIDUAL|AFFINE|RELU,
+// 11 = BIAS|RESIDUAL|RELU: FlowGNN with / without BatchNorm), -1: from `flags`
+template <int H, int MODE = 0, int EPIF = -1>
 __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     const unsigned char* __restrict__ plan, const int32_t* __restrict__ row_ptr,
     const int32_t* __restrict__ col, const float* __restrict__ ew, const float* __restrict__ x,
@@ -307,6 +346,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     const float* __restrict__ bias, const float* __restrict__ scale,
     const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
     using C = RCfg<H>;
+    if constexpr (EPIF >= 0) flags = EPIF;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
     _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
     _Float16* const AL = reinterpret_cast<_Float16*>(lds + C::OFF_AL);
@@ -323,6 +363,11 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     const int G = gridDim.x;
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, per_xcd = G >> 3;
     const int64_t nsteps = ring_steps(ntiles, G);
+#ifdef MIGNN_DIAG
+    RTrace rtr{(blockIdx.x < 8 && (wave == 0 || wave == 4)) ? g_ring_trace : nullptr, 0u, 0u, lane};
+#else
+    RTrace rtr{nullptr, 0u, 0u, lane};
+#endif
     auto tile_of = [&](int64_t s) -> int64_t { return (int64_t)xcd * nsteps * per_xcd + s * per_xcd + slot; };
     // a tile of this workgroup's schedule, or (past its end) tile 0: the DMA
     // op counts stay uniform, the loads are never read
@@ -337,44 +382,70 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     const uint32_t coff0 = static_cast<uint32_t>(c0 << 4);
 
     // ring DMA of step s: this wave's 8 records + its ext-list group (36
-    // lanes), then its share of the tile's own rows
-    auto dma_tile = [&](int64_t s) {
+    // lanes), then its share of the tile's own rows; SGPR bases, per-lane
+    // offsets fixed for the launch (a partial last tile clamps per lane)
+    const uint32_t ldxb = static_cast<uint32_t>(ldx) * 4u;
+    uint32_t xoff[C::NPX];
+#pragma unroll
+    for (int pp = 0; pp < C::NPX; ++pp) {
+        const int p = pp * C::NW + wave;
+        const int lr = p * C::RPP + lane / C::LPR;
+        const int pos = lane % C::LPR;
+        xoff[pp] = static_cast<uint32_t>(lr) * ldxb + 16u * static_cast<uint32_t>(pos ^ (lr & 7));
+    }
+    const uint32_t toff = lane < 32 ? static_cast<uint32_t>(wave * 512 + 16 * lane)
+                                    : static_cast<uint32_t>(C::BM * kRec + wave * (C::XLW * 4) + 16 * (lane - 32));
+    // piece q of step s's ring DMA: q = 0 the records, 1 .. NPX own rows
+    auto dma_tile_piece = [&](int64_t s, int q) {
         const int64_t tile = tile_or0(s);
         const int64_t t0 = row_begin + tile * C::BM;
         const int par = static_cast<int>(s & 1);
-        int l = lane;
-        asm volatile("" : "+v"(l));
-        const unsigned char* pb = plan + tile * C::TAB_BYTES;
-        const unsigned char* src = l < 32 ? pb + wave * 512 + 16 * l
-                                          : pb + C::BM * kRec + wave * (C::XLW * 4) + 16 * (l - 32);
-        if (l < 36) rdma(src, rlds(lds + C::OFF_TAB + par * C::TAB_BYTES + wave * 576));
+        if (q == 0) {
+            if (lane < 36)
+                rdma_s(plan + tile * C::TAB_BYTES, toff,
+                       rlds(lds + C::OFF_TAB + par * C::TAB_BYTES + wave * 576));
+            return;
+        }
+        const int pp = q - 1;
+        const int p = pp * C::NW + wave;
         unsigned char* const X = lds + (par ? C::OFF_X1 : C::OFF_X0);
-#pragma unroll
-        for (int pp = 0; pp < C::NPX; ++pp) {
-            const int p = pp * C::NW + wave;
+        if ((MODE & 8) == 0 && t0 + C::BM <= row_end) {
+            rdma_s(x + t0 * ldx, xoff[pp], rlds(X + p * 1024));
+        } else {
+            int l = lane;
+            asm volatile("" : "+v"(l));
             const int lr = p * C::RPP + l / C::LPR;
             const int pos = l % C::LPR;
             int64_t row = t0 + lr;
             if (row >= row_end) row = row_end - 1;
-            rdma(x + row * ldx + 4 * (pos ^ (lr & 7)), rlds(X + p * 1024));
+            rdma((MODE & 8) ? g_ring_zero_row + 4 * (pos & 31) : x + row * ldx + 4 * (pos ^ (lr & 7)),
+                 rlds(X + p * 1024));
         }
     };
-    // ext rows of step s (records in TAB slot s & 1): pieces of this wave's
-    // ext rows k = EPW wave .. +EPW (chunk c of row k at position c ^ (k & 7))
-    auto dma_ext = [&](int64_t s) {
+    auto dma_tile = [&](int64_t s) {
+#pragma unroll
+        for (int q = 0; q <= C::NPX; ++q) dma_tile_piece(s, q);
+    };
+    // ext rows of step s (records in TAB slot s & 1): piece i of this wave's
+    // ext rows k = EPW wave .. +EPW (chunk c of row k at position c ^ (k & 7));
+    // unused list entries hold column 0 (loaded, never read)
+    auto dma_ext_piece = [&](int64_t s, int i) {
         const unsigned char* const tab = lds + C::OFF_TAB + (s & 1) * C::TAB_BYTES + wave * 576 + 512;
         int l = lane;
         asm volatile("" : "+v"(l));
+        const int kk = i * C::RPP + l / C::LPR;          // within the wave's rows
+        const int k = wave * C::EPW + kk;
+        const int pos = l % C::LPR;
+        const uint32_t c = *reinterpret_cast<const uint32_t*>(tab + 4 * kk);
+        const unsigned char* src =
+            (MODE & 1) ? reinterpret_cast<const unsigned char*>(g_ring_zero_row + 4 * pos)
+                       : reinterpret_cast<const unsigned char*>(x) + static_cast<uint64_t>(c) * ldxb +
+                             16u * static_cast<uint32_t>(pos ^ (k & 7));
+        rdma(src, rlds(lds + C::OFF_EXT + (wave * C::EPW + i * C::RPP) * C::ROWB));
+    };
+    auto dma_ext = [&](int64_t s) {
 #pragma unroll
-        for (int i = 0; i < C::NPE; ++i) {
-            const int kk = i * C::RPP + l / C::LPR;          // within the wave's rows
-            const int k = wave * C::EPW + kk;
-            const int pos = l % C::LPR;
-            const uint32_t c = *reinterpret_cast<const uint32_t*>(tab + 4 * kk);
-            const float* src = c != 0xffffffffu ? x + static_cast<int64_t>(c) * ldx + 4 * (pos ^ (k & 7))
-                                                : g_ring_zero_row + 4 * pos;
-            rdma(src, rlds(lds + C::OFF_EXT + (wave * C::EPW + i * C::RPP) * C::ROWB));
-        }
+        for (int i = 0; i < C::NPE; ++i) dma_ext_piece(s, i);
     };
 
     // ------------------------------------------------------------ prologue
@@ -431,13 +502,14 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         const int par = static_cast<int>(s & 1);
         const unsigned char* const X = lds + (par ? C::OFF_X1 : C::OFF_X0);
         const unsigned char* const RW = REC + par * C::TAB_BYTES + wave * 576;   // my 8 records
-        rstamp(wave, lane, s, 0);
+        rtr.stamp(0);
         // (B0) this step's ext rows landed in every wave (and, older, its own
         //      rows and records): younger ops = the next tile's ring DMA and
         //      the last tile's row stores
         if (s == 0) rbar<rvm_l(C::NDMA)>();
         else rbar<rvm_l(C::NDMA + C::NST)>();
-        rstamp(wave, lane, s, 1);
+        rtr.flush(wave, lane, s - 1);
+        rtr.stamp(1);
         const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
             *reinterpret_cast<const int*>(RW + 512 + 4 * C::EPW)));
         const int maxdeg = static_cast<int>(summ & 0xffu);
@@ -452,7 +524,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             for (int j = 0; j < C::CH; ++j) acc[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (!slow && !far) {
 #pragma unroll 1
-            for (int u0 = 0; u0 < maxdeg; u0 += C::UB) {
+            for (int u0 = 0; u0 < ((MODE & 2) ? 0 : maxdeg); u0 += C::UB) {
                 uint4 rcd[C::NQ][C::UB / 2];
 #pragma unroll
                 for (int qd = 0; qd < C::NQ; ++qd)
@@ -507,7 +579,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                 }
             }
         }
-        rstamp(wave, lane, s, 2);
+        rtr.stamp(2);
         // (2) split into the A image (or the row-per-wave path for slow waves)
         if (!slow) {
 #pragma unroll
@@ -594,15 +666,14 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         }
         // (B1) A image complete; this step's own rows, records and ext rows read
         rbar<kRLgkm0>();
-        rstamp(wave, lane, s, 3);
+        rtr.stamp(3);
         // next step's ext rows (its records landed: younger than them = its
         // own rows and the last tile's stores), then step s+2's ring DMA into
         // the slot just freed
         if (s == 0) rwait<rvm(C::NPX)>();
         else rwait<rvm(C::NPX + C::NST)>();
-        dma_ext(s + 1);
-        dma_tile(s + 2);
-        rstamp(wave, lane, s, 4);
+        // (their NPE + NDMA pieces are issued between the MFMAs below)
+        rtr.stamp(4);
         // (3) transform: 16 output columns x my row blocks
         int pr[C::IBW];
         f32x4 accm[C::IBW];
@@ -624,17 +695,28 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             };
             f16x8r fh[2], fl[2];
             frag(0, fh[0], fl[0]);
+            // one DMA piece per MFMA step: step s+1's ext rows, then step
+            // s+2's ring DMA (the rest after the loop)
+            auto dma_piece = [&](int t) {
+                if (t < C::NPE) dma_ext_piece(s + 1, t);
+                else dma_tile_piece(s + 2, t - C::NPE);
+            };
+            constexpr int NPC = C::NPE + C::NDMA;
 #pragma unroll
             for (int t = 0; t < C::KC * C::IBW; ++t) {
                 const int kc = t / C::IBW, ib = t % C::IBW;
+                if (t < NPC) dma_piece(t);
+                if (MODE & 4) continue;
                 if (t + 1 < C::KC * C::IBW) frag(t + 1, fh[(t + 1) & 1], fl[(t + 1) & 1]);
                 accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fh[t & 1], accm[ib], 0, 0, 0);
                 accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fl[t & 1], accm[ib], 0, 0, 0);
                 accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[kc], fh[t & 1], accm[ib], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
+#pragma unroll
+            for (int t = C::KC * C::IBW; t < NPC; ++t) dma_piece(t);
         }
-        rstamp(wave, lane, s, 5);
+        rtr.stamp(5);
         // (B2) every wave done with the A image: stage there
         rbar<kRLgkm0>();
         {
@@ -656,7 +738,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                     f32x4{o[0], o[1], o[2], o[3]};
             }
         }
-        rstamp(wave, lane, s, 6);
+        rtr.stamp(6);
         // (B3) staged: my 8 rows out, whole rows
         rbar<kRLgkm0>();
         {
@@ -674,12 +756,38 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                     __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + 4 * ch));
             }
         }
-        rstamp(wave, lane, s, 7);
+        rtr.stamp(7);
     }
     rwait<rvm(0)>();   // no LDS-DMA may outlive the workgroup
-    rstamp(wave, lane, 63, 15);
+    rtr.flush(wave, lane, nsteps - 1);
 }
 
+template <int H, int MODE, int EPIF>
+void launch_ring_k(int G, hipStream_t st, const void* plan, const int32_t* row_ptr,
+                   const int32_t* col, const float* ew, const float* x, int64_t ldx, int64_t rb,
+                   int64_t re, const float* w, const float* bias, const float* scale,
+                   const float* shift, int flags, float* out, int64_t ldo) {
+    hipLaunchKernelGGL((gcn_ring_kernel<H, MODE, EPIF>), dim3(G), dim3(RCfg<H>::NT), 0, st,
+                       static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb, re, w,
+                       bias, scale, shift, flags, out, ldo);
+}
+
+template <int H, int MODE>
+void launch_ring_h(int G, hipStream_t st, const void* plan, const int32_t* row_ptr,
+                   const int32_t* col, const float* ew, const float* x, int64_t ldx, int64_t rb,
+                   int64_t re, const float* w, const float* bias, const float* scale,
+                   const float* shift, int flags, float* out, int64_t ldo) {
+    constexpr int kBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE | MIGNN_EPI_RELU;
+    constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
+    if (MODE == 0 && flags == kBN)
+        launch_ring_k<H, MODE, kBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+    else if (MODE == 0 && flags == kNoBN)
+        launch_ring_k<H, MODE, kNoBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+    else
+        launch_ring_k<H, MODE, -1>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+}
+
+template <int MODE = 0>
 int launch_ring(int h, const void* plan, const int32_t* row_ptr, const int32_t* col,
                 const float* ew, const float* x, int64_t ldx, int64_t rb, int64_t re,
                 const float* w, const float* bias, const float* scale, const float* shift,
@@ -688,13 +796,9 @@ int launch_ring(int h, const void* plan, const int32_t* row_ptr, const int32_t* 
     const int G = ring_grid(ntiles);
     MIGNN_REQUIRE(G > 0, "gcn_ring: device query failed");
     if (h == 128)
-        hipLaunchKernelGGL(gcn_ring_kernel<128>, dim3(G), dim3(RCfg<128>::NT), 0, st,
-                           static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb,
-                           re, w, bias, scale, shift, flags, out, ldo);
+        launch_ring_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
     else
-        hipLaunchKernelGGL(gcn_ring_kernel<64>, dim3(G), dim3(RCfg<64>::NT), 0, st,
-                           static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb,
-                           re, w, bias, scale, shift, flags, out, ldo);
+        launch_ring_h<64, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
     return launch_status("gcn_ring_kernel");
 }
 
@@ -756,5 +860,26 @@ extern "C" int mignn_gcn_layer_ring(const void* plan, const int32_t* row_ptr, co
 extern "C" int mignn_diag_ring_trace(void* buf) {
     MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ring_trace), &buf, sizeof(buf)));
     return MIGNN_OK;
+}
+#endif
+
+#ifdef MIGNN_DIAG
+extern "C" int mignn_diag_ring(int mode, const void* plan, const int32_t* row_ptr,
+                               const int32_t* col, const float* ew, const float* x, int64_t ldx,
+                               int64_t rb, int64_t re, int h, const float* w, const float* bias,
+                               const float* scale, const float* shift, int flags, float* out,
+                               int64_t ldo, void* stream) {
+    hipStream_t st = as_stream(stream);
+    switch (mode) {
+#define MIGNN_RING_MODE(M) \
+    case M: return launch_ring<M>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        MIGNN_RING_MODE(0) MIGNN_RING_MODE(1) MIGNN_RING_MODE(2) MIGNN_RING_MODE(3)
+        MIGNN_RING_MODE(4) MIGNN_RING_MODE(6) MIGNN_RING_MODE(7) MIGNN_RING_MODE(8)
+        MIGNN_RING_MODE(15)
+#undef MIGNN_RING_MODE
+        default: break;
+    }
+    set_error("diag_ring: unknown mode %d", mode);
+    return MIGNN_ERR_ARG;
 }
 #endif

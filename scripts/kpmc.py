@@ -1,0 +1,55 @@
+"""Short PMC target (round 4): the hot-kernel candidates on the bench mesh
+(250x200x200, locality order, H = KP_H), each launched KP_REPS times, nothing
+else -- run under `rocprofv3 --pmc ...` (scripts/gpu_kpmc.sh)."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "gnn-bfs-rans_amd"))
+import torch  # noqa: E402
+
+from mignn import _lib  # noqa: E402
+from mignn.gnn_model import build_csr, locality_order  # noqa: E402
+from mignn.synthetic import grid_graph  # noqa: E402
+
+dev = torch.device("cuda", 0)
+H = int(os.environ.get("KP_H", "128"))
+reps = int(os.environ.get("KP_REPS", "2"))
+kinds = os.environ.get("KP_KINDS", "pc,ring,planned,agg").split(",")
+pos, ei = grid_graph(250, 200, 200, device=dev)
+n = pos.shape[0]
+_, inv = locality_order(pos, ei)
+csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv)
+del ei
+L = _lib.lib()
+P = _lib.ptr
+st = _lib.stream()
+g = torch.Generator(device=dev).manual_seed(0)
+X = torch.randn(n, H, device=dev, generator=g)
+W = torch.randn(H, H, device=dev, generator=g) * 0.05
+b = torch.randn(H, device=dev, generator=g) * 0.05
+sc = torch.rand(H, device=dev, generator=g) + 0.5
+sh = torch.randn(H, device=dev, generator=g) * 0.1
+Y = torch.empty_like(X)
+nbr = L.mignn_gcn_ring_plan_bytes(0, n, H)
+rplan = torch.empty(nbr, dtype=torch.uint8, device=dev)
+_lib.check(L.mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(rplan), nbr, None, st), "rp")
+nb = L.mignn_gcn_plan_bytes(0, n)
+plan = torch.empty(nb, dtype=torch.uint8, device=dev)
+_lib.check(L.mignn_gcn_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(plan), nb, st), "p")
+for _ in range(reps):
+    if "pc" in kinds:
+        _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                           P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "pc")
+    if "ring" in kinds:
+        _lib.check(L.mignn_gcn_layer_ring(P(rplan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
+                                          0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "ring")
+    if "planned" in kinds:
+        _lib.check(L.mignn_gcn_layer_planned(P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
+                                             0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "tile")
+    if "agg" in kinds:
+        _lib.check(L.mignn_gcn_aggregate_planned(P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X),
+                                                 H, 0, n, H, P(Y), H, st), "agg")
+torch.cuda.synchronize()
+print("ok")

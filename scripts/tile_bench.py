@@ -98,6 +98,11 @@ for H in [int(v) for v in os.environ.get("TB_H", "128,64").split(",")]:
     res.setdefault("ring_plan_stats", {})[H] = stats.tolist()
     cases = {"plan": mk_plan, "planned": planned, "aggregate": agg, "pc_f16x3": pc,
              "ring_plan": mk_rplan, "ring": ring}
+    for m in [int(v) for v in os.environ.get("TB_RING_MODES", "").split(",") if v]:
+        def fr(m=m):
+            _lib.check(L.mignn_diag_ring(m, P(rplan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
+                                         0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y0), H, st), "dring")
+        cases[f"ring_mode{m}"] = fr
     if H == 128:
         for m in [int(v) for v in os.environ.get("TB_MODES", "").split(",") if v]:
             for a in (0, 1):
