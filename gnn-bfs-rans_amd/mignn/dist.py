@@ -323,6 +323,15 @@ class Shard:
 
     def layer(self, i: int, x: torch.Tensor, out: torch.Tensor, rb: int, re: int) -> None: ...
 
+    def halo_extra(self, i: int) -> Optional[torch.Tensor]:
+        """A second per-row tensor whose ghost rows travel with layer i's
+        feature halo (sharded GAT: the logits the previous layer's epilogue
+        formed), or None."""
+        return None
+
+    def end_layer(self, i: int) -> None:
+        """Layer i's rows are all written."""
+
     def before_halo(self, i: int, x: torch.Tensor) -> None:
         """Work of layer i that needs only owned rows (before the halo lands)."""
 
@@ -350,32 +359,49 @@ def sharded_forward(shards: List[Shard], exchange, xs_own: List[torch.Tensor]) -
     cur, nxt = bufs_a, bufs_b
     for i in range(first, shards[0].num_layers):
         h = exchange.start(shards, cur)
+        extra = [sh.halo_extra(i) for sh in shards]
+        h2 = exchange.start(shards, extra) if all(e is not None for e in extra) else None
         for sh, x, o in zip(shards, cur, nxt):
             sh.before_halo(i, x)
             sh.layer(i, x, o, 0, sh.layout.n_int)
         exchange.wait(h)
+        if h2 is not None:
+            exchange.wait(h2)
         for sh, x, o in zip(shards, cur, nxt):
             sh.after_halo(i, x)
             sh.layer(i, x, o, sh.layout.n_int, sh.layout.n_own)
+            sh.end_layer(i)
         cur, nxt = nxt, cur
     return [sh.output(x[:sh.layout.n_own]) for sh, x in zip(shards, cur)]
 
 
 class FlowGNNShard(Shard):
     """GPU shard: FlowGNN's native layers on the rank-local CSR (owned rows
-    in the interior/boundary locality order, then the ghosts)."""
+    in the interior/boundary locality order, then the ghosts).  The route is
+    the one FlowGNN.forward takes on one GPU: layer 0 composed with
+    input_proj from the coordinates (GCN, GIN H=256, GAT, TransformerConv:
+    FlowGNN._layer0_kind) with the ghost coordinates exchanged once per
+    layout, so layer 0 moves no feature halo; GAT layers form the next
+    layer's logits in their epilogue and the ghost rows' logits travel with
+    the feature halo (no logit GEMV)."""
 
     def __init__(self, model, layout: RangeLayout, x_own: torch.Tensor):
         self.model, self.layout = model, layout
         self.num_layers, self.hidden_dim = model.num_layers, model.hidden_dim
         self.x_own = x_own
-        self.logits = None
         self.csr = None
+        self.pos = None
+        self.kind0 = model._layer0_kind()
+        self.chain = (model.layer_type == "GAT" and model.precision == "f16x3"
+                      and model.gat_next_logits)
+        self.lg = None          # [n_total, 2 heads] logits of the layer about to run
+        self.lg_ready = False   # its owned rows written by the previous layer
+        self.lg_next = None
 
     def setup(self, exchange, shards: List["FlowGNNShard"]):
         """Per-graph setup of every shard in `shards` (collective over them):
         setup_graph (local CSRs, GCN ghost degrees + edge weights) and
-        setup_static (ghost cell centres for the fused GCN layer 0)."""
+        setup_static (ghost cell centres for the composed layer 0)."""
         self.setup_graph(exchange, shards)
         self.setup_static(exchange, shards)
 
@@ -398,11 +424,10 @@ class FlowGNNShard(Shard):
                 sh.csr.compute_gcn_weights(0, sh.layout.n_own)
 
     def setup_static(self, exchange, shards: List["FlowGNNShard"]):
-        """Static per-layout data: the ghost rows' cell centres (the fused
-        input_proj + GCN layer 0 reads coordinates, so layer 0 needs no
-        feature exchange)."""
+        """Static per-layout data: the ghost rows' cell centres (the composed
+        layer 0 reads coordinates, so layer 0 needs no feature exchange)."""
         m = self.model
-        if m._fuse_layer0():
+        if self.kind0 is not None:
             D = m.input_dim
             poss = []
             for sh in shards:
@@ -413,43 +438,62 @@ class FlowGNNShard(Shard):
             for sh, p in zip(shards, poss):
                 sh.pos = p
 
+    def _logits_buf(self):
+        return torch.empty((self.layout.n_total, 2 * _heads()), dtype=torch.float32,
+                           device=self.x_own.device)
+
     def first_layer(self, x_own, buf):
         m, lay = self.model, self.layout
-        if m._fuse_layer0():
-            from . import _lib
-            _lib.check(_lib.lib().mignn_gcn_layer0_coords(
-                _lib.ptr(self.csr.row_ptr), _lib.ptr(self.csr.col), _lib.ptr(self.csr.ew),
-                _lib.ptr(self.pos), self.pos.stride(0), m.input_dim, 0, lay.n_own,
-                _lib.ptr(m._layer0_coef()), m.hidden_dim, _lib.ptr(buf), buf.stride(0),
-                _lib.stream(buf.device)), "mignn_gcn_layer0_coords")
+        self.lg, self.lg_ready, self.lg_next = None, False, None
+        if self.kind0 is not None:
+            lg = None
+            if self.kind0 == "gat" and self.chain and self.num_layers > 1:
+                lg = self._logits_buf()
+            m._layer0(self.kind0, self.csr, self.pos, 0, lay.n_own, buf, logits_next=lg)
+            self.lg, self.lg_ready = lg, lg is not None
             return 1
         xo = x_own.contiguous().float()
         m._input_proj(xo, buf[:lay.n_own], rows=lay.perm.to(torch.int32))
         return 0
 
+    def halo_extra(self, i):
+        return self.lg if self.lg_ready else None
+
+    def _wlog(self, i):
+        layer = self.model.gnn_layers[i]
+        return self.model._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
+                                  lambda: self.model._gat_weights(layer))[0]
+
     def before_halo(self, i, x):
-        """GAT: the owned rows' logits, computed while the features move."""
-        if self.model.layer_type == "GAT":
+        """GAT without logits from the previous layer: the owned rows'
+        logits, computed while the features move."""
+        if self.model.layer_type == "GAT" and not self.lg_ready:
             from .gnn_model import linear
-            layer = self.model.gnn_layers[i]
-            wlog, _ = self.model._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
-                                         lambda: self.model._gat_weights(layer))
-            self.logits = torch.empty((self.layout.n_total, wlog.shape[0]), dtype=torch.float32,
-                                      device=x.device)
-            linear(x[:self.layout.n_own], wlog, out=self.logits[:self.layout.n_own])
+            self.lg = self._logits_buf()
+            linear(x[:self.layout.n_own], self._wlog(i), out=self.lg[:self.layout.n_own])
 
     def after_halo(self, i, x):
-        """GAT: the ghost rows' logits, from their rows that just landed."""
-        if self.model.layer_type == "GAT" and self.layout.n_ghost:
+        """GAT without exchanged logits: the ghost rows' logits, from their
+        rows that just landed."""
+        if self.model.layer_type == "GAT" and self.layout.n_ghost and not self.lg_ready:
             from .gnn_model import linear
-            layer = self.model.gnn_layers[i]
-            wlog, _ = self.model._cached("gat", i, (layer.lin.weight, layer.att_src, layer.att_dst),
-                                         lambda: self.model._gat_weights(layer))
-            linear(x[self.layout.n_own:], wlog, out=self.logits[self.layout.n_own:])
+            linear(x[self.layout.n_own:], self._wlog(i), out=self.lg[self.layout.n_own:])
 
     def layer(self, i, x, out, rb, re):
+        lg_next = None
+        if self.chain and i + 1 < self.num_layers:
+            if self.lg_next is None:
+                self.lg_next = self._logits_buf()
+            lg_next = self.lg_next
         self.model._layer(i, self.model.gnn_layers[i], self.csr, x, out, rb, re,
-                          logits=self.logits)
+                          logits=self.lg, logits_next=lg_next)
+
+    def end_layer(self, i):
+        if self.chain and i + 1 < self.num_layers:
+            self.lg, self.lg_next = self.lg_next, self.lg
+            self.lg_ready = True
+        else:
+            self.lg_ready = False
 
     def output(self, x_own):
         m = self.model
@@ -460,3 +504,8 @@ class FlowGNNShard(Shard):
         m._output_mlp(x_own, tmp, out, rows=self.layout.perm.to(torch.int32),
                       inv=self.layout.inv.to(torch.int32))
         return out
+
+
+def _heads() -> int:
+    from .gnn_model import HEADS
+    return HEADS

@@ -467,34 +467,11 @@ class FlowGNN(nn.Module):
         csr = self._csr.get(edge_index, num_nodes, mode, pos)
         cur, nxt = buf_a, buf_b
         first = 0
-        if self._fuse_layer0():
-            # input_proj + GCN layer 0 from the coordinates (mignn_gcn_layer0_coords)
+        kind = self._layer0_kind(edge_attr)
+        if kind is not None:
+            # input_proj composed into layer 0, from the coordinates
             try:
-                self._gcn_layer0(xin, csr, cur)
-            except RuntimeError as e:
-                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
-            first = 1
-        elif self._fuse_tf_layer0(edge_attr):
-            # input_proj + TransformerConv layer 0 from the coordinates
-            try:
-                self._tf_layer0(xin, csr, cur)
-            except RuntimeError as e:
-                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
-            first = 1
-        elif self._fuse_gat_layer0():
-            # input_proj + GAT layer 0 from the coordinates
-            try:
-                if self.gat_coords:
-                    self._gat_layer0(xin, csr, cur)   # collapsed (mignn_gat_layer0_coords)
-                else:
-                    self._gat_layer0_mfma(xin, csr, cur)   # mignn_gat_layer0_fused
-            except RuntimeError as e:
-                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
-            first = 1
-        elif self._fuse_gin_layer0():
-            # input_proj + GIN layer 0 at H = 256 from the coordinates (mignn_gin_layer0_fused)
-            try:
-                self._gin_layer0(xin, csr, cur)
+                self._layer0(kind, csr, self._coords(xin, csr), 0, num_nodes, cur)
             except RuntimeError as e:
                 raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
             first = 1
@@ -653,6 +630,43 @@ class FlowGNN(nn.Module):
             f"  x shape: {x.shape}, edge_attr shape: "
             f"{edge_attr.shape if edge_attr is not None else 'None'}")
 
+    def _layer0_kind(self, edge_attr=None) -> Optional[str]:
+        """The composition of input_proj into layer 0 that runs from the
+        node coordinates (no [N, H] input_proj output, no layer-0 halo when
+        sharded), or None: input_proj writes [N, H] and layer 0 runs as the
+        others.  gcn: mignn_gcn_layer0_coords; transformer:
+        mignn_transformer_layer0_coords; gat: mignn_gat_layer0_coords
+        (collapsed to 3-vectors), gat_mfma: mignn_gat_layer0_fused; gin (H =
+        256): mignn_gin_layer0_fused."""
+        if self._fuse_layer0():
+            return "gcn"
+        if self._fuse_tf_layer0(edge_attr):
+            return "transformer"
+        if self._fuse_gat_layer0():
+            return "gat" if self.gat_coords else "gat_mfma"
+        if self._fuse_gin_layer0():
+            return "gin"
+        return None
+
+    def _layer0(self, kind: str, csr: Csr, pos: torch.Tensor, rb: int, re: int, out,
+                logits_next=None):
+        """Layer 0 (input_proj composed in) for rows [rb, re) of the CSR from
+        pos [rows, input_dim] (coordinates of every row the CSR references, in
+        its node order).  logits_next (kind gat only): also the next GAT
+        layer's logits of the rows, from the same kernel."""
+        if kind == "gcn":
+            self._gcn_layer0(csr, pos, rb, re, out)
+        elif kind == "transformer":
+            self._tf_layer0(csr, pos, rb, re, out)
+        elif kind == "gat":
+            self._gat_layer0(csr, pos, rb, re, out, logits_next)
+        elif kind == "gat_mfma":
+            self._gat_layer0_mfma(csr, pos, rb, re, out)
+        elif kind == "gin":
+            self._gin_layer0(csr, pos, rb, re, out)
+        else:
+            raise ValueError(f"unknown layer-0 composition {kind!r}")
+
     def _fuse_layer0(self) -> bool:
         return (self.fuse_layer0 and self.layer_type == "GCN"
                 and self.num_layers > 0 and 1 <= self.input_dim <= 4
@@ -710,14 +724,13 @@ class FlowGNN(nn.Module):
             return T.float().contiguous(), gt.float().contiguous()
         return self._cached("tf0", 0, ts, make)
 
-    def _tf_layer0(self, x, csr: Csr, out):
+    def _tf_layer0(self, csr: Csr, pos, rb, re, out):
         T, gt = self._tf_layer0_tables()
-        pos = self._coords(x, csr)
         P = _lib.ptr
         _lib.check(_lib.lib().mignn_transformer_layer0_coords(
-            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), self.input_dim, 0, x.shape[0],
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), self.input_dim, rb, re,
             self.hidden_dim, HEADS, 1.0 / math.sqrt(self.hidden_dim), P(T), P(gt), 1, P(out),
-            out.stride(0), _stream(x)), "mignn_transformer_layer0_coords")
+            out.stride(0), _stream(pos)), "mignn_transformer_layer0_coords")
 
     def _fuse_gat_layer0(self) -> bool:
         # (the MFMA form, gat_coords off, has kernels for H in {64, 128} only;
@@ -727,7 +740,7 @@ class FlowGNN(nn.Module):
                 and (self.hidden_dim in (64, 128) or (self.hidden_dim == 256 and self.gat_coords))
                 and self.precision == "f16x3")
 
-    def _gat_layer0(self, x, csr: Csr, out):
+    def _gat_layer0(self, csr: Csr, pos, rb, re, out, logits_next=None):
         """input_proj + GAT layer 0 + residual + BN + ReLU collapsed to
         3-vectors (mignn_gat_layer0_coords): logits through lw = [wlog W_in |
         wlog b_in], per head P = sum alpha pos_j and S = sum alpha, output
@@ -769,14 +782,18 @@ class FlowGNN(nn.Module):
             T = torch.cat([A.permute(1, 0, 2).reshape(C, 3 * heads), e.t(), B, dd[:, None]], 1)
             return T.float().contiguous(), lw.float().contiguous()
         T, lw = self._cached("gat0c", 0, ts, make)
-        pos = self._coords(x, csr)
+        wlog_n = None
+        if logits_next is not None:
+            nl = self.gnn_layers[1]
+            wlog_n, _ = self._cached("gat", 1, (nl.lin.weight, nl.att_src, nl.att_dst),
+                                     lambda: self._gat_weights(nl))
         P = _lib.ptr
         _lib.check(_lib.lib().mignn_gat_layer0_coords(
-            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, 0, x.shape[0], H, HEADS,
-            float(layer.negative_slope), P(T), P(lw), 1, P(out), out.stride(0), None, None,
-            _stream(x)), "mignn_gat_layer0_coords")
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, rb, re, H, HEADS,
+            float(layer.negative_slope), P(T), P(lw), 1, P(out), out.stride(0), P(wlog_n),
+            P(logits_next), _stream(pos)), "mignn_gat_layer0_coords")
 
-    def _gat_layer0_mfma(self, x, csr: Csr, out):
+    def _gat_layer0_mfma(self, csr: Csr, pos, rb, re, out):
         """input_proj + GAT layer 0 + residual + BN + ReLU in one kernel: logits
         through [wlog W_in | wlog b_in], per head P = sum alpha pos_j and S =
         sum alpha, weighted sums W_in P + S b_in (fp64-composed weights)."""
@@ -801,12 +818,11 @@ class FlowGNN(nn.Module):
         img = self._img("w_gat", 0, (layer.lin.weight,), wcat)
         scale, shift = self._bn(0)
         epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
-        pos = self._coords(x, csr)
         P = _lib.ptr
         _lib.check(_lib.lib().mignn_gat_layer0_fused(
-            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, 0, x.shape[0], H,
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), D, rb, re, H,
             float(layer.negative_slope), P(self.input_proj.weight), P(self.input_proj.bias), P(lw),
-            P(img), P(layer.bias), P(scale), P(shift), epi, P(out), out.stride(0), _stream(x)),
+            P(img), P(layer.bias), P(scale), P(shift), epi, P(out), out.stride(0), _stream(pos)),
             "mignn_gat_layer0_fused")
 
     def _fuse_gin_layer0(self) -> bool:
@@ -814,7 +830,7 @@ class FlowGNN(nn.Module):
                 and self.num_layers > 0 and 1 <= self.input_dim <= 3 and self.hidden_dim == 256
                 and self._fused256())
 
-    def _gin_layer0(self, x, csr: Csr, out):
+    def _gin_layer0(self, csr: Csr, pos, rb, re, out):
         """input_proj + GIN layer 0 + residual + BN + ReLU in one kernel:
         a_i = W_in (sum_j pos_j + (1+eps) pos_i) + (deg_i + 1 + eps) b_in."""
         layer = self.gnn_layers[0]
@@ -824,12 +840,11 @@ class FlowGNN(nn.Module):
         img2 = self._cached("w_gin2p", 0, (nn2.weight,), lambda: gin_fused_image(nn2.weight))
         scale, shift = self._bn(0)
         epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
-        pos = self._coords(x, csr)
         P = _lib.ptr
         _lib.check(_lib.lib().mignn_gin_layer0_fused(
-            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), self.input_dim, 0, x.shape[0],
+            P(csr.row_ptr), P(csr.col), P(pos), pos.stride(0), self.input_dim, rb, re,
             256, eps, P(self.input_proj.weight), P(self.input_proj.bias), P(img1), P(nn0.bias),
-            P(img2), P(nn2.bias), P(scale), P(shift), epi, P(out), out.stride(0), _stream(x)),
+            P(img2), P(nn2.bias), P(scale), P(shift), epi, P(out), out.stride(0), _stream(pos)),
             "mignn_gin_layer0_fused")
 
     def _layer0_coef(self):
@@ -869,13 +884,11 @@ class FlowGNN(nn.Module):
             _stream(x)), "mignn_rows_gather")
         return pos
 
-    def _gcn_layer0(self, x, csr: Csr, out):
-        D = self.input_dim
-        pos = self._coords(x, csr)
+    def _gcn_layer0(self, csr: Csr, pos, rb, re, out):
         _lib.check(_lib.lib().mignn_gcn_layer0_coords(
             _lib.ptr(csr.row_ptr), _lib.ptr(csr.col), _lib.ptr(csr.ew), _lib.ptr(pos),
-            pos.stride(0), D, 0, x.shape[0], _lib.ptr(self._layer0_coef()), self.hidden_dim,
-            _lib.ptr(out), out.stride(0), _stream(x)), "mignn_gcn_layer0_coords")
+            pos.stride(0), self.input_dim, rb, re, _lib.ptr(self._layer0_coef()), self.hidden_dim,
+            _lib.ptr(out), out.stride(0), _stream(pos)), "mignn_gcn_layer0_coords")
 
     def _use_reorder(self, x) -> bool:
         if self.reorder not in ("auto", "0", "1"):

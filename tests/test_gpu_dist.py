@@ -1,7 +1,9 @@
 """The sharded forward on the GPU without a second GPU: P = 2 and 4 shards of
 one graph in one process, each a FlowGNNShard (the native layers on its
-rank-local CSR, owned rows in the interior/boundary locality order, fused
-GCN layer 0 from exchanged ghost coordinates), the halo filled by
+rank-local CSR, owned rows in the interior/boundary locality order, layer 0
+composed with input_proj from exchanged ghost coordinates for GCN, GAT, GIN
+H=256 and TransformerConv, GAT logits from the previous layer's epilogue
+with their ghost rows in the halo), the halo filled by
 device-to-device row copies through the same sharded_forward code the
 multi-process RCCL path runs.  Must equal the unsharded forward up to fp32
 summation order, for all four layer types, on k-slabs (natural order) and on
@@ -45,9 +47,10 @@ def _sharded(model, x, ei, P, ordered=True):
 
 
 @pytest.mark.parametrize("shuffle", [None, 2])
-@pytest.mark.parametrize("P", [2, 4])
-@pytest.mark.parametrize("lt,H", [("GCN", 128), ("GCN", 64), ("GAT", 64), ("GIN", 64),
-                                  ("Transformer", 64)])
+@pytest.mark.parametrize("P", [2, 4, 8])
+@pytest.mark.parametrize("lt,H", [("GCN", 128), ("GCN", 64), ("GAT", 64), ("GAT", 128),
+                                  ("GAT", 256), ("GIN", 64), ("GIN", 256), ("Transformer", 64),
+                                  ("Transformer", 256)])
 def test_sharded_matches_unsharded(lt, H, P, shuffle):
     cfg = dict(hidden_dim=H, num_layers=3, layer_type=lt)
     m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
@@ -70,6 +73,39 @@ def test_sharded_matches_unsharded(lt, H, P, shuffle):
         assert all(l.n_ghost == 2 * plane for l in lays)      # k-slabs: two halo planes
     assert err <= 2e-6 * scale
     assert e64 <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("lt,H,kind", [("GCN", 128, "gcn"), ("GAT", 128, "gat"),
+                                       ("GAT", 256, "gat"), ("GIN", 256, "gin"),
+                                       ("Transformer", 128, "transformer")])
+def test_sharded_route_matches_one_gpu(lt, H, kind, monkeypatch):
+    """The shards take FlowGNN.forward's route: layer 0 composed from the
+    coordinates (the kind the 1-GPU forward runs), and sharded GAT forms
+    every later layer's logits in the previous layer's epilogue, their ghost
+    rows travelling with the halo -- no logit GEMV (mignn.gnn_model.linear)
+    is launched."""
+    import mignn.gnn_model as gm
+    cfg = dict(hidden_dim=H, num_layers=3, layer_type=lt)
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=8))
+    m = m.to(DEV).eval()
+    assert m._layer0_kind() == kind
+    x, ei = grid_graph(24, 20, 16, device=DEV)
+    with torch.no_grad():
+        y = m(x, ei)
+    calls = []
+    real = gm.linear
+
+    def counting(*a, **k):
+        calls.append(a[0].shape)
+        return real(*a, **k)
+    monkeypatch.setattr(gm, "linear", counting)
+    ys, lays = _sharded(m, x, ei, 4)
+    assert all(l.n_ghost > 0 for l in lays)
+    if lt == "GAT":
+        assert calls == [], f"logit GEMVs in the sharded GAT forward: {calls}"
+    scale = max(1.0, y.abs().max().item())
+    assert (ys - y).abs().max().item() <= 2e-6 * scale
 
 
 def test_sharded_single_shard_is_plain_forward():
