@@ -335,7 +335,9 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
 // ---------------------------------------------------------------- layer
 // MODE (timing ablations, mignn_diag_ring only; 0 in the product; every
 // variant keeps the DMA op counts): 1 ext rows from the zero row, 2 no
-// aggregation sums, 4 no MFMAs, 8 own rows DMA'd from the zero row
+// aggregation sums, 4 no MFMAs, 8 own rows DMA'd from the zero row; 16 the
+// epilogue stored straight from the accumulators (no staging, 2 barriers per
+// step instead of 4)
 // EPIF: the epilogue flags at compile time (15 = BIAS|RESIDUAL|AFFINE|RELU,
 // 11 = BIAS|RESIDUAL|RELU: FlowGNN with / without BatchNorm), -1: from `flags`
 template <int H, int MODE = 0, int EPIF = -1>
@@ -717,6 +719,31 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             for (int t = C::KC * C::IBW; t < NPC; ++t) dma_piece(t);
         }
         rtr.stamp(5);
+        if constexpr ((MODE & 16) != 0) {
+            // epilogue straight from the accumulators: lane (rr, gg) holds
+            // row lr's columns n0 + 4 gg .. + 3 -- one 16-B store per row block
+            // (16 rows x 64 B per instruction; no staging, no barrier)
+            static_assert(C::NST == C::IBW, "direct stores keep the per-step store count");
+            const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 4 * gg]);
+            const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + n0 + 4 * gg]);
+#pragma unroll
+            for (int ib = 0; ib < C::IBW; ++ib) {
+                f32x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = ldexpf(accm[ib][r], -(pr[ib] + qw));
+                    if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
+                    if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
+                    o[r] = v;
+                }
+                const int lr = (wm * C::IBW + ib) * 16 + rr;
+                if (t0 + lr < row_end)
+                    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + n0 + 4 * gg));
+            }
+            rtr.stamp(6);
+            rtr.stamp(7);
+            continue;
+        }
         // (B2) every wave done with the A image: stage there
         rbar<kRLgkm0>();
         {
@@ -875,7 +902,8 @@ extern "C" int mignn_diag_ring(int mode, const void* plan, const int32_t* row_pt
     case M: return launch_ring<M>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
         MIGNN_RING_MODE(0) MIGNN_RING_MODE(1) MIGNN_RING_MODE(2) MIGNN_RING_MODE(3)
         MIGNN_RING_MODE(4) MIGNN_RING_MODE(6) MIGNN_RING_MODE(7) MIGNN_RING_MODE(8)
-        MIGNN_RING_MODE(15)
+        MIGNN_RING_MODE(15) MIGNN_RING_MODE(16) MIGNN_RING_MODE(17) MIGNN_RING_MODE(18)
+        MIGNN_RING_MODE(20)
 #undef MIGNN_RING_MODE
         default: break;
     }

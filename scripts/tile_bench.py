@@ -118,6 +118,16 @@ for H in [int(v) for v in os.environ.get("TB_H", "128,64").split(",")]:
     planned()
     pc()
     torch.cuda.synchronize()
+    # variants that keep the arithmetic (mode 16: direct-store epilogue) must
+    # write the product ring kernel's bits
+    for m in [int(v) for v in os.environ.get("TB_RING_MODES", "").split(",") if v]:
+        if m & 15 == 0:
+            ring()
+            cases[f"ring_mode{m}"]()
+            torch.cuda.synchronize()
+            res.setdefault("ring_mode_bitwise_equal", {})[f"{H}_{m}"] = bool(torch.equal(Y0, Yr))
+    pc()
+    torch.cuda.synchronize()
     diff = (Y - Y0).abs().max().item()
     res.setdefault("ring_vs_pc_max_diff", {})[H] = (Yr - Y0).abs().max().item()
     same = (Y == Y0).all(1).float().mean().item()
