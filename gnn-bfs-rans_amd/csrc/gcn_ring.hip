@@ -348,6 +348,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     const float* __restrict__ bias, const float* __restrict__ scale,
     const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
     using C = RCfg<H>;
+    constexpr bool AGG = (MODE & 32) != 0;   // aggregate only (mignn_gcn_aggregate_ring)
     if constexpr (EPIF >= 0) flags = EPIF;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
     _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
@@ -456,8 +457,8 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     const int wn = wave % C::WN, wm = wave / C::WN;
     const int n0 = 16 * wn;
     f16x8r wh[C::KC], wl[C::KC];
-    int qw;
-    {
+    int qw = 0;
+    if constexpr (!AGG) {
         float wv[C::KC][8];
         uint32_t m = 0;
 #pragma unroll
@@ -481,7 +482,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                 wl[kc][j] = static_cast<_Float16>(s - static_cast<float>(h));
             }
     }
-    if (wm == 0 && lane < 16) {
+    if (!AGG && wm == 0 && lane < 16) {
         const int n = n0 + lane;
         EPI[n] = (flags & MIGNN_EPI_BIAS) ? bias[n] : 0.f;
         EPI[H + n] = (flags & MIGNN_EPI_AFFINE) ? scale[n] : 1.f;
@@ -517,6 +518,31 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         const int maxdeg = static_cast<int>(summ & 0xffu);
         const bool far = ((summ >> 8) & 1u) != 0u;
         const bool slow = (summ >> 16) != 0u;
+        // row-per-wave sum of local row 8 wave + q (lane: VPL consecutive
+        // columns), CSR order: the path of waves holding a hub row
+        auto slow_row = [&](int q, float (&a)[C::VPL]) {
+            const int loff = lane * (4 * C::VPL);
+            const int64_t row = t0 + 8 * wave + q;
+#pragma unroll
+            for (int k = 0; k < C::VPL; ++k) a[k] = 0.f;
+            if (row < row_end) {
+                const int e_begin = __builtin_amdgcn_readfirstlane(row_ptr[row]);
+                const int e_end = __builtin_amdgcn_readfirstlane(row_ptr[row + 1]);
+#pragma unroll 1
+                for (int e = e_begin; e < e_end; ++e) {
+                    const int c = __builtin_amdgcn_readfirstlane(col[e]);
+                    const float w = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ew[e])));
+                    const uint32_t off = static_cast<uint32_t>(static_cast<int64_t>(c) - t0);
+                    float vv[C::VPL];
+                    if (static_cast<int64_t>(c) >= t0 && off < nloc)
+                        ldv<C::VPL>(reinterpret_cast<const float*>(X + (off * C::ROWB + (static_cast<uint32_t>(loff) ^ ((off & 7u) << 4)))), vv);
+                    else
+                        ldv<C::VPL>(reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(x + (int64_t)c * ldx) + loff), vv);
+#pragma unroll
+                    for (int k = 0; k < C::VPL; ++k) a[k] = fmaf(w, vv[k], a[k]);
+                }
+            }
+        };
 
         // (1) aggregate my 8 rows in CSR order
         f32x4 acc[C::NQ][C::CH];
@@ -582,6 +608,43 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             }
         }
         rtr.stamp(2);
+        if constexpr (AGG) {
+            // aggregate only: the fp32 sums are the output.  Slow waves sum
+            // row by row and come back to the lane layout through their own
+            // rows of the (unused) A image
+            if (slow) {
+                unsigned char* const stg = lds + C::OFF_AH + 8 * wave * C::ROWB;
+#pragma unroll 1
+                for (int q = 0; q < 8; ++q) {
+                    float a[C::VPL];
+                    slow_row(q, a);
+#pragma unroll
+                    for (int k = 0; k < C::VPL; ++k)
+                        reinterpret_cast<float*>(stg + q * C::ROWB)[C::VPL * lane + k] = a[k];
+                }
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j)
+                        acc[qd][j] = *reinterpret_cast<const f32x4*>(stg + (4 * qd + gq) * C::ROWB + 16 * (c0 + 16 * j));
+            }
+            // (B1) every wave done with this step's rows
+            rbar<kRLgkm0>();
+            if (s == 0) rwait<rvm(C::NPX)>();
+            else rwait<rvm(C::NPX + C::NST)>();
+            dma_ext(s + 1);
+            dma_tile(s + 2);
+            static_assert(C::NQ * C::CH == C::NST, "aggregate stores keep the per-step store count");
+#pragma unroll
+            for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                for (int j = 0; j < C::CH; ++j) {
+                    const int lrow = 8 * wave + 4 * qd + gq;
+                    if (t0 + lrow < row_end)
+                        __builtin_nontemporal_store(acc[qd][j], reinterpret_cast<f32x4*>(out + (t0 + lrow) * ldo + 4 * (c0 + 16 * j)));
+                }
+            continue;
+        }
         // (2) split into the A image (or the row-per-wave path for slow waves)
         if (!slow) {
 #pragma unroll
@@ -612,30 +675,10 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                 if (iq == 0) REXP[lrow] = p;
             }
         } else {
-            const int loff = lane * (4 * C::VPL);
 #pragma unroll 1
             for (int q = 0; q < 8; ++q) {
-                const int64_t row = t0 + 8 * wave + q;
                 float a[C::VPL];
-#pragma unroll
-                for (int k = 0; k < C::VPL; ++k) a[k] = 0.f;
-                if (row < row_end) {
-                    const int e_begin = __builtin_amdgcn_readfirstlane(row_ptr[row]);
-                    const int e_end = __builtin_amdgcn_readfirstlane(row_ptr[row + 1]);
-#pragma unroll 1
-                    for (int e = e_begin; e < e_end; ++e) {
-                        const int c = __builtin_amdgcn_readfirstlane(col[e]);
-                        const float w = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ew[e])));
-                        const uint32_t off = static_cast<uint32_t>(static_cast<int64_t>(c) - t0);
-                        float vv[C::VPL];
-                        if (static_cast<int64_t>(c) >= t0 && off < nloc)
-                            ldv<C::VPL>(reinterpret_cast<const float*>(X + (off * C::ROWB + (static_cast<uint32_t>(loff) ^ ((off & 7u) << 4)))), vv);
-                        else
-                            ldv<C::VPL>(reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(x + (int64_t)c * ldx) + loff), vv);
-#pragma unroll
-                        for (int k = 0; k < C::VPL; ++k) a[k] = fmaf(w, vv[k], a[k]);
-                    }
-                }
+                slow_row(q, a);
                 uint32_t m = __float_as_uint(fabsf(a[0]));
                 if constexpr (C::VPL == 2) m = max(m, __float_as_uint(fabsf(a[1])));
                 const int p = rsplit_exp(rwave_max(m));
@@ -881,6 +924,22 @@ extern "C" int mignn_gcn_layer_ring(const void* plan, const int32_t* row_ptr, co
     if (re == rb) return MIGNN_OK;
     return launch_ring(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out,
                        ldo, as_stream(stream));
+}
+
+extern "C" int mignn_gcn_aggregate_ring(const void* plan, const int32_t* row_ptr,
+                                        const int32_t* col, const float* ew, const float* x,
+                                        int64_t ldx, int64_t rb, int64_t re, int h, float* out,
+                                        int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(plan && row_ptr && col && ew && x && out, "gcn_aggregate_ring: null pointer");
+    MIGNN_REQUIRE(h == 64 || h == 128, "gcn_aggregate_ring: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(aligned16(x) && aligned16(out) && aligned16(plan), "gcn_aggregate_ring: unaligned");
+    MIGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && ldx >= h && ldo >= h,
+                  "gcn_aggregate_ring: bad strides");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_aggregate_ring: bad row range");
+    MIGNN_REQUIRE(x != out, "gcn_aggregate_ring: in-place not supported (neighbours read x)");
+    if (re == rb) return MIGNN_OK;
+    return launch_ring<32>(h, plan, row_ptr, col, ew, x, ldx, rb, re, nullptr, nullptr, nullptr,
+                           nullptr, 0, out, ldo, as_stream(stream));
 }
 
 #ifdef MIGNN_DIAG

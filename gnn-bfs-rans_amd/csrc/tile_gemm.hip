@@ -167,7 +167,6 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
         auto gather = [&](int64_t tile, const WaveIdx& ix, float* A, float* Rt) {
             int lane_ = lane;
             asm volatile("" : "+v"(lane_));   // keep lane-derived offsets out of LICM
-            const int c = lane_ % C::LPR, grp = lane_ / C::LPR;
             const int64_t r0 = first_row(tile);
             if constexpr (MODE == ROWS) {
                 constexpr int CH = PROWS * C::LPR;
@@ -195,7 +194,6 @@ __global__ __launch_bounds__(NTHREADS, 4) void fused_tile_kernel(
                 // and VPL fmas per lane.  All PROWS x 8 loads are issued before
                 // the first fma.
                 constexpr int VPL = C::VPL;
-                const int safe_row = static_cast<int>(row_end - 1);   // valid x row
                 int rp[PROWS + 1];
 #pragma unroll
                 for (int q = 0; q <= PROWS; ++q) rp[q] = __builtin_amdgcn_readlane(ix.rpv, q);

@@ -75,6 +75,8 @@ SIGNATURES = {
     "mignn_gcn_ring_plan": (c_int, [_P, _P, _P, c_int64, c_int64, c_int, _P, c_size_t, _P, _P]),
     "mignn_gcn_layer_ring": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                      _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_aggregate_ring": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int,
+                                         _P, c_int64, _P]),
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
     "mignn_mlp_head_prep": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int, c_int, _P, c_size_t,
                                     _P]),

@@ -320,6 +320,11 @@ int mignn_gcn_layer_ring(const void* plan, const int32_t* row_ptr, const int32_t
                          int64_t row_end, int h, const float* w, const float* bias,
                          const float* scale, const float* shift, int flags, float* out,
                          int64_t ldo, void* stream);
+/* The GCN aggregation alone by the ring kernel (mignn_gcn_ring_plan's plan
+ * for the same h): out_i = sum_e ew_e x_{col e} in CSR order, fp32. */
+int mignn_gcn_aggregate_ring(const void* plan, const int32_t* row_ptr, const int32_t* col,
+                             const float* ew, const float* x, int64_t ldx, int64_t row_begin,
+                             int64_t row_end, int h, float* out, int64_t ldo, void* stream);
 /* The GCN aggregation alone over the plan: out_i = sum_e ew_e x_{col e}
  * (= mignn_gcn_aggregate's D^-1/2 (A + I) D^-1/2 x with ew from dinv), fp32;
  * the SURVEY 8(d) "aggregate kernel alone" of the north-star target. */

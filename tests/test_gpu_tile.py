@@ -257,6 +257,22 @@ def test_gcn_layer_ring(H, case):
         assert torch.isnan(out[:, H:]).all()
         d = (out[rb:re, :H] - old[rb:re, :H]).abs().max().item()
         assert d < 2e-6, (rb, re, d)
+        # the aggregate alone by the ring kernel: fp32 sums in CSR order
+        agg = torch.full((n, ld), float("nan"), device=DEV)
+        _lib.check(L.mignn_gcn_aggregate_ring(
+            P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), ld, rb, re, H, P(agg), ld,
+            _lib.stream()), "gcn_aggregate_ring")
+        rp = csr.row_ptr.long().cpu()
+        cl, ew, Xd = csr.col.long().cpu(), csr.ew.cpu().double(), X.cpu().double()
+        rows = torch.unique(torch.cat([torch.arange(rb, min(re, rb + 70)),
+                                       torch.randint(rb, re, (500,), generator=g)]))
+        aref = torch.stack([(ew[rp[r]:rp[r + 1], None] * Xd[cl[rp[r]:rp[r + 1]]]).sum(0)
+                            for r in rows.tolist()])
+        ag = agg[:, :H].cpu().double()
+        assert (ag[rows] - aref).abs().max().item() < 2e-6 * max(1.0, aref.abs().max().item())
+        assert torch.isnan(ag[:rb]).all() and torch.isnan(ag[re:]).all()
+        assert not torch.isnan(ag[rb:re]).any()
+        assert torch.isnan(agg[:, H:]).all()
         st = stats.tolist()
         if case == "shuffled":
             assert st[1] > 0          # far entries exercised
