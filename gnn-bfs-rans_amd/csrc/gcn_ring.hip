@@ -337,7 +337,9 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
 // variant keeps the DMA op counts): 1 ext rows from the zero row, 2 no
 // aggregation sums, 4 no MFMAs, 8 own rows DMA'd from the zero row; 16 the
 // epilogue stored straight from the accumulators (no staging, 2 barriers per
-// step instead of 4)
+// step instead of 4); 64 two 16-column blocks per wave (each A fragment feeds
+// both: half the A-image LDS reads); 32 aggregate only (product:
+// mignn_gcn_aggregate_ring)
 // EPIF: the epilogue flags at compile time (15 = BIAS|RESIDUAL|AFFINE|RELU,
 // 11 = BIAS|RESIDUAL|RELU: FlowGNN with / without BatchNorm), -1: from `flags`
 template <int H, int MODE = 0, int EPIF = -1>
@@ -454,16 +456,24 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     // ------------------------------------------------------------ prologue
     for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
     const int rr = lane & 15, gg = lane >> 4;
-    const int wn = wave % C::WN, wm = wave / C::WN;
-    const int n0 = 16 * wn;
-    f16x8r wh[C::KC], wl[C::KC];
-    int qw = 0;
-    if constexpr (!AGG) {
+    // the transform's wave grid: CPW 16-column blocks x IBW 16-row blocks per
+    // wave (CPW = 2: every A fragment read from LDS feeds both column blocks)
+    constexpr int CPW = (MODE & 64) ? 2 : 1;
+    constexpr int WN = H / (16 * CPW), WM = C::NW / WN, IBW = (C::BM / 16) / WM;
+    static_assert(WN * WM == C::NW && IBW * WM * 16 == C::BM, "ring transform grid");
+    const int wn = wave % WN, wm = wave / WN;
+    const int n0 = 16 * CPW * wn;                 // column block cb: n0 + 16 cb
+    f16x8r wh[CPW][C::KC], wl[CPW][C::KC];
+    int qw[CPW];
+#pragma unroll
+    for (int cb = 0; cb < CPW; ++cb) {
+        qw[cb] = 0;
+        if constexpr (AGG) continue;
         float wv[C::KC][8];
         uint32_t m = 0;
 #pragma unroll
         for (int kc = 0; kc < C::KC; ++kc) {
-            const float* p = W + (int64_t)(n0 + rr) * H + 32 * kc + 8 * gg;
+            const float* p = W + (int64_t)(n0 + 16 * cb + rr) * H + 32 * kc + 8 * gg;
             const float4 a = ld4(p), b = ld4(p + 4);
             float* w8 = wv[kc];
             w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
@@ -471,18 +481,18 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
 #pragma unroll
             for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(w8[j])));
         }
-        qw = rsplit_exp(rwave_max(m));    // one exponent per wave's 16 columns
+        qw[cb] = rsplit_exp(rwave_max(m));    // one exponent per 16-column block
 #pragma unroll
         for (int kc = 0; kc < C::KC; ++kc)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float s = ldexpf(wv[kc][j], qw);
+                const float s = ldexpf(wv[kc][j], qw[cb]);
                 const _Float16 h = static_cast<_Float16>(s);
-                wh[kc][j] = h;
-                wl[kc][j] = static_cast<_Float16>(s - static_cast<float>(h));
+                wh[cb][kc][j] = h;
+                wl[cb][kc][j] = static_cast<_Float16>(s - static_cast<float>(h));
             }
     }
-    if (!AGG && wm == 0 && lane < 16) {
+    if (!AGG && wm == 0 && lane < 16 * CPW) {
         const int n = n0 + lane;
         EPI[n] = (flags & MIGNN_EPI_BIAS) ? bias[n] : 0.f;
         EPI[H + n] = (flags & MIGNN_EPI_AFFINE) ? scale[n] : 1.f;
@@ -695,18 +705,20 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         }
         // residual + bias of my output block (rows of my row group, my 16
         // columns), before the ring slot is refilled
-        f32x4 seed[C::IBW];
-        {
-            const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[n0 + 4 * gg]);
+        f32x4 seed[CPW][IBW];
 #pragma unroll
-            for (int ib = 0; ib < C::IBW; ++ib) {
-                const int lr = (wm * C::IBW + ib) * 16 + rr;
+        for (int cb = 0; cb < CPW; ++cb) {
+            const int nb = n0 + 16 * cb;
+            const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[nb + 4 * gg]);
+#pragma unroll
+            for (int ib = 0; ib < IBW; ++ib) {
+                const int lr = (wm * IBW + ib) * 16 + rr;
                 float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (has_res) {
-                    const int ch = (n0 >> 2) + gg;
+                    const int ch = (nb >> 2) + gg;
                     rv = *reinterpret_cast<const float4*>(X + lr * C::ROWB + ((ch ^ (lr & 7)) << 4));
                 }
-                seed[ib] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
+                seed[cb][ib] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
             }
         }
         // (B1) A image complete; this step's own rows, records and ext rows read
@@ -720,21 +732,23 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         // (their NPE + NDMA pieces are issued between the MFMAs below)
         rtr.stamp(4);
         // (3) transform: 16 output columns x my row blocks
-        int pr[C::IBW];
-        f32x4 accm[C::IBW];
+        int pr[IBW];
+        f32x4 accm[CPW][IBW];
 #pragma unroll
-        for (int ib = 0; ib < C::IBW; ++ib) {
-            pr[ib] = REXP[(wm * C::IBW + ib) * 16 + rr];
+        for (int ib = 0; ib < IBW; ++ib) {
+            pr[ib] = REXP[(wm * IBW + ib) * 16 + rr];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) accm[ib][r] = ldexpf(seed[ib][r], pr[ib] + qw);
+            for (int cb = 0; cb < CPW; ++cb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) accm[cb][ib][r] = ldexpf(seed[cb][ib][r], pr[ib] + qw[cb]);
         }
         {
-            int fb = (wm * C::IBW * 16 + rr) * C::AS + 8 * gg;
+            int fb = (wm * IBW * 16 + rr) * C::AS + 8 * gg;
             asm volatile("" : "+v"(fb));
             const _Float16* const AHb = AH + fb;
             const _Float16* const ALb = AL + fb;
             auto frag = [&](int t, f16x8r& bh, f16x8r& bl) {
-                const int kc = t / C::IBW, ib = t % C::IBW;
+                const int kc = t / IBW, ib = t % IBW;
                 bh = *reinterpret_cast<const f16x8r*>(&AHb[ib * 16 * C::AS + 32 * kc]);
                 bl = *reinterpret_cast<const f16x8r*>(&ALb[ib * 16 * C::AS + 32 * kc]);
             };
@@ -748,40 +762,47 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             };
             constexpr int NPC = C::NPE + C::NDMA;
 #pragma unroll
-            for (int t = 0; t < C::KC * C::IBW; ++t) {
-                const int kc = t / C::IBW, ib = t % C::IBW;
+            for (int t = 0; t < C::KC * IBW; ++t) {
+                const int kc = t / IBW, ib = t % IBW;
                 if (t < NPC) dma_piece(t);
                 if (MODE & 4) continue;
-                if (t + 1 < C::KC * C::IBW) frag(t + 1, fh[(t + 1) & 1], fl[(t + 1) & 1]);
-                accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fh[t & 1], accm[ib], 0, 0, 0);
-                accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fl[t & 1], accm[ib], 0, 0, 0);
-                accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[kc], fh[t & 1], accm[ib], 0, 0, 0);
+                if (t + 1 < C::KC * IBW) frag(t + 1, fh[(t + 1) & 1], fl[(t + 1) & 1]);
+#pragma unroll
+                for (int cb = 0; cb < CPW; ++cb) {
+                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], fh[t & 1], accm[cb][ib], 0, 0, 0);
+                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], fl[t & 1], accm[cb][ib], 0, 0, 0);
+                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cb][kc], fh[t & 1], accm[cb][ib], 0, 0, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int t = C::KC * C::IBW; t < NPC; ++t) dma_piece(t);
+            for (int t = C::KC * IBW; t < NPC; ++t) dma_piece(t);
         }
         rtr.stamp(5);
         if constexpr ((MODE & 16) != 0) {
             // epilogue straight from the accumulators: lane (rr, gg) holds
             // row lr's columns n0 + 4 gg .. + 3 -- one 16-B store per row block
             // (16 rows x 64 B per instruction; no staging, no barrier)
-            static_assert(C::NST == C::IBW, "direct stores keep the per-step store count");
-            const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 4 * gg]);
-            const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + n0 + 4 * gg]);
+            static_assert(C::NST == CPW * IBW, "direct stores keep the per-step store count");
 #pragma unroll
-            for (int ib = 0; ib < C::IBW; ++ib) {
-                f32x4 o;
+            for (int cb = 0; cb < CPW; ++cb) {
+                const int nb = n0 + 16 * cb;
+                const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + nb + 4 * gg]);
+                const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + nb + 4 * gg]);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = ldexpf(accm[ib][r], -(pr[ib] + qw));
-                    if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                    if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
-                    o[r] = v;
+                for (int ib = 0; ib < IBW; ++ib) {
+                    f32x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = ldexpf(accm[cb][ib][r], -(pr[ib] + qw[cb]));
+                        if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
+                        if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
+                        o[r] = v;
+                    }
+                    const int lr = (wm * IBW + ib) * 16 + rr;
+                    if (t0 + lr < row_end)
+                        __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + nb + 4 * gg));
                 }
-                const int lr = (wm * C::IBW + ib) * 16 + rr;
-                if (t0 + lr < row_end)
-                    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (t0 + lr) * ldo + n0 + 4 * gg));
             }
             rtr.stamp(6);
             rtr.stamp(7);
@@ -789,21 +810,23 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         }
         // (B2) every wave done with the A image: stage there
         rbar<kRLgkm0>();
-        {
-            const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 4 * gg]);
-            const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + n0 + 4 * gg]);
 #pragma unroll
-            for (int ib = 0; ib < C::IBW; ++ib) {
+        for (int cb = 0; cb < CPW; ++cb) {
+            const int nb = n0 + 16 * cb;
+            const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + nb + 4 * gg]);
+            const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + nb + 4 * gg]);
+#pragma unroll
+            for (int ib = 0; ib < IBW; ++ib) {
                 float o[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float v = ldexpf(accm[ib][r], -(pr[ib] + qw));
+                    float v = ldexpf(accm[cb][ib][r], -(pr[ib] + qw[cb]));
                     if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
                     if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
                     o[r] = v;
                 }
-                const int lr = (wm * C::IBW + ib) * 16 + rr;
-                const int ch = (n0 >> 2) + gg;
+                const int lr = (wm * IBW + ib) * 16 + rr;
+                const int ch = (nb >> 2) + gg;
                 *reinterpret_cast<f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4)) =
                     f32x4{o[0], o[1], o[2], o[3]};
             }
@@ -962,7 +985,7 @@ extern "C" int mignn_diag_ring(int mode, const void* plan, const int32_t* row_pt
         MIGNN_RING_MODE(0) MIGNN_RING_MODE(1) MIGNN_RING_MODE(2) MIGNN_RING_MODE(3)
         MIGNN_RING_MODE(4) MIGNN_RING_MODE(6) MIGNN_RING_MODE(7) MIGNN_RING_MODE(8)
         MIGNN_RING_MODE(15) MIGNN_RING_MODE(16) MIGNN_RING_MODE(17) MIGNN_RING_MODE(18)
-        MIGNN_RING_MODE(20)
+        MIGNN_RING_MODE(20) MIGNN_RING_MODE(64) MIGNN_RING_MODE(80)
 #undef MIGNN_RING_MODE
         default: break;
     }
