@@ -52,6 +52,9 @@ from ._lib import (CSR_ONE_SELF_LOOP, CSR_TRANSPOSE, CSR_VERBATIM, EPI_AFFINE, E
                    EPI_RESIDUAL)
 
 HEADS = 4  # gnn_model.py:67, :79
+# the split-fp16 GCN layer kernel of FlowGNN.gcn_kernel = "auto", per hidden
+# width: the fastest measured on the bench mesh
+GCN_KERNEL_AUTO = {64: "tile", 128: "pc"}
 
 
 # ---------------------------------------------------------------------------
@@ -136,13 +139,30 @@ class Csr:
         self.ew = ew
         self.perm = self.inv = self.pos = None
         self.key_tensor = None   # the caller's edge_index the cache key was made from
-        self.plans: Dict[Tuple[int, int, int], torch.Tensor] = {}
+        self.plans: Dict[Tuple[str, int, int, int], torch.Tensor] = {}
+
+    def ring_plan(self, h: int, row_begin: int, row_end: int) -> torch.Tensor:
+        """The ring kernel's plan of rows [row_begin, row_end) for hidden
+        width h (mignn_gcn_ring_plan: per-tile records, ext-row lists and the
+        schedule of this device), built on first use and kept with the CSR."""
+        key = ("ring", h, row_begin, row_end)
+        plan = self.plans.get(key)
+        if plan is None:
+            L = _lib.lib()
+            nb = L.mignn_gcn_ring_plan_bytes(row_begin, row_end, h)
+            plan = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.col.device)
+            _lib.check(L.mignn_gcn_ring_plan(_lib.ptr(self.row_ptr), _lib.ptr(self.col),
+                                             _lib.ptr(self.ew), row_begin, row_end, h,
+                                             _lib.ptr(plan), nb, None,
+                                             _lib.stream(self.col.device)), "mignn_gcn_ring_plan")
+            self.plans[key] = plan
+        return plan
 
     def gcn_plan(self, h: int, row_begin: int, row_end: int) -> torch.Tensor:
         """The tile plan of rows [row_begin, row_end) for hidden width h
         (mignn_gcn_plan), built on first use and kept with the CSR (it copies
         the ew weights: rebuilt after compute_gcn_weights)."""
-        key = (h, row_begin, row_end)
+        key = ("tile", h, row_begin, row_end)
         plan = self.plans.get(key)
         if plan is None:
             L = _lib.lib()
@@ -408,12 +428,14 @@ class FlowGNN(nn.Module):
         # nodes with 3-D cell-centre features), "1" always, "0" never
         self.reorder = os.environ.get("MIGNN_REORDER", "auto")
         # split-fp16 GCN layer kernel at H in {64, 128}: "tile" (the tile-plan
-        # kernel, csrc/gcn_tile.hip), "pc" (the producer / consumer kernel,
-        # csrc/gcn_f16x3.hip) or "auto" (the faster one measured per H: tile at
-        # H = 64, pc at H = 128); read once here, not per forward
+        # kernel, csrc/gcn_tile.hip), "ring" (the persistent ring kernel,
+        # csrc/gcn_ring.hip), "pc" (the producer / consumer kernel,
+        # csrc/gcn_f16x3.hip) or "auto" (the fastest measured per H,
+        # GCN_KERNEL_AUTO); read once here, not per forward
         self.gcn_kernel = os.environ.get("MIGNN_GCN_KERNEL", "auto")
-        if self.gcn_kernel not in ("tile", "pc", "auto"):
-            raise ValueError(f"MIGNN_GCN_KERNEL must be auto, tile or pc, got {self.gcn_kernel!r}")
+        if self.gcn_kernel not in ("tile", "ring", "pc", "auto"):
+            raise ValueError(
+                f"MIGNN_GCN_KERNEL must be auto, tile, ring or pc, got {self.gcn_kernel!r}")
         # kernel-route switches (A/B studies; the defaults are the measured
         # fastest routes), read once at construction -- plain attributes after
         # that, never environment lookups inside forward:
@@ -465,6 +487,7 @@ class FlowGNN(nn.Module):
         mode = CSR_ONE_SELF_LOOP if self.layer_type in ("GCN", "GAT") else CSR_VERBATIM
         pos = xin if self._use_reorder(xin) else None
         csr = self._csr.get(edge_index, num_nodes, mode, pos)
+        self._prepare_plans(csr, 0, num_nodes)
         cur, nxt = buf_a, buf_b
         first = 0
         kind = self._layer0_kind(edge_attr)
@@ -890,6 +913,21 @@ class FlowGNN(nn.Module):
             pos.stride(0), self.input_dim, rb, re, _lib.ptr(self._layer0_coef()), self.hidden_dim,
             _lib.ptr(out), out.stride(0), _stream(pos)), "mignn_gcn_layer0_coords")
 
+    def _gcn_kernel(self, H: int) -> str:
+        return self.gcn_kernel if self.gcn_kernel != "auto" else GCN_KERNEL_AUTO.get(H, "pc")
+
+    def _prepare_plans(self, csr: "Csr", row_begin: int, row_end: int):
+        """Build the per-graph plan of the GCN layer kernel before the layer
+        loop (part of the graph setup, with the CSR; not inside a layer)."""
+        H = self.hidden_dim
+        if self.layer_type != "GCN" or H not in (64, 128) or self.precision != "f16x3":
+            return
+        kern = self._gcn_kernel(H)
+        if kern == "ring":
+            csr.ring_plan(H, row_begin, row_end)
+        elif kern == "tile":
+            csr.gcn_plan(H, row_begin, row_end)
+
     def _use_reorder(self, x) -> bool:
         if self.reorder not in ("auto", "0", "1"):
             raise ValueError(f"MIGNN_REORDER must be auto, 0 or 1, got {self.reorder!r}")
@@ -971,8 +1009,15 @@ class FlowGNN(nn.Module):
             return
         if self.layer_type == "GCN":
             w, b = layer.lin.weight, layer.bias
-            kern = self.gcn_kernel if self.gcn_kernel != "auto" else ("tile" if H == 64 else "pc")
-            if H in (64, 128) and self.precision == "f16x3" and kern == "tile":
+            kern = self._gcn_kernel(H)
+            if H in (64, 128) and self.precision == "f16x3" and kern == "ring":
+                # the hot kernel: persistent ring over the CSR's ring plan
+                plan = csr.ring_plan(H, rb, re)
+                _lib.check(L.mignn_gcn_layer_ring(
+                    P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
+                    P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),
+                    "mignn_gcn_layer_ring")
+            elif H in (64, 128) and self.precision == "f16x3" and kern == "tile":
                 # the hot kernel: split-fp16 GCN layer over the CSR's tile plan
                 plan = csr.gcn_plan(H, rb, re)
                 _lib.check(L.mignn_gcn_layer_planned(

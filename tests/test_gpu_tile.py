@@ -278,3 +278,35 @@ def test_gcn_layer_ring(H, case):
             assert st[1] > 0          # far entries exercised
         if case == "hub" and rb <= 5 < re:
             assert st[2] > 0          # a row-per-wave wave exercised
+
+
+@pytest.mark.parametrize("H", [64, 128])
+@pytest.mark.parametrize("reorder", ["0", "1"])
+def test_model_gcn_kernel_routes_agree(H, reorder):
+    """FlowGNN with each split-fp16 GCN layer kernel (ring, tile, pc): the
+    same model output up to fp32 summation order, and within the fp64
+    oracle's tolerance; the plan is built with the CSR (before the layers)."""
+    from mignn import FlowGNN
+    from mignn.synthetic import seeded_state_dict
+    from oracle import flowgnn_oracle as orc
+    cfg = dict(hidden_dim=H, num_layers=4, layer_type="GCN")
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    sd = seeded_state_dict(m.state_dict(), seed=5)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    m.reorder = reorder
+    x, ei = grid_graph(36, 28, 20, device=DEV, permute_seed=3)
+    ys = {}
+    for kern in ("pc", "tile", "ring"):
+        m.gcn_kernel = kern
+        m._csr.entries.clear()
+        with torch.no_grad():
+            ys[kern] = m(x, ei)
+        csr = next(iter(m._csr.entries.values()))
+        kinds = {k[0] for k in csr.plans}
+        assert kinds == ({"ring"} if kern == "ring" else {"tile"} if kern == "tile" else set())
+    scale = max(1.0, ys["pc"].abs().max().item())
+    for kern in ("tile", "ring"):
+        assert (ys[kern] - ys["pc"]).abs().max().item() <= 2e-6 * scale, kern
+    ref = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
+    assert (ys["ring"].cpu().double() - ref).abs().max().item() <= 1e-5 * scale
