@@ -65,12 +65,17 @@ struct RCfg {
     static constexpr int EPW = KX / NW;                // ext rows DMA'd per wave (12)
     static constexpr int TAB_BYTES = BM * kRec + NW * XLW * 4;   // records + ext list (4608)
     static constexpr int A_BYTES = BM * AS * 2;
-    // LDS: X[2] | EXT | TAB[2] | zero row | AH | AL | REXP | EPI
+    // E2 (where LDS allows): the ext rows double-buffered and DMA'd a whole
+    // step ahead (at the top of the previous step), the records 3 steps ahead
+    static constexpr bool E2 = H == 64;
+    static constexpr int NE = E2 ? 2 : 1;              // ext areas
+    static constexpr int NTB = E2 ? 3 : 2;             // record (TAB) slots
+    // LDS: X[2] | EXT[NE] | TAB[NTB] | zero row | AH | AL | REXP | EPI
     static constexpr int OFF_X0 = 0;
     static constexpr int OFF_X1 = X_BYTES;
     static constexpr int OFF_EXT = 2 * X_BYTES;
-    static constexpr int OFF_TAB = OFF_EXT + EXT_BYTES;
-    static constexpr int OFF_ZERO = OFF_TAB + 2 * TAB_BYTES;
+    static constexpr int OFF_TAB = OFF_EXT + NE * EXT_BYTES;
+    static constexpr int OFF_ZERO = OFF_TAB + NTB * TAB_BYTES;
     static constexpr int OFF_AH = OFF_ZERO + ROWB;
     static constexpr int OFF_AL = OFF_AH + A_BYTES;
     static constexpr int OFF_REXP = OFF_AL + A_BYTES;
@@ -93,7 +98,7 @@ struct RCfg {
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     static_assert(BM * ROWB <= 2 * A_BYTES, "staging tile fits the A image");
     static_assert(EPW == NPE * RPP && EPW <= 12, "ext rows per wave");
-    static_assert(OFF_EXT + EXT_BYTES <= (1 << 17), "codes below bit 17");
+    static_assert(OFF_EXT + NE * EXT_BYTES <= (1 << 17), "codes below bit 17");
 };
 
 // the launch grid of the ring kernel and the step parity of each tile under
@@ -247,7 +252,9 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
         const int64_t t0 = rb + t * 64;
         const int64_t r = t0 + lr;
         const uint32_t nloc = static_cast<uint32_t>(re - t0 < 64 ? re - t0 : 64);
-        const uint32_t xoff = ring_parity(t, ntiles, G) ? C::OFF_X1 : C::OFF_X0;
+        const int tpar = ring_parity(t, ntiles, G);
+        const uint32_t xoff = tpar ? C::OFF_X1 : C::OFF_X0;
+        const uint32_t eoff = C::OFF_EXT + (C::E2 && tpar ? C::EXT_BYTES : 0);
         for (int i = lr; i < C::NW * C::XLW; i += 64) xl[i] = 0u;   // unused: row 0, never read
         int e0 = 0, deg = 0, next = 0;
         if (r < re) {
@@ -286,7 +293,7 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
                     const uint32_t off = static_cast<uint32_t>(c - t0);
                     code = (xoff + off * C::ROWB) | ((off & 7u) << 4);
                 } else if (k < C::KX) {
-                    code = (C::OFF_EXT + k * C::ROWB) | ((static_cast<uint32_t>(k) & 7u) << 4);
+                    code = (eoff + k * C::ROWB) | ((static_cast<uint32_t>(k) & 7u) << 4);
                     xl[(k / C::EPW) * C::XLW + k % C::EPW] = static_cast<uint32_t>(c);
                     ++k;
                 } else {
@@ -400,17 +407,24 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     }
     const uint32_t toff = lane < 32 ? static_cast<uint32_t>(wave * 512 + 16 * lane)
                                     : static_cast<uint32_t>(C::BM * kRec + wave * (C::XLW * 4) + 16 * (lane - 32));
-    // piece q of step s's ring DMA: q = 0 the records, 1 .. NPX own rows
+    // the record slot of step s
+    auto tslot = [&](int64_t s) -> int { return C::E2 ? static_cast<int>(s % 3) : static_cast<int>(s & 1); };
+    auto dma_tab = [&](int64_t s) {
+        const int64_t tile = tile_or0(s);
+        if (lane < 36)
+            rdma_s(plan + tile * C::TAB_BYTES, toff,
+                   rlds(lds + C::OFF_TAB + tslot(s) * C::TAB_BYTES + wave * 576));
+    };
+    // piece q of step s's ring DMA: q = 0 the records (E2: those of step
+    // s + 1), 1 .. NPX own rows
     auto dma_tile_piece = [&](int64_t s, int q) {
+        if (q == 0) {
+            dma_tab(C::E2 ? s + 1 : s);
+            return;
+        }
         const int64_t tile = tile_or0(s);
         const int64_t t0 = row_begin + tile * C::BM;
         const int par = static_cast<int>(s & 1);
-        if (q == 0) {
-            if (lane < 36)
-                rdma_s(plan + tile * C::TAB_BYTES, toff,
-                       rlds(lds + C::OFF_TAB + par * C::TAB_BYTES + wave * 576));
-            return;
-        }
         const int pp = q - 1;
         const int p = pp * C::NW + wave;
         unsigned char* const X = lds + (par ? C::OFF_X1 : C::OFF_X0);
@@ -431,11 +445,11 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
 #pragma unroll
         for (int q = 0; q <= C::NPX; ++q) dma_tile_piece(s, q);
     };
-    // ext rows of step s (records in TAB slot s & 1): piece i of this wave's
+    // ext rows of step s (its records' ext list): piece i of this wave's
     // ext rows k = EPW wave .. +EPW (chunk c of row k at position c ^ (k & 7));
     // unused list entries hold column 0 (loaded, never read)
     auto dma_ext_piece = [&](int64_t s, int i) {
-        const unsigned char* const tab = lds + C::OFF_TAB + (s & 1) * C::TAB_BYTES + wave * 576 + 512;
+        const unsigned char* const tab = lds + C::OFF_TAB + tslot(s) * C::TAB_BYTES + wave * 576 + 512;
         int l = lane;
         asm volatile("" : "+v"(l));
         const int kk = i * C::RPP + l / C::LPR;          // within the wave's rows
@@ -446,7 +460,8 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             (MODE & 1) ? reinterpret_cast<const unsigned char*>(g_ring_zero_row + 4 * pos)
                        : reinterpret_cast<const unsigned char*>(x) + static_cast<uint64_t>(c) * ldxb +
                              16u * static_cast<uint32_t>(pos ^ (k & 7));
-        rdma(src, rlds(lds + C::OFF_EXT + (wave * C::EPW + i * C::RPP) * C::ROWB));
+        rdma(src, rlds(lds + C::OFF_EXT + (C::E2 && (s & 1) ? C::EXT_BYTES : 0) +
+                       (wave * C::EPW + i * C::RPP) * C::ROWB));
     };
     auto dma_ext = [&](int64_t s) {
 #pragma unroll
@@ -500,10 +515,18 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     }
     const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
 
-    dma_tile(0);
-    rbar<rvm_l(0)>();                 // step 0's records and rows (all waves), zero row, EPI
-    dma_ext(0);
-    dma_tile(1);
+    if constexpr (C::E2) {
+        dma_tab(0);
+        dma_tile(0);                  // records of step 1, rows of step 0
+        dma_tile(1);                  // records of step 2, rows of step 1
+        rbar<rvm_l(0)>();             // (all waves), zero row, EPI
+        dma_ext(0);
+    } else {
+        dma_tile(0);
+        rbar<rvm_l(0)>();             // step 0's records and rows (all waves), zero row, EPI
+        dma_ext(0);
+        dma_tile(1);
+    }
 
     unsigned char* const REC = lds + C::OFF_TAB;      // + parity * TAB_BYTES + wave * 576
     for (int64_t s = 0; s < nsteps; ++s) {
@@ -514,13 +537,15 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         const uint32_t nloc = static_cast<uint32_t>(rem < C::BM ? rem : C::BM);
         const int par = static_cast<int>(s & 1);
         const unsigned char* const X = lds + (par ? C::OFF_X1 : C::OFF_X0);
-        const unsigned char* const RW = REC + par * C::TAB_BYTES + wave * 576;   // my 8 records
+        const unsigned char* const RW = REC + tslot(s) * C::TAB_BYTES + wave * 576;   // my 8 records
         rtr.stamp(0);
         // (B0) this step's ext rows landed in every wave (and, older, its own
         //      rows and records): younger ops = the next tile's ring DMA and
         //      the last tile's row stores
-        if (s == 0) rbar<rvm_l(C::NDMA)>();
+        // (E2: older than these ext rows are the records of step s + 1 too)
+        if (s == 0) rbar<rvm_l(C::E2 ? 0 : C::NDMA)>();
         else rbar<rvm_l(C::NDMA + C::NST)>();
+        if constexpr (C::E2) dma_ext(s + 1);     // into the ext area step s - 1 used
         rtr.flush(wave, lane, s - 1);
         rtr.stamp(1);
         const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
@@ -640,9 +665,11 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             }
             // (B1) every wave done with this step's rows
             rbar<kRLgkm0>();
-            if (s == 0) rwait<rvm(C::NPX)>();
-            else rwait<rvm(C::NPX + C::NST)>();
-            dma_ext(s + 1);
+            if constexpr (!C::E2) {
+                if (s == 0) rwait<rvm(C::NPX)>();
+                else rwait<rvm(C::NPX + C::NST)>();
+                dma_ext(s + 1);
+            }
             dma_tile(s + 2);
             static_assert(C::NQ * C::CH == C::NST, "aggregate stores keep the per-step store count");
 #pragma unroll
@@ -727,9 +754,12 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         // next step's ext rows (its records landed: younger than them = its
         // own rows and the last tile's stores), then step s+2's ring DMA into
         // the slot just freed
-        if (s == 0) rwait<rvm(C::NPX)>();
-        else rwait<rvm(C::NPX + C::NST)>();
-        // (their NPE + NDMA pieces are issued between the MFMAs below)
+        if constexpr (!C::E2) {
+            if (s == 0) rwait<rvm(C::NPX)>();
+            else rwait<rvm(C::NPX + C::NST)>();
+        }
+        // (their NPE + NDMA pieces -- E2: the NDMA -- are issued between the
+        // MFMAs below)
         rtr.stamp(4);
         // (3) transform: 16 output columns x my row blocks
         int pr[IBW];
@@ -756,11 +786,12 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             frag(0, fh[0], fl[0]);
             // one DMA piece per MFMA step: step s+1's ext rows, then step
             // s+2's ring DMA (the rest after the loop)
+            constexpr int NPE1 = C::E2 ? 0 : C::NPE;
             auto dma_piece = [&](int t) {
-                if (t < C::NPE) dma_ext_piece(s + 1, t);
-                else dma_tile_piece(s + 2, t - C::NPE);
+                if (t < NPE1) dma_ext_piece(s + 1, t);
+                else dma_tile_piece(s + 2, t - NPE1);
             };
-            constexpr int NPC = C::NPE + C::NDMA;
+            constexpr int NPC = NPE1 + C::NDMA;
 #pragma unroll
             for (int t = 0; t < C::KC * IBW; ++t) {
                 const int kc = t / IBW, ib = t % IBW;
@@ -986,6 +1017,7 @@ extern "C" int mignn_diag_ring(int mode, const void* plan, const int32_t* row_pt
         MIGNN_RING_MODE(4) MIGNN_RING_MODE(6) MIGNN_RING_MODE(7) MIGNN_RING_MODE(8)
         MIGNN_RING_MODE(15) MIGNN_RING_MODE(16) MIGNN_RING_MODE(17) MIGNN_RING_MODE(18)
         MIGNN_RING_MODE(20) MIGNN_RING_MODE(64) MIGNN_RING_MODE(80)
+        MIGNN_RING_MODE(32) MIGNN_RING_MODE(33) MIGNN_RING_MODE(34) MIGNN_RING_MODE(40)
 #undef MIGNN_RING_MODE
         default: break;
     }
