@@ -448,7 +448,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     // ext rows of step s (its records' ext list): piece i of this wave's
     // ext rows k = EPW wave .. +EPW (chunk c of row k at position c ^ (k & 7));
     // unused list entries hold column 0 (loaded, never read)
-    auto dma_ext_piece = [&](int64_t s, int i) {
+    auto ext_src = [&](int64_t s, int i) -> const unsigned char* {
         const unsigned char* const tab = lds + C::OFF_TAB + tslot(s) * C::TAB_BYTES + wave * 576 + 512;
         int l = lane;
         asm volatile("" : "+v"(l));
@@ -456,16 +456,20 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         const int k = wave * C::EPW + kk;
         const int pos = l % C::LPR;
         const uint32_t c = *reinterpret_cast<const uint32_t*>(tab + 4 * kk);
-        const unsigned char* src =
-            (MODE & 1) ? reinterpret_cast<const unsigned char*>(g_ring_zero_row + 4 * pos)
-                       : reinterpret_cast<const unsigned char*>(x) + static_cast<uint64_t>(c) * ldxb +
-                             16u * static_cast<uint32_t>(pos ^ (k & 7));
+        return (MODE & 1) ? reinterpret_cast<const unsigned char*>(g_ring_zero_row + 4 * pos)
+                          : reinterpret_cast<const unsigned char*>(x) + static_cast<uint64_t>(c) * ldxb +
+                                16u * static_cast<uint32_t>(pos ^ (k & 7));
+    };
+    auto ext_dma = [&](int64_t s, int i, const unsigned char* src) {
         rdma(src, rlds(lds + C::OFF_EXT + (C::E2 && (s & 1) ? C::EXT_BYTES : 0) +
                        (wave * C::EPW + i * C::RPP) * C::ROWB));
     };
     auto dma_ext = [&](int64_t s) {
+        const unsigned char* es[C::NPE];
 #pragma unroll
-        for (int i = 0; i < C::NPE; ++i) dma_ext_piece(s, i);
+        for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(s, i);   // (the list reads first)
+#pragma unroll
+        for (int i = 0; i < C::NPE; ++i) ext_dma(s, i, es[i]);
     };
 
     // ------------------------------------------------------------ prologue
@@ -782,13 +786,23 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                 bh = *reinterpret_cast<const f16x8r*>(&AHb[ib * 16 * C::AS + 32 * kc]);
                 bl = *reinterpret_cast<const f16x8r*>(&ALb[ib * 16 * C::AS + 32 * kc]);
             };
-            f16x8r fh[2], fl[2];
-            frag(0, fh[0], fl[0]);
+            // the next step's ext sources, all list reads before the loop (a
+            // list read per piece inside it would wait on the fragment reads)
+            constexpr int NPE1 = C::E2 ? 0 : C::NPE;
+            const unsigned char* es[NPE1 > 0 ? NPE1 : 1];
+#pragma unroll
+            for (int i = 0; i < NPE1; ++i) es[i] = ext_src(s + 1, i);
+            __builtin_amdgcn_sched_barrier(0);
+            // A fragments PD steps ahead (a ring of PD + 1): a read issued one
+            // step ahead waited its LDS latency behind a single MFMA
+            constexpr int PD = 1, NF = PD + 1, NTT = C::KC * IBW;
+            f16x8r fh[NF], fl[NF];
+#pragma unroll
+            for (int t = 0; t < PD && t < NTT; ++t) frag(t, fh[t], fl[t]);
             // one DMA piece per MFMA step: step s+1's ext rows, then step
             // s+2's ring DMA (the rest after the loop)
-            constexpr int NPE1 = C::E2 ? 0 : C::NPE;
             auto dma_piece = [&](int t) {
-                if (t < NPE1) dma_ext_piece(s + 1, t);
+                if (t < NPE1) ext_dma(s + 1, t, es[t]);
                 else dma_tile_piece(s + 2, t - NPE1);
             };
             constexpr int NPC = NPE1 + C::NDMA;
@@ -797,12 +811,12 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                 const int kc = t / IBW, ib = t % IBW;
                 if (t < NPC) dma_piece(t);
                 if (MODE & 4) continue;
-                if (t + 1 < C::KC * IBW) frag(t + 1, fh[(t + 1) & 1], fl[(t + 1) & 1]);
+                if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
 #pragma unroll
                 for (int cb = 0; cb < CPW; ++cb) {
-                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], fh[t & 1], accm[cb][ib], 0, 0, 0);
-                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], fl[t & 1], accm[cb][ib], 0, 0, 0);
-                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cb][kc], fh[t & 1], accm[cb][ib], 0, 0, 0);
+                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], fh[t % NF], accm[cb][ib], 0, 0, 0);
+                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], fl[t % NF], accm[cb][ib], 0, 0, 0);
+                    accm[cb][ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cb][kc], fh[t % NF], accm[cb][ib], 0, 0, 0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
