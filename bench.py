@@ -285,7 +285,8 @@ def main():
             traffic = None
     roofline = None
     if args.layer_type == "GCN":
-        roofline = gcn_roofline(launches, H, deg_plus_self, model.precision, traffic)
+        roofline = gcn_roofline(launches, H, deg_plus_self, model.precision, traffic,
+                                model._gcn_kernel(H))
 
     exact = None
     if model.precision != "f32":
@@ -334,8 +335,8 @@ def main():
         "exact_f32": exact,
         "device_errors": dev_errors[0],
     }
-    if world == 1 and args.layer_type == "GCN" and H in (64, 128):
-        line["aggregate_alone"] = aggregate_roofline(model, x, H, args.steps)
+    if world == 1 and args.layer_type == "GCN":
+        line["aggregate_alone"] = aggregate_roofline(model, x, args.steps)
     if world > 1:
         dist.barrier()
     if not args.no_config4:
@@ -402,12 +403,14 @@ def time_layers(model, recording):
     return restore
 
 
-def aggregate_roofline(model, x, H, steps):
-    """SURVEY 8(d) target (i): the GCN aggregate kernel alone
-    (mignn_gcn_aggregate_planned: out = D^-1/2 (A + I) D^-1/2 x, fp32) over the
-    bench graph's CSR in the locality order (the model's cached CSR of the
-    graph-cached loop), HIP events on the launch stream; algorithmic bytes as
-    the layer's: read x and write the output once, the CSR arrays once."""
+def aggregate_roofline(model, x, steps):
+    """SURVEY 8(d) target (i): the GCN aggregate kernel alone (out = D^-1/2
+    (A + I) D^-1/2 x, fp32, CSR order) at H = 128 and 64 over the bench graph's
+    CSR in the locality order (the model's cached CSR of the graph-cached
+    loop), HIP events on the launch stream; algorithmic bytes as the layer's:
+    read x and write the output once, the CSR arrays once.  The ring kernel
+    (mignn_gcn_aggregate_ring) is reported, the tile-plan kernel
+    (mignn_gcn_aggregate_planned) beside it."""
     from mignn import _lib
     csr = None
     for c in model._csr.entries.values():
@@ -415,37 +418,58 @@ def aggregate_roofline(model, x, H, steps):
     if csr is None:
         return None
     n = csr.num_nodes
-    plan = csr.gcn_plan(H, 0, n)
-    X = torch.randn((n, H), device=x.device, generator=torch.Generator(device=x.device).manual_seed(3))
-    Y = torch.empty_like(X)
+    nnz = int(csr.row_ptr[-1].item())
     L = _lib.lib()
     P = _lib.ptr
     st = _lib.stream(x.device)
-
-    def run():
-        _lib.check(L.mignn_gcn_aggregate_planned(P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew),
-                                                 P(X), H, 0, n, H, P(Y), H, st),
-                   "mignn_gcn_aggregate_planned")
-    for _ in range(3):
-        run()
     k = max(5, min(steps, 20))
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(k):
-        run()
-    e1.record()
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / k
-    nnz = int(csr.row_ptr[-1].item())
-    by = 4 * (2 * n * H + (n + 1) + nnz + n)
-    return {"kernel": "gcn_tile_kernel<%d, agg> (mignn_gcn_aggregate_planned)" % H,
-            "bound": "hbm", "achieved": round(by / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK / 1e9,
-            "unit": "GB/s", "frac": round(by / (ms * 1e-3) / HBM_PEAK, 4), "traffic": None,
-            "avg_launch_ms": round(ms, 4), "launches": k, "algorithmic_bytes_per_launch": by,
-            "H": H, "rows": n, "csr_entries": nnz}
+    res = {}
+    for H in (128, 64):
+        X = torch.randn((n, H), device=x.device,
+                        generator=torch.Generator(device=x.device).manual_seed(3))
+        Y = torch.empty_like(X)
+        rplan = csr.ring_plan(H, 0, n)
+        tplan = csr.gcn_plan(H, 0, n)
+        runs = {
+            "ring": ("gcn_ring_kernel<%d, aggregate> (mignn_gcn_aggregate_ring)" % H,
+                     lambda: _lib.check(L.mignn_gcn_aggregate_ring(
+                         P(rplan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(Y), H,
+                         st), "mignn_gcn_aggregate_ring")),
+            "tile": ("gcn_tile_kernel<%d, agg> (mignn_gcn_aggregate_planned)" % H,
+                     lambda: _lib.check(L.mignn_gcn_aggregate_planned(
+                         P(tplan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H, P(Y), H,
+                         st), "mignn_gcn_aggregate_planned")),
+        }
+        by = 4 * (2 * n * H + (n + 1) + nnz + n)
+        out = {}
+        for name, (kname, run) in runs.items():
+            for _ in range(3):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(k):
+                run()
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / k
+            out[name] = {"kernel": kname, "bound": "hbm",
+                         "achieved": round(by / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(by / (ms * 1e-3) / HBM_PEAK, 4),
+                         "traffic": None, "avg_launch_ms": round(ms, 4), "launches": k,
+                         "algorithmic_bytes_per_launch": by}
+        best = dict(out["ring"])
+        best.update({"H": H, "rows": n, "csr_entries": nnz, "tile_kernel": out["tile"]})
+        res[f"H{H}"] = best
+        del X, Y
+    return res
 
 
-def gcn_roofline(launches, H, deg_plus_self, precision, traffic):
+GCN_KERNEL_NAMES = {"pc": "gcn_f16x3_kernel<%d> (mignn_gcn_layer_f16x3)",
+                    "tile": "gcn_tile_kernel<%d> (mignn_gcn_layer_planned)",
+                    "ring": "gcn_ring_kernel<%d> (mignn_gcn_layer_ring)"}
+
+
+def gcn_roofline(launches, H, deg_plus_self, precision, traffic, route="pc"):
     """Roofline of the fused GCN layer kernel from its timed launches."""
     if not launches:
         return None
@@ -461,7 +485,7 @@ def gcn_roofline(launches, H, deg_plus_self, precision, traffic):
         # gather-aggregate FMAs on the fp32 VALU
         t_comp = (3 * 2 * n_rows * H * H / F16_MFMA_PEAK
                   + 2 * n_rows * deg_plus_self * H / F32_MFMA_PEAK)
-        kname = "gcn_f16x3_kernel<%d> (mignn_gcn_layer_f16x3)" % H
+        kname = GCN_KERNEL_NAMES[route] % H
         comp_peak, comp_note = F16_MFMA_PEAK, "f16 MFMA x3 (split fp32) + f32 VALU aggregate"
     else:
         t_comp = tot_flops / F32_MFMA_PEAK
@@ -580,7 +604,8 @@ def eval_leg(name, dev, precision, steps, warmup, cpu_threads=None):
            "nodes": N, "edges": E, "graph_setup_in_step": setup_in_step,
            "ms_per_forward": round(1e3 * el / steps, 3), "edges_per_s": L * E * steps / el}
     if lt == "GCN" and H in (64, 128):
-        out["roofline"] = gcn_roofline(launches, H, e_rows / N, precision, None)
+        out["roofline"] = gcn_roofline(launches, H, e_rows / N, precision, None,
+                                       model._gcn_kernel(H))
     else:
         tot_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in launches)
         n_rows = sum(n for _, _, n in launches)

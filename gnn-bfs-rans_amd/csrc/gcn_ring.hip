@@ -67,13 +67,18 @@ struct RCfg {
     static constexpr int A_BYTES = BM * AS * 2;
     // E2 (where LDS allows): the ext rows double-buffered and DMA'd a whole
     // step ahead (at the top of the previous step), the records 3 steps ahead
-    static constexpr bool E2 = H == 64;
+    static constexpr bool E2 = false;   // (measured no faster at H = 64)
+    // X1: one own-row slot (the next tile's rows DMA'd once this tile's are
+    // consumed), which leaves LDS for WGPC = 2 workgroups per CU
+    static constexpr bool X1 = H == 64;
+    static constexpr int WGPC = X1 ? 2 : 1;
+    static_assert(!(X1 && E2), "X1 with E2: not built");
     static constexpr int NE = E2 ? 2 : 1;              // ext areas
     static constexpr int NTB = E2 ? 3 : 2;             // record (TAB) slots
     // LDS: X[2] | EXT[NE] | TAB[NTB] | zero row | AH | AL | REXP | EPI
     static constexpr int OFF_X0 = 0;
-    static constexpr int OFF_X1 = X_BYTES;
-    static constexpr int OFF_EXT = 2 * X_BYTES;
+    static constexpr int OFF_X1 = X1 ? 0 : X_BYTES;
+    static constexpr int OFF_EXT = (X1 ? 1 : 2) * X_BYTES;
     static constexpr int OFF_TAB = OFF_EXT + NE * EXT_BYTES;
     static constexpr int OFF_ZERO = OFF_TAB + NTB * TAB_BYTES;
     static constexpr int OFF_AH = OFF_ZERO + ROWB;
@@ -95,7 +100,7 @@ struct RCfg {
     static constexpr int LPRW = ROWB / 16, RPI = 64 / LPRW;
     static constexpr int NST = 8 / RPI;                // row stores per wave (8 rows)
     static constexpr int NDMA = 1 + NPX;               // ring DMA ops per wave per tile
-    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+    static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
     static_assert(BM * ROWB <= 2 * A_BYTES, "staging tile fits the A image");
     static_assert(EPW == NPE * RPP && EPW <= 12, "ext rows per wave");
     static_assert(OFF_EXT + NE * EXT_BYTES <= (1 << 17), "codes below bit 17");
@@ -110,7 +115,7 @@ __host__ __device__ inline int ring_parity(int64_t tile, int64_t ntiles, int G) 
     return static_cast<int>(((tile % chunk) / per_xcd) & 1);
 }
 
-int ring_grid(int64_t ntiles) {
+int ring_grid(int64_t ntiles, int wgpc) {
     static int cus_cache[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
@@ -120,7 +125,7 @@ int ring_grid(int64_t ntiles) {
             return -1;
         if (cus < 1) cus = 1;
     }
-    int G = (cus / 8) * 8;
+    int G = (cus * wgpc / 8) * 8;
     if (G < 8) G = 8;
     if (ntiles < G) G = static_cast<int>(((ntiles + 7) / 8) * 8);
     return G;
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
 // EPIF: the epilogue flags at compile time (15 = BIAS|RESIDUAL|AFFINE|RELU,
 // 11 = BIAS|RESIDUAL|RELU: FlowGNN with / without BatchNorm), -1: from `flags`
 template <int H, int MODE = 0, int EPIF = -1>
-__global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
+__global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
     const unsigned char* __restrict__ plan, const int32_t* __restrict__ row_ptr,
     const int32_t* __restrict__ col, const float* __restrict__ ew, const float* __restrict__ x,
     int64_t ldx, int64_t row_begin, int64_t row_end, const float* __restrict__ W,
@@ -445,6 +450,13 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
 #pragma unroll
         for (int q = 0; q <= C::NPX; ++q) dma_tile_piece(s, q);
     };
+    // piece q of the ring DMA issued after B1 of step s: the records of step
+    // s + 2 (E2: s + 3), then the own rows of step s + 2 (X1: s + 1, into the
+    // slot step s just released)
+    auto ring_piece = [&](int64_t s, int q) {
+        if (q == 0) dma_tab(C::E2 ? s + 3 : s + 2);
+        else dma_tile_piece(C::X1 ? s + 1 : s + 2, q);
+    };
     // ext rows of step s (its records' ext list): piece i of this wave's
     // ext rows k = EPW wave .. +EPW (chunk c of row k at position c ^ (k & 7));
     // unused list entries hold column 0 (loaded, never read)
@@ -519,7 +531,12 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
     }
     const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
 
-    if constexpr (C::E2) {
+    if constexpr (C::X1) {
+        dma_tile(0);                  // records and rows of step 0
+        dma_tab(1);
+        rbar<rvm_l(0)>();             // (all waves), zero row, EPI
+        dma_ext(0);
+    } else if constexpr (C::E2) {
         dma_tab(0);
         dma_tile(0);                  // records of step 1, rows of step 0
         dma_tile(1);                  // records of step 2, rows of step 1
@@ -546,9 +563,11 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
         // (B0) this step's ext rows landed in every wave (and, older, its own
         //      rows and records): younger ops = the next tile's ring DMA and
         //      the last tile's row stores
-        // (E2: older than these ext rows are the records of step s + 1 too)
-        if (s == 0) rbar<rvm_l(C::E2 ? 0 : C::NDMA)>();
-        else rbar<rvm_l(C::NDMA + C::NST)>();
+        // (E2: older than these ext rows are the records of step s + 1 too;
+        //  X1: this step's own rows were issued after them: only the last
+        //  tile's stores may fly)
+        if (s == 0) rbar<rvm_l((C::E2 || C::X1) ? 0 : C::NDMA)>();
+        else rbar<rvm_l(C::X1 ? C::NST : C::NDMA + C::NST)>();
         if constexpr (C::E2) dma_ext(s + 1);     // into the ext area step s - 1 used
         rtr.flush(wave, lane, s - 1);
         rtr.stamp(1);
@@ -674,7 +693,8 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
                 else rwait<rvm(C::NPX + C::NST)>();
                 dma_ext(s + 1);
             }
-            dma_tile(s + 2);
+#pragma unroll
+            for (int q = 0; q <= C::NPX; ++q) ring_piece(s, q);
             static_assert(C::NQ * C::CH == C::NST, "aggregate stores keep the per-step store count");
 #pragma unroll
             for (int qd = 0; qd < C::NQ; ++qd)
@@ -803,7 +823,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, 1) void gcn_ring_kernel(
             // s+2's ring DMA (the rest after the loop)
             auto dma_piece = [&](int t) {
                 if (t < NPE1) ext_dma(s + 1, t, es[t]);
-                else dma_tile_piece(s + 2, t - NPE1);
+                else ring_piece(s, t - NPE1);
             };
             constexpr int NPC = NPE1 + C::NDMA;
 #pragma unroll
@@ -931,7 +951,7 @@ int launch_ring(int h, const void* plan, const int32_t* row_ptr, const int32_t* 
                 const float* w, const float* bias, const float* scale, const float* shift,
                 int flags, float* out, int64_t ldo, hipStream_t st) {
     const int64_t ntiles = (re - rb + 63) / 64;
-    const int G = ring_grid(ntiles);
+    const int G = ring_grid(ntiles, h == 128 ? RCfg<128>::WGPC : RCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_ring: device query failed");
     if (h == 128)
         launch_ring_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
@@ -962,7 +982,7 @@ extern "C" int mignn_gcn_ring_plan(const int32_t* row_ptr, const int32_t* col, c
     MIGNN_REQUIRE(plan_bytes >= mignn_gcn_ring_plan_bytes(rb, re, h),
                   "gcn_ring_plan: plan buffer too small");
     const int64_t ntiles = (re - rb + 63) / 64;
-    const int G = ring_grid(ntiles);
+    const int G = ring_grid(ntiles, h == 128 ? RCfg<128>::WGPC : RCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_ring_plan: device query failed");
     const unsigned grid = static_cast<unsigned>(ntiles < (1 << 20) ? ntiles : (1 << 20));
     if (h == 128)

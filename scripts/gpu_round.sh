@@ -10,7 +10,7 @@ timeout -k 10 400 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 if [ -z "${NO_TESTS:-}" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
+  timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
       > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
   if [ $rc -gt 1 ]; then exit $rc; fi
