@@ -54,15 +54,21 @@ constexpr uint32_t kFar = 0x80000000u;
 template <int H>
 struct RCfg {
     static_assert(H == 64 || H == 128, "ring GCN layer: H in {64, 128}");
-    static constexpr int BM = 64, NW = 8, NT = NW * 64;
+    // 64-row tiles (the locality order's 4 x 4 x 4 blocks).  (32-row tiles at
+    // H = 128 -- 4 x 4 x 2 slabs, two workgroups per CU -- measured slower:
+    // 3.15 vs 3.09 ms, their 2:1 out-of-tile rows per own row cost more
+    // than the second workgroup gains; BM = 32 builds, KX = 64 then)
+    static constexpr int BM = 64, NW = BM / 8, NT = NW * 64;
     static constexpr int F = H / 16, CH = F / 4;       // floats / 16-B chunks per lane of a row
     static constexpr int ROWB = H * 4;
     static constexpr int AS = H + 16;                  // A row stride, halfs
     static constexpr int X_BYTES = BM * ROWB;
-    static constexpr int KX = 96;                      // ext rows per tile in LDS
+    static constexpr int KX = BM == 32 ? 64 : 96;      // ext rows per tile in LDS
     static constexpr int EXT_BYTES = KX * ROWB;
-    static constexpr int XLW = 16;                     // ext-list group per wave: 12 columns, the summary
-    static constexpr int EPW = KX / NW;                // ext rows DMA'd per wave (12)
+    static constexpr int EPW = KX / NW;                // ext rows DMA'd per wave (12 or 16)
+    static constexpr int XLW = (EPW + 4) / 4 * 4;      // ext-list group per wave: EPW columns, the summary
+    static constexpr int RECW = 8 * kRec + XLW * 4;    // a wave's records + list in LDS
+    static constexpr int TLANES = RECW / 16;           // lanes of its DMA
     static constexpr int TAB_BYTES = BM * kRec + NW * XLW * 4;   // records + ext list (4608)
     static constexpr int A_BYTES = BM * AS * 2;
     // E2 (where LDS allows): the ext rows double-buffered and DMA'd a whole
@@ -102,7 +108,7 @@ struct RCfg {
     static constexpr int NDMA = 1 + NPX;               // ring DMA ops per wave per tile
     static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
     static_assert(BM * ROWB <= 2 * A_BYTES, "staging tile fits the A image");
-    static_assert(EPW == NPE * RPP && EPW <= 12, "ext rows per wave");
+    static_assert(EPW == NPE * RPP && EPW < XLW && RECW % 16 == 0 && TLANES <= 64, "ext rows per wave");
     static_assert(OFF_EXT + NE * EXT_BYTES <= (1 << 17), "codes below bit 17");
 };
 
@@ -244,7 +250,7 @@ struct RTrace {
 // not deduplicated; slot k < KX lives at LDS row k of the ext area, its column
 // in list entry (k / EPW) * XLW + k % EPW (the DMA pieces of wave k / EPW).
 template <int H>
-__global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict__ row_ptr,
+__global__ __launch_bounds__(RCfg<H>::BM) void ring_plan_kernel(const int32_t* __restrict__ row_ptr,
                                                        const int32_t* __restrict__ col,
                                                        const float* __restrict__ ew, int64_t rb,
                                                        int64_t re, int64_t ntiles, int G,
@@ -254,13 +260,13 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
     const int lr = threadIdx.x;
     __shared__ uint32_t xl[C::NW * C::XLW];
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int64_t t0 = rb + t * 64;
+        const int64_t t0 = rb + t * C::BM;
         const int64_t r = t0 + lr;
-        const uint32_t nloc = static_cast<uint32_t>(re - t0 < 64 ? re - t0 : 64);
+        const uint32_t nloc = static_cast<uint32_t>(re - t0 < C::BM ? re - t0 : C::BM);
         const int tpar = ring_parity(t, ntiles, G);
         const uint32_t xoff = tpar ? C::OFF_X1 : C::OFF_X0;
         const uint32_t eoff = C::OFF_EXT + (C::E2 && tpar ? C::EXT_BYTES : 0);
-        for (int i = lr; i < C::NW * C::XLW; i += 64) xl[i] = 0u;   // unused: row 0, never read
+        for (int i = lr; i < C::NW * C::XLW; i += C::BM) xl[i] = 0u;   // unused: row 0, never read
         int e0 = 0, deg = 0, next = 0;
         if (r < re) {
             e0 = row_ptr[r];
@@ -271,11 +277,11 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
                     if (!(c >= t0 && c < t0 + nloc)) ++next;
                 }
         }
-        // exclusive prefix of the ext counts over the 64 rows
+        // exclusive prefix of the ext counts over the tile's rows
         int pre = next;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(pre, d, 64);
+        for (int d = 1; d < C::BM; d <<= 1) {
+            const int v = __shfl_up(pre, d, C::BM);
             if (lr >= d) pre += v;
         }
         pre -= next;
@@ -331,14 +337,14 @@ __global__ __launch_bounds__(64) void ring_plan_kernel(const int32_t* __restrict
         uint4* dst = reinterpret_cast<uint4*>(base + lr * kRec);
 #pragma unroll
         for (int i = 0; i < 4; ++i) dst[i] = make_uint4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
-        for (int i = lr; i < C::NW * C::XLW; i += 64)
+        for (int i = lr; i < C::NW * C::XLW; i += C::BM)
             reinterpret_cast<uint32_t*>(base + C::BM * kRec)[i] = xl[i];
         if (stats != nullptr) {
-            const int kt = __shfl(pre + next, 63, 64);
+            const int kt = __shfl(pre + next, C::BM - 1, C::BM);
             if (nfar) atomicAdd(&stats[1], nfar);
             if (slow) atomicAdd(&stats[2], 1ull);
-            if (lr == 63 && kt > C::KX) atomicAdd(&stats[0], 1ull);
-            if (lr == 63) atomicMax(&stats[3], static_cast<unsigned long long>(kt));
+            if (lr == C::BM - 1 && kt > C::KX) atomicAdd(&stats[0], 1ull);
+            if (lr == C::BM - 1) atomicMax(&stats[3], static_cast<unsigned long long>(kt));
         }
         __syncthreads();
     }
@@ -416,9 +422,9 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
     auto tslot = [&](int64_t s) -> int { return C::E2 ? static_cast<int>(s % 3) : static_cast<int>(s & 1); };
     auto dma_tab = [&](int64_t s) {
         const int64_t tile = tile_or0(s);
-        if (lane < 36)
+        if (lane < C::TLANES)
             rdma_s(plan + tile * C::TAB_BYTES, toff,
-                   rlds(lds + C::OFF_TAB + tslot(s) * C::TAB_BYTES + wave * 576));
+                   rlds(lds + C::OFF_TAB + tslot(s) * C::TAB_BYTES + wave * C::RECW));
     };
     // piece q of step s's ring DMA: q = 0 the records (E2: those of step
     // s + 1), 1 .. NPX own rows
@@ -461,7 +467,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
     // ext rows k = EPW wave .. +EPW (chunk c of row k at position c ^ (k & 7));
     // unused list entries hold column 0 (loaded, never read)
     auto ext_src = [&](int64_t s, int i) -> const unsigned char* {
-        const unsigned char* const tab = lds + C::OFF_TAB + tslot(s) * C::TAB_BYTES + wave * 576 + 512;
+        const unsigned char* const tab = lds + C::OFF_TAB + tslot(s) * C::TAB_BYTES + wave * C::RECW + 512;
         int l = lane;
         asm volatile("" : "+v"(l));
         const int kk = i * C::RPP + l / C::LPR;          // within the wave's rows
@@ -489,7 +495,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
     const int rr = lane & 15, gg = lane >> 4;
     // the transform's wave grid: CPW 16-column blocks x IBW 16-row blocks per
     // wave (CPW = 2: every A fragment read from LDS feeds both column blocks)
-    constexpr int CPW = (MODE & 64) ? 2 : 1;
+    constexpr int CPW = ((MODE & 64) || H / 16 > C::NW) ? 2 : 1;
     constexpr int WN = H / (16 * CPW), WM = C::NW / WN, IBW = (C::BM / 16) / WM;
     static_assert(WN * WM == C::NW && IBW * WM * 16 == C::BM, "ring transform grid");
     const int wn = wave % WN, wm = wave / WN;
@@ -549,7 +555,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
         dma_tile(1);
     }
 
-    unsigned char* const REC = lds + C::OFF_TAB;      // + parity * TAB_BYTES + wave * 576
+    unsigned char* const REC = lds + C::OFF_TAB;      // + slot * TAB_BYTES + wave * RECW
     for (int64_t s = 0; s < nsteps; ++s) {
         const int64_t tile = tile_of(s);
         if (tile >= ntiles) break;                    // uniform over the workgroup
@@ -558,7 +564,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
         const uint32_t nloc = static_cast<uint32_t>(rem < C::BM ? rem : C::BM);
         const int par = static_cast<int>(s & 1);
         const unsigned char* const X = lds + (par ? C::OFF_X1 : C::OFF_X0);
-        const unsigned char* const RW = REC + tslot(s) * C::TAB_BYTES + wave * 576;   // my 8 records
+        const unsigned char* const RW = REC + tslot(s) * C::TAB_BYTES + wave * C::RECW;   // my 8 records
         rtr.stamp(0);
         // (B0) this step's ext rows landed in every wave (and, older, its own
         //      rows and records): younger ops = the next tile's ring DMA and
@@ -950,7 +956,8 @@ int launch_ring(int h, const void* plan, const int32_t* row_ptr, const int32_t* 
                 const float* ew, const float* x, int64_t ldx, int64_t rb, int64_t re,
                 const float* w, const float* bias, const float* scale, const float* shift,
                 int flags, float* out, int64_t ldo, hipStream_t st) {
-    const int64_t ntiles = (re - rb + 63) / 64;
+    const int bm = h == 128 ? RCfg<128>::BM : RCfg<64>::BM;
+    const int64_t ntiles = (re - rb + bm - 1) / bm;
     const int G = ring_grid(ntiles, h == 128 ? RCfg<128>::WGPC : RCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_ring: device query failed");
     if (h == 128)
@@ -967,7 +974,8 @@ using namespace mignn;
 
 extern "C" size_t mignn_gcn_ring_plan_bytes(int64_t row_begin, int64_t row_end, int h) {
     if (row_end <= row_begin || (h != 64 && h != 128)) return 0;
-    const int64_t ntiles = (row_end - row_begin + 63) / 64;
+    const int bm = h == 128 ? RCfg<128>::BM : RCfg<64>::BM;
+    const int64_t ntiles = (row_end - row_begin + bm - 1) / bm;
     return static_cast<size_t>(ntiles) * (h == 128 ? RCfg<128>::TAB_BYTES : RCfg<64>::TAB_BYTES);
 }
 
@@ -981,15 +989,16 @@ extern "C" int mignn_gcn_ring_plan(const int32_t* row_ptr, const int32_t* col, c
     if (re == rb) return MIGNN_OK;
     MIGNN_REQUIRE(plan_bytes >= mignn_gcn_ring_plan_bytes(rb, re, h),
                   "gcn_ring_plan: plan buffer too small");
-    const int64_t ntiles = (re - rb + 63) / 64;
+    const int bm = h == 128 ? RCfg<128>::BM : RCfg<64>::BM;
+    const int64_t ntiles = (re - rb + bm - 1) / bm;
     const int G = ring_grid(ntiles, h == 128 ? RCfg<128>::WGPC : RCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_ring_plan: device query failed");
     const unsigned grid = static_cast<unsigned>(ntiles < (1 << 20) ? ntiles : (1 << 20));
     if (h == 128)
-        hipLaunchKernelGGL(ring_plan_kernel<128>, dim3(grid), dim3(64), 0, as_stream(stream), row_ptr,
+        hipLaunchKernelGGL(ring_plan_kernel<128>, dim3(grid), dim3(RCfg<128>::BM), 0, as_stream(stream), row_ptr,
                            col, ew, rb, re, ntiles, G, static_cast<unsigned char*>(plan), stats);
     else
-        hipLaunchKernelGGL(ring_plan_kernel<64>, dim3(grid), dim3(64), 0, as_stream(stream), row_ptr,
+        hipLaunchKernelGGL(ring_plan_kernel<64>, dim3(grid), dim3(RCfg<64>::BM), 0, as_stream(stream), row_ptr,
                            col, ew, rb, re, ntiles, G, static_cast<unsigned char*>(plan), stats);
     return launch_status("ring_plan_kernel");
 }

@@ -54,7 +54,10 @@ from ._lib import (CSR_ONE_SELF_LOOP, CSR_TRANSPOSE, CSR_VERBATIM, EPI_AFFINE, E
 HEADS = 4  # gnn_model.py:67, :79
 # the split-fp16 GCN layer kernel of FlowGNN.gcn_kernel = "auto", per hidden
 # width: the fastest measured on the bench mesh
-GCN_KERNEL_AUTO = {64: "tile", 128: "pc"}
+# (H = 64: the ring kernel, two workgroups per CU, 1.39-1.41 ms vs the tile
+# kernel's 1.57-1.59 per 10M-row layer; H = 128: the producer / consumer
+# kernel -- the ring kernel ties it per layer but needs a 0.49 ms plan per graph)
+GCN_KERNEL_AUTO = {64: "ring", 128: "pc"}
 
 
 # ---------------------------------------------------------------------------
