@@ -1187,10 +1187,7 @@ struct GatCfg {
     static constexpr int OFF_ST = OFF_AL + AW * 16 * 4 * 8 * 4;   // (max, sum) [AW][16][4]
     static constexpr int OFF_EPI = OFF_ST + AW * 16 * 4 * 8;       // QF | BF | SC | SH [H]
     static constexpr int OFF_TB = OFF_EPI + 4 * H * 4;  // (layer 0) [W_in | b_in] [H][4]
-    static constexpr int OFF_WLN = OFF_TB + H * 16;     // (LG) next layer's logit weights [8][H]
-    static constexpr int OFF_CJ = OFF_WLN + 8 * H * 4;  // the next tile's CSR slots [AW][16][8]
-    static constexpr int LDS_BYTES = OFF_CJ + AW * 16 * 8 * 4;
-    static_assert(BM * H * 4 <= STEPW, "staging rows fit one W buffer");
+    static constexpr int LDS_BYTES = OFF_TB + H * 16;
     static_assert(LDS_BYTES <= 160 * 1024, "gat_fused LDS");
 };
 
@@ -1226,19 +1223,13 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     asm volatile("" : "+v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 15, g = lane >> 4;
-    // persistent: workgroup (xcd, slot) walks steps s = 0, 1, ... of its XCD's
-    // contiguous tile range; the next tile's CSR slots and first W chunk are
-    // loaded under the current tile's last chunk
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
-    const int G = static_cast<int>(gridDim.x);
-    const int64_t per_xcd = G >> 3;
-    const int64_t nsteps = (ntiles + G - 1) / G;
-    const int64_t xbase = static_cast<int64_t>(blockIdx.x & 7) * nsteps * per_xcd + (blockIdx.x >> 3);
-    auto tile_of = [&](int64_t s) -> int64_t {
-        const int64_t t = xbase + s * per_xcd;
-        return (s < nsteps && t < ntiles) ? t : -1;
-    };
-    if (tile_of(0) < 0) return;
+    const int64_t per_xcd = gridDim.x >> 3;
+    const int64_t tile = static_cast<int64_t>(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= ntiles) return;
+    const int64_t row = rb + tile * C::BM + 16 * wave + r;
+    const bool rv = row < re;
+    const int64_t rowc = rv ? row : re - 1;
 
     // W chunks of x chunk t (heads 0..3: image chunks k XC + t) -> buffer t & 1
     auto w_dma = [&](int t) {
@@ -1253,7 +1244,6 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         }
     };
     w_dma(0);
-    const float slope_ = slope;
     if (tid < H) {
         const int32_t* q = reinterpret_cast<const int32_t*>(
             img + static_cast<size_t>(4 * C::XC) * C::NPB * 2 * AFRAG);
@@ -1273,51 +1263,14 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         }
     }
 
-    float* const WLN = reinterpret_cast<float*>(lds + C::OFF_WLN);   // (LG) [8][H]
-    if constexpr (LG)
-        for (int i = tid; i < 8 * H; i += C::NT) WLN[i] = wlog_next[i];
-
-    // a tile's CSR slots, prefetched: its row bounds (lane (r, g): row r),
-    // then slots 2 g, 2 g + 1, then into LDS (CJ[wave][r][8]) for the row's
-    // four lanes
-    static_assert(AS == 8, "two slots per lane");
-    int* const CJ = reinterpret_cast<int*>(lds + C::OFF_CJ) + (wave * 16 + r) * 8;
-    int e0n = 0, degn = 0, c0n = -1, c1n = -1;
-    auto csr_bounds = [&](int64_t tile) {
-        const int64_t row = rb + tile * C::BM + 16 * wave + r;
-        const bool rv = row < re;
-        const int64_t rowc = rv ? row : re - 1;
-        e0n = row_ptr[rowc];
-        degn = rv ? row_ptr[rowc + 1] - e0n : 0;
-    };
-    auto csr_pair = [&]() {
-        c0n = 2 * g < degn ? col[e0n + 2 * g] : -1;
-        c1n = 2 * g + 1 < degn ? col[e0n + 2 * g + 1] : -1;
-    };
-    auto csr_park = [&]() { *reinterpret_cast<int2*>(CJ + 2 * g) = make_int2(c0n, c1n); };
-    csr_bounds(tile_of(0));
-    csr_pair();
-    csr_park();
-
-#pragma unroll 1
-  for (int64_t step = 0; tile_of(step) >= 0; ++step) {
-    const int64_t tile = tile_of(step);
-    const int64_t tnext = tile_of(step + 1);
-    const int64_t row = rb + tile * C::BM + 16 * wave + r;
-    const bool rv = row < re;
-    const int64_t rowc = rv ? row : re - 1;
     // ---- CSR slots, scores of head g, softmax statistics, alphas
-    const int e0 = e0n;
-    const int deg = degn;
+    const int e0 = row_ptr[rowc];
+    const int deg = rv ? row_ptr[rowc + 1] - e0 : 0;
     int cj[AS];
-    {
-        const int4 u = *reinterpret_cast<const int4*>(CJ);
-        const int4 v = *reinterpret_cast<const int4*>(CJ + 4);
-        cj[0] = u.x; cj[1] = u.y; cj[2] = u.z; cj[3] = u.w;
-        cj[4] = v.x; cj[5] = v.y; cj[6] = v.z; cj[7] = v.w;
-    }
+#pragma unroll
+    for (int e = 0; e < AS; ++e) cj[e] = e < deg ? col[e0 + e] : -1;
     const bool extra = __builtin_amdgcn_ballot_w64(deg > AS) != 0ull;
-    auto leaky = [&](float v) { return v > 0.f ? v : v * slope_; };
+    auto leaky = [&](float v) { return v > 0.f ? v : v * slope; };
     float* const AL = reinterpret_cast<float*>(lds + C::OFF_AL) + ((wave * 16 + r) * 4) * 8;
     float pi[3] = {0.f, 0.f, 0.f};
     f32x4 PSK[HEADS];                          // (L0) per head: P = sum alpha pos_j | S = sum alpha
@@ -1444,14 +1397,6 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     for (int t = 0; t < C::XC; ++t) {
         chunk_barrier();                           // W chunks of t and this chunk's rows landed
         w_dma(t + 1);
-        // the next tile, under this tile's last two chunks: its row bounds,
-        // then its first W chunk into buffer 0 (chunk XC - 2's, free: XC is
-        // even) and its CSR slots
-        if (t == C::XC - 2 && tnext >= 0) csr_bounds(tnext);
-        if (t == C::XC - 1 && tnext >= 0) {
-            w_dma(0);
-            csr_pair();
-        }
         // the 4 heads' weighted sums of this x chunk (CSR order)
         f32x4 a[HEADS][2];
 #pragma unroll
@@ -1544,19 +1489,26 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    // epilogue (staged, whole-row stores) in W buffer 1, free once every wave
-    // is past its last MFMA (buffer 0 holds the next tile's first W chunk);
-    // the vectors [q | bias | scale | shift] are QF..SH as they stand
-    if (tnext >= 0) csr_park();                // (this wave's rows: read back in order)
+    // epilogue (staged, whole-row stores): the W / alpha buffers are free once
+    // every wave is past its last MFMA; the vectors move after the staging rows
     vm_barrier<0>();
     if (flags & MIGNN_DIAG_NO_LOCAL) {         // (ablation: no epilogue)
         if (rv && acc[0][0] == 12345.f) out[rowc * ldo] = acc[1][1];
-        continue;
+        return;
     }
-    staged_epilogue<C::NCB, L0, LG>(lds + C::STEPW, reinterpret_cast<const float*>(QF), acc, p,
-                                    flags, x, ldx, out, ldo, rb + tile * C::BM, re, wave, lane,
-                                    16 * wave + r, g, TB, pi[0], pi[1], pi[2], WLN, lg_next);
-  }
+    float* const EV2 = reinterpret_cast<float*>(lds + C::BM * H * 4);
+    if (tid < H) {
+        reinterpret_cast<int32_t*>(EV2)[tid] = QF[tid];
+        EV2[H + tid] = BF[tid];
+        EV2[2 * H + tid] = SC[tid];
+        EV2[3 * H + tid] = SH[tid];
+    }
+    float* const WLN = EV2 + 4 * H;                // (LG) the next layer's logit weights [8][H]
+    if constexpr (LG)
+        for (int i = tid; i < 8 * H; i += C::NT) WLN[i] = wlog_next[i];
+    staged_epilogue<C::NCB, L0, LG>(lds, EV2, acc, p, flags, x, ldx, out, ldo, rb + tile * C::BM,
+                                    re, wave, lane, 16 * wave + r, g, TB, pi[0], pi[1], pi[2], WLN,
+                                    lg_next);
 }
 
 // ------------------------------------------------------------------ TransformerConv
@@ -1951,18 +1903,8 @@ int launch_gat_fused(const int32_t* row_ptr, const int32_t* col, const float* lo
                      float* lg_next = nullptr) {
     using C = GatCfg<H>;
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
-    // persistent: one workgroup per CU (LDS), a multiple of 8 (XCDs)
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, v = 0;
-        MIGNN_REQUIRE(hipGetDevice(&dev) == hipSuccess &&
-                          hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
-                              hipSuccess,
-                      "gat_fused: device query failed");
-        cus = v > 8 ? v : 8;
-    }
-    int64_t nb = (cus / 8) * 8;
-    if (ntiles < nb) nb = (ntiles + 7) / 8 * 8;
+    const int64_t nb = (ntiles + 7) / 8 * 8;
+    MIGNN_REQUIRE(nb < (int64_t(1) << 31), "gat_fused: too many rows");
     if (!L0 && lg_next != nullptr)
         hipLaunchKernelGGL((gat_fused_kernel<H, false, true>), dim3(static_cast<unsigned>(nb)),
                            dim3(C::NT), 0, st, row_ptr, col, logits, x, ldx, rb, re, slope,
