@@ -306,7 +306,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
     for (int e = 0; e < AS; ++e) {
         const int c = e < deg ? col[e0 + e] : -1;
-        wgt[e] = (MODE == AGG_GCN && e < deg) ? ew[e0 + e] : 0.f;
+        // (GIN: weight 1 -- the sum as FMAs, so an empty slot is a weight-0
+        // read of the row's own x_i, finite whenever the output is: no select)
+        wgt[e] = e < deg ? (MODE == AGG_GCN ? ew[e0 + e] : 1.f) : 0.f;
         const uint32_t off = static_cast<uint32_t>(c - static_cast<int>(t0));
         if (c < 0) {
             code[e] = -1;
@@ -323,11 +325,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     const bool slow = deg > AS || next > ES;
     if (slow) {
 #pragma unroll
-        for (int e = 0; e < AS; ++e) code[e] = -1;
+        for (int e = 0; e < AS; ++e) {
+            code[e] = -1;
+            wgt[e] = 0.f;
+        }
 #pragma unroll
         for (int k = 0; k < ES; ++k) xc[k] = -1;
     }
     const bool any_slow = __builtin_amdgcn_ballot_w64(slow) != 0ull;
+    // slots past every row's degree are skipped (a uniform branch)
+    int maxdeg = 0;
+#pragma unroll
+    for (int e = 1; e <= AS; ++e)
+        if (__builtin_amdgcn_ballot_w64(!slow && deg >= e) != 0ull) maxdeg = e;
     unsigned char* const EXT = lds + OFF_EXT + wave * EXTB;
     // (slots no row of the wave uses are skipped: only the own rows' refill,
     // issued last, is counted by the waits)
@@ -371,33 +381,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
         const bool dsum = !(flags & MIGNN_DIAG_NO_PRODUCE);
 #pragma unroll
         for (int e = 0; e < AS; ++e) {
-            if (!dsum) break;
+            if (!dsum || e >= maxdeg) break;
             const int c = code[e];
             uint32_t ad0, ad1;                     // LDS byte offsets of the 2 x 16 B
             if (c >= 256) {
                 ad0 = static_cast<uint32_t>(OFF_EXT + wave * EXTB + (2 * (c - 256)) * 1024 + lane * 16);
                 ad1 = ad0 + 1024;
             } else {
-                const int li = c < 0 ? 0 : c;
+                const int li = c < 0 ? lself : c;  // (empty: the own row, weight 0)
                 const uint32_t rp = static_cast<uint32_t>(OFF_OWN + (kc % 3) * OWNB + li * 128);
                 ad0 = rp + 16 * ((2 * g + li) & 7);
                 ad1 = rp + 16 * ((2 * g + 1 + li) & 7);
             }
-            f32x4 v0 = *reinterpret_cast<const f32x4*>(lds + ad0);
-            f32x4 v1 = *reinterpret_cast<const f32x4*>(lds + ad1);
-            if (c < 0) {
-                v0 = f32x4{0.f, 0.f, 0.f, 0.f};
-                v1 = v0;
-            }
-            if constexpr (MODE == AGG_GCN) {
+            const f32x4 v0 = *reinterpret_cast<const f32x4*>(lds + ad0);
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(lds + ad1);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    a0[i] = fmaf(wgt[e], v0[i], a0[i]);
-                    a1[i] = fmaf(wgt[e], v1[i], a1[i]);
-                }
-            } else {
-                a0 += v0;
-                a1 += v1;
+            for (int i = 0; i < 4; ++i) {
+                a0[i] = fmaf(wgt[e], v0[i], a0[i]);
+                a1[i] = fmaf(wgt[e], v1[i], a1[i]);
             }
             if ((e & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }

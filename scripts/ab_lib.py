@@ -1,0 +1,73 @@
+"""A/B of one fused layer entry between two builds of libmignn.so (the
+current one and gnn-bfs-rans_amd/mignn/libmignn_prev.so, built from an earlier
+tree), same inputs, interleaved rounds, HIP events, median.  Env: AB_MODE
+(gin | gcn | gat), AB_GRID."""
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "gnn-bfs-rans_amd"))
+import torch  # noqa: E402
+
+from mignn import _lib  # noqa: E402
+from mignn.gnn_model import build_csr, f16x3_image, gin_fused_image, locality_order  # noqa: E402
+from mignn.synthetic import grid_graph  # noqa: E402
+
+dev = torch.device("cuda", 0)
+mode = os.environ.get("AB_MODE", "gin")
+H = 128 if mode == "gat" else 256
+nx, ny, nz = (int(v) for v in os.environ.get("AB_GRID", "500,400,63").split(","))
+pos, ei = grid_graph(nx, ny, nz, device=dev)
+n = pos.shape[0]
+_, inv = locality_order(pos, ei)
+csr = build_csr(ei, n, _lib.CSR_VERBATIM if mode == "gin" else _lib.CSR_ONE_SELF_LOOP, relabel=inv)
+del ei, pos
+g = torch.Generator(device=dev).manual_seed(0)
+X = torch.randn(n, H, device=dev, generator=g)
+W1 = torch.randn(H, H, device=dev, generator=g) / 16
+W2 = torch.randn(H, H, device=dev, generator=g) / 16
+b1 = torch.randn(H, device=dev, generator=g) * 0.05
+b2 = torch.randn(H, device=dev, generator=g) * 0.05
+sc = torch.rand(H, device=dev, generator=g) + 0.5
+sh = torch.randn(H, device=dev, generator=g) * 0.1
+img1, img2 = f16x3_image(W1), gin_fused_image(W2)
+libs = {"cur": _lib.lib(),
+        "prev": _lib._load(os.path.join(HERE, "gnn-bfs-rans_amd", "mignn", "libmignn_prev.so"),
+                           _lib.SIGNATURES)}
+P = _lib.ptr
+st = _lib.stream()
+
+
+def run(L, Y):
+    if mode == "gin":
+        _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
+                                           P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15,
+                                           P(Y), H, st), "gin")
+    else:
+        _lib.check(L.mignn_gcn_layer_fused(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n,
+                                           H, P(img1), P(b1), P(sc), P(sh), 15, P(Y), H, st), "gcn")
+
+
+Ys = {k: torch.empty_like(X) for k in libs}
+for k, L in libs.items():
+    run(L, Ys[k])
+torch.cuda.synchronize()
+res = {"mode": mode, "n": n, "max_diff": (Ys["cur"] - Ys["prev"]).abs().max().item(),
+       "bitwise_equal": bool(torch.equal(Ys["cur"], Ys["prev"]))}
+times = {k: [] for k in libs}
+for rnd in range(int(os.environ.get("AB_REPS", "5")) + 1):
+    for k, L in libs.items():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            run(L, Ys[k])
+        e1.record()
+        e1.synchronize()
+        if rnd > 0:
+            times[k].append(e0.elapsed_time(e1) / 3)
+res["ms"] = {k: round(statistics.median(v), 4) for k, v in times.items()}
+print(json.dumps(res), flush=True)
