@@ -224,7 +224,8 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
 // rows of chunk kc+1 (the youngest 2 pieces) must have landed.  A row whose
 // first AS entries hold more than ES out-of-tile ones, or with more than AS
 // entries, takes all its entries one at a time (correct, not fast).
-template <int MODE, bool CHAIN>
+// EPIF: the epilogue flags at compile time (the model's 15 / 11), -1: `flags`
+template <int MODE, bool CHAIN, int EPIF = -1>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void agg_gemm_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t rb,
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     const float* __restrict__ b1, const unsigned char* __restrict__ img2,
     const float* __restrict__ b2, const float* __restrict__ scale,
     const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+    if constexpr (EPIF >= 0) flags = EPIF;
     constexpr int AW = 8, BM = 16 * AW;
     constexpr int NC = AKP * (CHAIN ? 2 : 1);          // W chunks streamed per tile
     constexpr int OWNB = BM * 128;                      // one own-row chunk slice
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
         const bool dsum = !(flags & MIGNN_DIAG_NO_PRODUCE);
 #pragma unroll
         for (int e = 0; e < AS; ++e) {
-            if (!dsum || e >= maxdeg) break;
+            if (!dsum || e >= maxdeg) continue;   // (uniform)
             const int c = code[e];
             uint32_t ad0, ad1;                     // LDS byte offsets of the 2 x 16 B
             if (c >= 256) {
@@ -1886,10 +1888,17 @@ int launch_agg_gemm(const int32_t* row_ptr, const int32_t* col, const float* ew,
     const int64_t ntiles = (re - rb + BM - 1) / BM;
     const int64_t nb = (ntiles + 7) / 8 * 8;
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "agg_gemm: too many rows");
-    hipLaunchKernelGGL((agg_gemm_kernel<MODE, CHAIN>), dim3(static_cast<unsigned>(nb)), dim3(512),
-                       0, st, row_ptr, col, ew, x, ldx, rb, re, self_scale,
-                       static_cast<const unsigned char*>(img1), b1,
-                       static_cast<const unsigned char*>(img2), b2, scale, shift, flags, out, ldo);
+    constexpr int kBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE | MIGNN_EPI_RELU;
+    constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nb)), dim3(512), 0, st, row_ptr, col,
+                           ew, x, ldx, rb, re, self_scale, static_cast<const unsigned char*>(img1),
+                           b1, static_cast<const unsigned char*>(img2), b2, scale, shift, flags,
+                           out, ldo);
+    };
+    if (flags == kBN) go(agg_gemm_kernel<MODE, CHAIN, kBN>);
+    else if (flags == kNoBN) go(agg_gemm_kernel<MODE, CHAIN, kNoBN>);
+    else go(agg_gemm_kernel<MODE, CHAIN>);
     return launch_status("agg_gemm_kernel");
 }
 
