@@ -1203,7 +1203,7 @@ struct GatCfg {
 // the row's other lanes through LDS: it gave wrong rows in waves 4-7 of some
 // tiles, run to run, with or without extra barriers; the register form is
 // exact and deterministic.)
-template <int H, bool L0 = false, bool LG = false>
+template <int H, bool L0 = false, bool LG = false, int EPIF = -1>
 __global__ __launch_bounds__(GatCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void
 gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                  const float* __restrict__ logits, const float* __restrict__ x, int64_t ldx,
@@ -1215,6 +1215,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
                  const float* __restrict__ wlog_next = nullptr, float* __restrict__ lg_next = nullptr) {
     using C = GatCfg<H>;
     constexpr int HEADS = 4;
+    if constexpr (EPIF >= 0) flags = EPIF;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
     int32_t* const QF = reinterpret_cast<int32_t*>(lds + C::OFF_EPI);
     float* const BF = reinterpret_cast<float*>(QF + H);
@@ -1583,12 +1584,14 @@ __global__ __launch_bounds__(256) void tf_prep_frag_kernel(const float* __restri
 // [3][32 KB] (LDS-DMA two chunks ahead, one counted wait + barrier per chunk)
 // | per row TF_XS extra raw scores; after the loop the whole LDS is the
 // staged epilogue's (rows [128][1 KB] | q bias scale shift).
+template <int EPIF = -1>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void tf_fused_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ qt, int64_t ldq, const float* __restrict__ x, int64_t ldx,
     int64_t rb, int64_t re, float score_scale, const unsigned char* __restrict__ img,
     const float* __restrict__ bias, const float* __restrict__ scale,
     const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+    if constexpr (EPIF >= 0) flags = EPIF;
     constexpr int AW = 8, BM = 16 * AW;
     constexpr int WPC = ACHUNK / 1024 / AW;              // W pieces per wave per chunk (4)
     constexpr int OFF_XS = 3 * ACHUNK;
@@ -1915,16 +1918,22 @@ int launch_gat_fused(const int32_t* row_ptr, const int32_t* col, const float* lo
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     const int64_t nb = (ntiles + 7) / 8 * 8;
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "gat_fused: too many rows");
-    if (!L0 && lg_next != nullptr)
-        hipLaunchKernelGGL((gat_fused_kernel<H, false, true>), dim3(static_cast<unsigned>(nb)),
-                           dim3(C::NT), 0, st, row_ptr, col, logits, x, ldx, rb, re, slope,
-                           static_cast<const unsigned char*>(img), bias, scale, shift, flags, out,
-                           ldo, w_in, b_in, lw, d, wlog_next, lg_next);
-    else
-        hipLaunchKernelGGL((gat_fused_kernel<H, L0>), dim3(static_cast<unsigned>(nb)), dim3(C::NT),
-                           0, st, row_ptr, col, logits, x, ldx, rb, re, slope,
-                           static_cast<const unsigned char*>(img), bias, scale, shift, flags, out,
-                           ldo, w_in, b_in, lw, d, nullptr, nullptr);
+    constexpr int kBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE | MIGNN_EPI_RELU;
+    constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
+    auto go = [&](auto kern, const float* wn, float* ln) {
+        hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nb)), dim3(C::NT), 0, st, row_ptr, col,
+                           logits, x, ldx, rb, re, slope, static_cast<const unsigned char*>(img),
+                           bias, scale, shift, flags, out, ldo, w_in, b_in, lw, d, wn, ln);
+    };
+    if (!L0 && lg_next != nullptr) {
+        if (flags == kBN) go(gat_fused_kernel<H, false, true, kBN>, wlog_next, lg_next);
+        else if (flags == kNoBN) go(gat_fused_kernel<H, false, true, kNoBN>, wlog_next, lg_next);
+        else go(gat_fused_kernel<H, false, true>, wlog_next, lg_next);
+    } else {
+        if (flags == kBN) go(gat_fused_kernel<H, L0, false, kBN>, nullptr, nullptr);
+        else if (flags == kNoBN) go(gat_fused_kernel<H, L0, false, kNoBN>, nullptr, nullptr);
+        else go(gat_fused_kernel<H, L0>, nullptr, nullptr);
+    }
     return launch_status("gat_fused_kernel");
 }
 
@@ -2083,9 +2092,16 @@ int tf_fused(const int32_t* row_ptr, const int32_t* col, const float* qt, int64_
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "transformer_layer: too many rows");
     const auto* im = static_cast<const unsigned char*>(img);
     flags |= g_fused_diag_flags;
-hipLaunchKernelGGL(tf_fused_kernel, dim3(static_cast<unsigned>(nb)), dim3(512), 0,
-                       as_stream(stream), row_ptr, col, qt, ldq, x, ldx, rb, re, score_scale, im,
-                       bias, scale, shift, flags, out, ldo);
+    constexpr int kBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE | MIGNN_EPI_RELU;
+    constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nb)), dim3(512), 0, as_stream(stream),
+                           row_ptr, col, qt, ldq, x, ldx, rb, re, score_scale, im, bias, scale,
+                           shift, flags, out, ldo);
+    };
+    if (flags == kBN) go(tf_fused_kernel<kBN>);
+    else if (flags == kNoBN) go(tf_fused_kernel<kNoBN>);
+    else go(tf_fused_kernel<>);
     return launch_status("tf_fused_kernel");
 }
 }  // namespace mignn

@@ -34,7 +34,13 @@ b1 = torch.randn(H, device=dev, generator=g) * 0.05
 b2 = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
-img1, img2 = f16x3_image(W1), gin_fused_image(W2)
+img1, img2 = (f16x3_image(W1), gin_fused_image(W2)) if H == 256 else (None, None)
+if mode == "gat":
+    WLOG = torch.randn(8, H, device=dev, generator=g) / H ** 0.5
+    WCAT = torch.randn(H, 4 * H, device=dev, generator=g) / (2 * H) ** 0.5
+    imgc = f16x3_image(WCAT)
+    GSCR = torch.empty(max(_lib.lib().mignn_gat_layer_scratch_bytes(n, n, H, 4), 1),
+                       dtype=torch.uint8, device=dev)
 libs = {"cur": _lib.lib(),
         "prev": _lib._load(os.path.join(HERE, "gnn-bfs-rans_amd", "mignn", "libmignn_prev.so"),
                            _lib.SIGNATURES)}
@@ -47,6 +53,10 @@ def run(L, Y):
         _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
                                            P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15,
                                            P(Y), H, st), "gin")
+    elif mode == "gat":
+        _lib.check(L.mignn_gat_layer(P(csr.row_ptr), P(csr.col), P(X), H, n, 0, n, H, 4, 0.2,
+                                     P(WLOG), None, 8, P(WCAT), P(imgc), P(b1), P(sc), P(sh), 15,
+                                     P(GSCR), GSCR.numel(), P(Y), H, st), "gat")
     else:
         _lib.check(L.mignn_gcn_layer_fused(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n,
                                            H, P(img1), P(b1), P(sc), P(sh), 15, P(Y), H, st), "gcn")
