@@ -286,7 +286,9 @@ __device__ __forceinline__ void p_load_entries(PIdx& t, const int32_t* __restric
     t.ew = lane < ne ? ew[e0 + lane] : 0.f;
 }
 
-template <int H, int NC>
+// EPIF: the flags at compile time (the model's 15 / 11: no schedule or
+// ablation bits), -1: `flags`
+template <int H, int NC, int EPIF = -1>
 __global__ __launch_bounds__((SCfg<H, NC>::NT)) void gcn_f16x3_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ x, int64_t ldx, int64_t row_begin,
@@ -294,6 +296,7 @@ __global__ __launch_bounds__((SCfg<H, NC>::NT)) void gcn_f16x3_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift, int flags,
     float* __restrict__ out, int64_t ldo, unsigned long long* trace) {
     using C = SCfg<H, NC>;
+    if constexpr (EPIF >= 0) flags = EPIF;
     constexpr int UBE = C::UB;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
     int* const cntX = reinterpret_cast<int*>(lds + C::OFF_CNT);
@@ -894,9 +897,16 @@ int launch_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew, co
     const int64_t ntiles = (re - rb + C::BM - 1) / C::BM;
     int grid = G;
     if (ntiles < grid) grid = static_cast<int>(((ntiles + 7) / 8) * 8);
-    hipLaunchKernelGGL((gcn_f16x3_kernel<H, NC>), dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x,
-                       ldx, rb, re, w, bias, scale, shift, flags, out, ldo,
-                       (flags & MIGNN_DIAG_TRACE) ? g_trace16_host : nullptr);
+    constexpr int kBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE | MIGNN_EPI_RELU;
+    constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(C::NT), 0, st, row_ptr, col, ew, x, ldx, rb, re, w,
+                           bias, scale, shift, flags, out, ldo,
+                           (flags & MIGNN_DIAG_TRACE) ? g_trace16_host : nullptr);
+    };
+    if (flags == kBN) go(gcn_f16x3_kernel<H, NC, kBN>);
+    else if (flags == kNoBN) go(gcn_f16x3_kernel<H, NC, kNoBN>);
+    else go(gcn_f16x3_kernel<H, NC>);
     return launch_status("gcn_f16x3_kernel");
 }
 

@@ -19,7 +19,7 @@ from mignn.synthetic import grid_graph  # noqa: E402
 
 dev = torch.device("cuda", 0)
 mode = os.environ.get("AB_MODE", "gin")
-H = 128 if mode == "gat" else 256
+H = int(os.environ.get("AB_H", "128")) if mode in ("gat", "pc", "ring") else 256
 nx, ny, nz = (int(v) for v in os.environ.get("AB_GRID", "500,400,63").split(","))
 pos, ei = grid_graph(nx, ny, nz, device=dev)
 n = pos.shape[0]
@@ -53,6 +53,14 @@ def run(L, Y):
         _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
                                            P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15,
                                            P(Y), H, st), "gin")
+    elif mode == "pc":
+        _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
+                                           P(W1), P(b1), P(sc), P(sh), 15, P(Y),
+                                           H, st), "pc")
+    elif mode == "ring":
+        _lib.check(L.mignn_gcn_layer_ring(P(RPLAN), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
+                                          0, n, H, P(W1), P(b1), P(sc), P(sh), 15, P(Y), H, st),
+                   "ring")
     elif mode == "gat":
         _lib.check(L.mignn_gat_layer(P(csr.row_ptr), P(csr.col), P(X), H, n, 0, n, H, 4, 0.2,
                                      P(WLOG), None, 8, P(WCAT), P(imgc), P(b1), P(sc), P(sh), 15,
@@ -62,6 +70,11 @@ def run(L, Y):
                                            H, P(img1), P(b1), P(sc), P(sh), 15, P(Y), H, st), "gcn")
 
 
+if mode == "ring":
+    nbr = _lib.lib().mignn_gcn_ring_plan_bytes(0, n, H)
+    RPLAN = torch.empty(nbr, dtype=torch.uint8, device=dev)
+    _lib.check(_lib.lib().mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H,
+                                              P(RPLAN), nbr, None, st), "rplan")
 Ys = {k: torch.empty_like(X) for k in libs}
 for k, L in libs.items():
     run(L, Ys[k])
