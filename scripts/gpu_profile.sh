@@ -8,6 +8,6 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 [ -n "${SKIP_STATS:-}" ] || timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv \
     -- python bench.py --steps 5 --warmup 2 --no-cpu --no-bfs --no-train > gpurun_out/prof.log 2>&1
 rc=$?; echo "rocprof stats rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/prof.log; exit $rc; fi
-BENCH_ARGS="--steps 3 --warmup 1 --no-cpu --no-bfs --no-legs --no-train --no-graph" bash scripts/pmc.sh
+BENCH_ARGS="--steps 3 --warmup 1 --no-cpu --no-bfs --no-legs --no-train --no-graph --no-config4" bash scripts/pmc.sh
 rc=$?; if [ $rc -ne 0 ]; then exit $rc; fi
-BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-bfs --no-train --no-graph" bash scripts/pmc_sq.sh
+[ -n "${SKIP_SQ:-}" ] || BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-bfs --no-train --no-graph" bash scripts/pmc_sq.sh
