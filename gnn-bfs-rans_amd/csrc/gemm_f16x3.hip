@@ -151,12 +151,16 @@ __device__ __forceinline__ void load_a8(const float* __restrict__ A, int64_t lda
     }
 }
 
+// EPIF: the flags at compile time (the callers' common sets, no diagnostic
+// bits), -1: `flags`
+template <int EPIF = -1>
 __global__ __launch_bounds__(GNT, RPW == 1 ? 2 : 1) void gemm_f16x3_kernel(
     const float* __restrict__ A, int64_t lda, int64_t M, int k1, const float* __restrict__ A2,
     int64_t lda2, int K, const unsigned char* __restrict__ img, int kp, int npb, int N,
     const float* __restrict__ bias, const float* __restrict__ R, int64_t ldr,
     const float* __restrict__ scale, const float* __restrict__ shift, int flags,
     float* __restrict__ C, int64_t ldc, int64_t ntiles_m, int ntiles_n) {
+    if constexpr (EPIF >= 0) flags = EPIF;
     __shared__ __attribute__((aligned(16))) unsigned char lds[2 * CHUNK_BYTES + GBN * 16];
     const int tid = threadIdx.x;
     int lane = tid & 63;
@@ -487,10 +491,22 @@ static int linear_f16x3_impl(const float* a, int64_t lda, int64_t m, int k1,
     const int tnr = npb / CBT;
     int64_t nb = ((tmr * tnr + 7) / 8) * 8;
     MIGNN_REQUIRE(nb < (int64_t(1) << 31), "linear_f16x3: m too large");
-    hipLaunchKernelGGL(gemm_f16x3_kernel, dim3(static_cast<unsigned>(nb)), dim3(GNT), 0,
-                       as_stream(stream), a, lda, m, k1, k2 ? a2 : a, lda2, K,
-                       static_cast<const unsigned char*>(img), kp, npb, n, bias, residual, ldr,
-                       scale, shift, flags, c, ldc, tmr, tnr);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nb)), dim3(GNT), 0, as_stream(stream), a,
+                           lda, m, k1, k2 ? a2 : a, lda2, K, static_cast<const unsigned char*>(img),
+                           kp, npb, n, bias, residual, ldr, scale, shift, flags, c, ldc, tmr, tnr);
+    };
+    constexpr int kB = MIGNN_EPI_BIAS, kBR = MIGNN_EPI_BIAS | MIGNN_EPI_RELU;
+    constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
+    constexpr int kBN = kNoBN | MIGNN_EPI_AFFINE;
+    switch (flags) {
+        case 0: go(gemm_f16x3_kernel<0>); break;
+        case kB: go(gemm_f16x3_kernel<kB>); break;
+        case kBR: go(gemm_f16x3_kernel<kBR>); break;
+        case kNoBN: go(gemm_f16x3_kernel<kNoBN>); break;
+        case kBN: go(gemm_f16x3_kernel<kBN>); break;
+        default: go(gemm_f16x3_kernel<>); break;
+    }
     return launch_status("gemm_f16x3_kernel");
 }
 

@@ -53,6 +53,9 @@ def run(L, Y):
         _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
                                            P(img1), P(b1), P(img2), P(b2), P(sc), P(sh), 15,
                                            P(Y), H, st), "gin")
+    elif mode == "gemm":
+        _lib.check(L.mignn_linear_f16x3(P(X), H, n, H, None, 0, 0, P(GIMG), GN, P(GB), None, 0,
+                                        None, None, 1, P(Y), GN, st), "gemm")
     elif mode == "pc":
         _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                            P(W1), P(b1), P(sc), P(sh), 15, P(Y),
@@ -75,7 +78,15 @@ if mode == "ring":
     RPLAN = torch.empty(nbr, dtype=torch.uint8, device=dev)
     _lib.check(_lib.lib().mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H,
                                               P(RPLAN), nbr, None, st), "rplan")
-Ys = {k: torch.empty_like(X) for k in libs}
+if mode == "gemm":
+    # TransformerConv's Q~K shape: [n, 256] x [256 -> 4 x 256] + bias
+    GN = 4 * H
+    GW = torch.randn(GN, H, device=dev, generator=g) / 16
+    GB = torch.randn(GN, device=dev, generator=g) * 0.05
+    GIMG = f16x3_image(GW)
+    Ys = {k: torch.empty((n, GN), device=dev) for k in libs}
+else:
+    Ys = {k: torch.empty_like(X) for k in libs}
 for k, L in libs.items():
     run(L, Ys[k])
 torch.cuda.synchronize()
