@@ -56,6 +56,10 @@ def run(L, Y):
     elif mode == "gemm":
         _lib.check(L.mignn_linear_f16x3(P(X), H, n, H, None, 0, 0, P(GIMG), GN, P(GB), None, 0,
                                         None, None, 1, P(Y), GN, st), "gemm")
+    elif mode == "tf":
+        _lib.check(L.mignn_transformer_layer_fused(
+            P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 4, 1.0 / H ** 0.5, P(TQIMG), P(TBQ),
+            P(TFIMG), P(TBO), P(sc), P(sh), 15, P(TSCR), TSCR.numel(), P(Y), H, st), "tf")
     elif mode == "pc":
         _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                            P(W1), P(b1), P(sc), P(sh), 15, P(Y),
@@ -78,6 +82,29 @@ if mode == "ring":
     RPLAN = torch.empty(nbr, dtype=torch.uint8, device=dev)
     _lib.check(_lib.lib().mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H,
                                               P(RPLAN), nbr, None, st), "rplan")
+if mode == "tf":
+    TWQ = torch.randn(4 * H + 4, H, device=dev, generator=g) / 16
+    TBQ = torch.randn(4 * H + 4, device=dev, generator=g) * 0.05
+    TWO = torch.randn(H, 4 * H + 4 + H, device=dev, generator=g) / 32
+    TBO = torch.randn(H, device=dev, generator=g) * 0.05
+    TQIMG = f16x3_image(TWQ)
+    Lc = _lib.lib()
+    TFIMG = torch.empty(Lc.mignn_transformer_fused_prep_bytes(H, 4), dtype=torch.uint8, device=dev)
+    _lib.check(Lc.mignn_transformer_fused_prep(P(TWO), H, 4, P(TFIMG), TFIMG.numel(), st), "prep")
+    TSCR = torch.empty(Lc.mignn_transformer_layer_scratch_bytes(n, H, 4), dtype=torch.uint8,
+                       device=dev)
+if mode == "tf":
+    TWQ = torch.randn(4 * H + 4, H, device=dev, generator=g) / 16
+    TBQ = torch.randn(4 * H + 4, device=dev, generator=g) * 0.05
+    TWO = torch.randn(H, 4 * H + 4 + H, device=dev, generator=g) / 32
+    TBO = torch.randn(H, device=dev, generator=g) * 0.05
+    TQIMG = f16x3_image(TWQ)
+    Lc = _lib.lib()
+    TFIMG = torch.empty(Lc.mignn_transformer_fused_prep_bytes(H, 4), dtype=torch.uint8, device=dev)
+    _lib.check(Lc.mignn_transformer_fused_prep(P(TWO), H, 4, P(TFIMG), TFIMG.numel(), st), "prep")
+    TSCR = torch.empty(Lc.mignn_transformer_layer_scratch_bytes(n, H, 4), dtype=torch.uint8,
+                       device=dev)
+
 if mode == "gemm":
     # TransformerConv's Q~K shape: [n, 256] x [256 -> 4 x 256] + bias
     GN = 4 * H
