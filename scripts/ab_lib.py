@@ -93,17 +93,6 @@ if mode == "tf":
     _lib.check(Lc.mignn_transformer_fused_prep(P(TWO), H, 4, P(TFIMG), TFIMG.numel(), st), "prep")
     TSCR = torch.empty(Lc.mignn_transformer_layer_scratch_bytes(n, H, 4), dtype=torch.uint8,
                        device=dev)
-if mode == "tf":
-    TWQ = torch.randn(4 * H + 4, H, device=dev, generator=g) / 16
-    TBQ = torch.randn(4 * H + 4, device=dev, generator=g) * 0.05
-    TWO = torch.randn(H, 4 * H + 4 + H, device=dev, generator=g) / 32
-    TBO = torch.randn(H, device=dev, generator=g) * 0.05
-    TQIMG = f16x3_image(TWQ)
-    Lc = _lib.lib()
-    TFIMG = torch.empty(Lc.mignn_transformer_fused_prep_bytes(H, 4), dtype=torch.uint8, device=dev)
-    _lib.check(Lc.mignn_transformer_fused_prep(P(TWO), H, 4, P(TFIMG), TFIMG.numel(), st), "prep")
-    TSCR = torch.empty(Lc.mignn_transformer_layer_scratch_bytes(n, H, 4), dtype=torch.uint8,
-                       device=dev)
 
 if mode == "gemm":
     # TransformerConv's Q~K shape: [n, 256] x [256 -> 4 x 256] + bias
