@@ -367,6 +367,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
     for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     int p = 100;                                   // the row's running exponent
+    bool fresh = true;                             // (the row's first chunk not seen yet)
     const unsigned char* const wl0 = lds + lane * 16;
 
     // ---------------------------------------------------------------- transform 1
@@ -440,13 +441,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
         for (int i = 0; i < 4; ++i)
             m = max(m, max(__float_as_uint(fabsf(a0[i])), __float_as_uint(fabsf(a1[i]))));
         const int pc = sexp_ag(rowmax4(m));
-        if (pc < p) {                              // lower the row's scale: exact rescale
+        // the row's first nonzero chunk sets the scale with 2 bits of headroom
+        // (accumulators still zero: nothing to rescale), so later chunks
+        // rarely lower it; a lowering is a uniform branch, exact rescale
+        if (fresh) p = pc - 2;
+        if (!fresh && __builtin_amdgcn_ballot_w64(pc < p) != 0ull) {
+            const int dp = pc < p ? pc - p : 0;
 #pragma unroll
             for (int cb = 0; cb < ACB; ++cb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
-            p = pc;
+                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], dp);
+            p = pc < p ? pc : p;
         }
+        fresh = false;
         const float spv = p2_ag(p);
         f16x8 bh, bl;
 #pragma unroll
@@ -627,6 +634,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
 #pragma unroll
     for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     int p = 100;
+    bool fresh = true;                             // (the row's first chunk not seen yet)
     const unsigned char* const wl0 = lds + lane * 16;
     auto mfma3 = [&](const unsigned char* wb, const f16x8& bh, const f16x8& bl) {
 #pragma unroll
@@ -652,13 +660,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
             m = max(m, __float_as_uint(fabsf(a[j])));
         }
         const int pc = sexp_ag(rowmax4(m));
-        if (pc < p) {
+        // the row's first nonzero chunk sets the scale with 2 bits of headroom
+        // (accumulators still zero: nothing to rescale), so later chunks
+        // rarely lower it; a lowering is a uniform branch, exact rescale
+        if (fresh) p = pc - 2;
+        if (!fresh && __builtin_amdgcn_ballot_w64(pc < p) != 0ull) {
+            const int dp = pc < p ? pc - p : 0;
 #pragma unroll
             for (int cb = 0; cb < ACB; ++cb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
-            p = pc;
+                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], dp);
+            p = pc < p ? pc : p;
         }
+        fresh = false;
         const float spv = p2_ag(p);
         f16x8 bh, bl;
 #pragma unroll
@@ -1030,6 +1044,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
 #pragma unroll
     for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     int p = 100;
+    bool fresh = true;                             // (the row's first chunk not seen yet)
     const unsigned char* const wl0 = lds + lane * 16;
     auto mfma3 = [&](const unsigned char* wb, int ncb, const f16x8& bh, const f16x8& bl) {
 #pragma unroll
@@ -1055,13 +1070,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
         for (int i = 0; i < 4; ++i)
             m = max(m, max(__float_as_uint(fabsf(cur[0][i])), __float_as_uint(fabsf(cur[1][i]))));
         const int pc = sexp_ag(rowmax4(m));
-        if (pc < p) {
+        // the row's first nonzero chunk sets the scale with 2 bits of headroom
+        // (accumulators still zero: nothing to rescale), so later chunks
+        // rarely lower it; a lowering is a uniform branch, exact rescale
+        if (fresh) p = pc - 2;
+        if (!fresh && __builtin_amdgcn_ballot_w64(pc < p) != 0ull) {
+            const int dp = pc < p ? pc - p : 0;
 #pragma unroll
             for (int cb = 0; cb < ACB; ++cb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
-            p = pc;
+                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], dp);
+            p = pc < p ? pc : p;
         }
+        fresh = false;
         const float spv = p2_ag(p);
         f16x8 bh, bl;
 #pragma unroll
@@ -1395,6 +1416,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
 #pragma unroll
     for (int cb = 0; cb < C::NCB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     int p = 100;
+    bool fresh = true;                             // (the row's first chunk not seen yet)
     const unsigned char* const wl0 = lds + lane * 16;
 
 #pragma unroll 1
@@ -1462,13 +1484,19 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
             for (int i = 0; i < 4; ++i)
                 m = max(m, max(__float_as_uint(fabsf(a[k][0][i])), __float_as_uint(fabsf(a[k][1][i]))));
             const int pc = sexp_ag(rowmax4(m));
-            if (pc < p) {
+            // the row's first nonzero chunk sets the scale with 2 bits of headroom
+            // (accumulators still zero: nothing to rescale), so later chunks
+            // rarely lower it; a lowering is a uniform branch, exact rescale
+            if (fresh) p = pc - 2;
+            if (!fresh && __builtin_amdgcn_ballot_w64(pc < p) != 0ull) {
+                const int dp = pc < p ? pc - p : 0;
 #pragma unroll
                 for (int cb = 0; cb < C::NCB; ++cb)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
-                p = pc;
+                    for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], dp);
+                p = pc < p ? pc : p;
             }
+            fresh = false;
             const float spv = p2_ag(p);
             f16x8 bh, bl;
 #pragma unroll
@@ -1767,6 +1795,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
 #pragma unroll
     for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     int p = 100;
+    bool fresh = true;                             // (the row's first chunk not seen yet)
     int c = 0;
     const unsigned char* const wl0 = lds + lane * 16;
     auto step = [&](const f32x4& a0, const f32x4& a1) {
@@ -1776,13 +1805,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
         for (int i = 0; i < 4; ++i)
             mb = max(mb, max(__float_as_uint(fabsf(a0[i])), __float_as_uint(fabsf(a1[i]))));
         const int pc = sexp_ag(rowmax4(mb));
-        if (pc < p) {
+        // the row's first nonzero chunk sets the scale with 2 bits of headroom
+        // (accumulators still zero: nothing to rescale), so later chunks
+        // rarely lower it; a lowering is a uniform branch, exact rescale
+        if (fresh) p = pc - 2;
+        if (!fresh && __builtin_amdgcn_ballot_w64(pc < p) != 0ull) {
+            const int dp = pc < p ? pc - p : 0;
 #pragma unroll
             for (int cb = 0; cb < ACB; ++cb)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], pc - p);
-            p = pc;
+                for (int i = 0; i < 4; ++i) acc[cb][i] = ldexpf(acc[cb][i], dp);
+            p = pc < p ? pc : p;
         }
+        fresh = false;
         const float spv = p2_ag(p);
         f16x8 bh, bl;
 #pragma unroll
