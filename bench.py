@@ -327,8 +327,9 @@ def main():
                                     "columns, mignn_locality_order; part of the per-step graph "
                                     "setup)" if world == 1 else
                                     "locality order inside each rank's range, interior rows "
-                                    "first (built once per partition; the rank-local CSR is "
-                                    "rebuilt every step)")
+                                    "first; the partition layout (ghost / send lists, the "
+                                    "order) and the rank-local CSR are rebuilt inside every "
+                                    "timed step, as the N = 1 step rebuilds its CSR and order")
                                    if model._use_reorder(x) else "as given",
         },
         "roofline": roofline,

@@ -449,6 +449,10 @@ class FlowGNN(nn.Module):
         #   fused256        H = 256 fused layer / head kernels: "1", "0",
         #                   "layer" or "head" (MIGNN_FUSED256)
         self.fuse_layer0 = os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1"
+        # after every eval forward, read the device's sticky in-kernel error word
+        # and raise if a bounded wait ran out (costs a device sync; off by
+        # default -- bench.py and the tests check it themselves)
+        self.check_device_errors = os.environ.get("MIGNN_CHECK_ERRORS", "0") == "1"
         self.gat_coords = os.environ.get("MIGNN_GAT_COORDS", "1") == "1"
         self.gat_next_logits = os.environ.get("MIGNN_GAT_NEXT_LOGITS", "1") == "1"
         self.fused256 = os.environ.get("MIGNN_FUSED256", "1")
@@ -526,6 +530,8 @@ class FlowGNN(nn.Module):
                 raise self._layer_error(i, e, num_nodes, edge_index, cur, edge_attr) from e
             cur, nxt = nxt, cur
         self._output_mlp(cur, nxt, out, rows=csr.perm, inv=csr.inv)
+        if self.check_device_errors:
+            _lib.check_device_errors("FlowGNN.forward")
         return out
 
     # ------------------------------------------------------------- internals

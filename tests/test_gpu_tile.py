@@ -310,3 +310,20 @@ def test_model_gcn_kernel_routes_agree(H, reorder):
         assert (ys[kern] - ys["pc"]).abs().max().item() <= 2e-6 * scale, kern
     ref = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
     assert (ys["ring"].cpu().double() - ref).abs().max().item() <= 1e-5 * scale
+
+
+def test_forward_device_error_check_opt_in():
+    """FlowGNN.check_device_errors (MIGNN_CHECK_ERRORS=1): the forward reads
+    the device's sticky error word after the last kernel and raises on a
+    nonzero word; a clean forward returns normally and leaves the word clear."""
+    from mignn import FlowGNN
+    from mignn.synthetic import seeded_state_dict
+    m = FlowGNN(input_dim=3, output_dim=7, hidden_dim=128, num_layers=3, layer_type="GCN")
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=2))
+    m = m.to(DEV).eval()
+    m.check_device_errors = True
+    x, ei = grid_graph(20, 16, 12, device=DEV)
+    with torch.no_grad():
+        y = m(x, ei)
+    assert torch.isfinite(y).all()
+    assert _lib.device_errors(clear=True) == 0
