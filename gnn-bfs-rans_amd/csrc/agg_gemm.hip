@@ -62,6 +62,11 @@ __device__ __forceinline__ int sexp_ag(uint32_t mbits) {
 __device__ __forceinline__ float p2_ag(int p) {
     return __uint_as_float(static_cast<uint32_t>(p + 127) << 23);
 }
+// 2^-q for q in [-126, 126] in one v_mad_i32_i24 (the per-column unscale of
+// a split image: acc 2^-q is exact, so acc 2^-q 2^-p rounds like ldexp)
+__device__ __forceinline__ float p2neg_ag(int q) {
+    return __uint_as_float(static_cast<uint32_t>(__mul24(q, -8388608) + 0x3f800000));
+}
 __device__ __forceinline__ uint32_t lds_addr_ag(const unsigned char* p) {
     return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_ag)(p)));
 }
@@ -117,7 +122,7 @@ __device__ __forceinline__ float rowsum4(float v) {
 // NCB*4 values -- row lself, columns 16 cb + 4 g + i: bias, residual, BN, ReLU
 // (gnn_model.py:184-191 order: conv + bias, + x, BN, ReLU) -- in place, and
 // the wave stores whole rows (the accumulator layout would store 16 rows x
-// 64 B per instruction).  EV = [q (int) | bias | scale | shift][NCB*16] in LDS,
+// 64 B per instruction).  EV = [2^-q | bias (0: off) | scale | shift][NCB*16] in LDS,
 // written by the caller before the call.
 // CRES: the residual is not read but computed, x_i[n] = TB[n] . (c0, c1, c2, 1)
 // (GIN layer 0 from the coordinates: x = input_proj(pos), TB = [W_in | b_in])
@@ -141,15 +146,21 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
     if (res && !CRES) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int li = 16 * wave + RPI * i + ri;
-            int64_t rr = t0 + li;
-            if (rr >= re) rr = re - 1;
-            glds16_ag(x + rr * ldx + 4 * (ci ^ (li & 15)), lds_addr_ag(STG + (16 * wave + RPI * i) * ROWB));
+            if constexpr (RPI == 1) {          // one row per instruction: scalar row address
+                int64_t rr = t0 + 16 * wave + i;
+                if (rr >= re) rr = re - 1;
+                glds16_ag(x + rr * ldx + 4 * (l ^ i), lds_addr_ag(STG + (16 * wave + i) * ROWB));
+            } else {
+                const int li = 16 * wave + RPI * i + ri;
+                int64_t rr = t0 + li;
+                if (rr >= re) rr = re - 1;
+                glds16_ag(x + rr * ldx + 4 * (ci ^ (li & 15)), lds_addr_ag(STG + (16 * wave + RPI * i) * ROWB));
+            }
         }
     }
     vm_barrier<0>();                           // (EV of every wave; this wave's rows landed)
     unsigned char* const srow = STG + lself * ROWB;
-    const int32_t* const EQ = reinterpret_cast<const int32_t*>(EV);
+    const float spr = p2_ag(-p);               // the row's 2^-p (p in [-116, 100])
     float lp[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
@@ -167,15 +178,17 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
         } else if (res) {
             xv = *slot;
         }
-        const int4 q = *reinterpret_cast<const int4*>(EQ + n);
+        const f32x4 sq = *reinterpret_cast<const f32x4*>(EV + n);
         const f32x4 bo = *reinterpret_cast<const f32x4*>(EV + N + n);
         const f32x4 so = *reinterpret_cast<const f32x4*>(EV + 2 * N + n);
         const f32x4 ho = *reinterpret_cast<const f32x4*>(EV + 3 * N + n);
-        const int qn[4] = {q.x, q.y, q.z, q.w};
         f32x4 o;
+        // acc 2^-q exact (= the output 2^p), times 2^-p exact, + bias (0 when
+        // the flag is off) rounded once: ldexp(acc, -(p + q)) + bias
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            o[i] = epilogue(ldexpf(acc[cb][i], -(p + qn[i])), flags, bo[i], xv[i], so[i], ho[i]);
+            o[i] = epilogue(fmaf(acc[cb][i] * sq[i], spr, bo[i]), flags & ~MIGNN_EPI_BIAS, 0.f,
+                            xv[i], so[i], ho[i]);
         *slot = o;
     }
     if constexpr (LG) {
@@ -201,12 +214,25 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
         }
     }
     // this wave's rows out (its own staging rows: in-order LDS)
+    if constexpr (RPI == 1) {                  // ((16 wave + i) & 15 == i; the row is uniform)
+        f32x4 v[NI];                           // (every read issued before the first store)
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        const int li = 16 * wave + RPI * i + ri;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(STG + li * ROWB + ci * 16);
-        if (t0 + li < re)
-            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + li) * ldo + 4 * (ci ^ (li & 15))));
+        for (int i = 0; i < NI; ++i)
+            v[i] = *reinterpret_cast<const f32x4*>(STG + (16 * wave + i) * ROWB + l * 16);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int64_t rr = t0 + 16 * wave + i;
+            if (rr < re)
+                __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + rr * ldo + 4 * (l ^ i)));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int li = 16 * wave + RPI * i + ri;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(STG + li * ROWB + ci * 16);
+            if (t0 + li < re)
+                __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + (t0 + li) * ldo + 4 * (ci ^ (li & 15))));
+        }
     }
 }
 
@@ -480,6 +506,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
         // h = relu(acc 2^-(p + q1) + b1) in the accumulator layout: lane (r, g)
         // holds h[r][16 cb + 4 g + i]; one exponent per row over all 256
         const int32_t* const q1 = reinterpret_cast<const int32_t*>(img1 + FB);
+        const float spr1 = p2_ag(-p);
         uint32_t m = 0;
 #pragma unroll
         for (int cb = 0; cb < ACB; ++cb) {
@@ -488,10 +515,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
             const int qn[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                float h = ldexpf(acc[cb][i], -(p + qn[i])) + bb[i];
-                h = h < 0.f ? 0.f : h;
+                // (the staged epilogue's unscale; h >= +0 or NaN: its bits are the max key)
+                const float h = __builtin_elementwise_maximum(
+                    fmaf(acc[cb][i] * p2neg_ag(qn[i]), spr1, bb[i]), 0.f);
                 acc[cb][i] = h;
-                m = max(m, __float_as_uint(fabsf(h)));
+                m = max(m, __float_as_uint(h));
             }
         }
         p = sexp_ag(rowmax4(m));
@@ -544,7 +572,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     if (tid < AH) {
         const int32_t* const qf = reinterpret_cast<const int32_t*>((CHAIN ? img2 : img1) + FB);
         const float* const bf = CHAIN ? b2 : b1;
-        reinterpret_cast<int32_t*>(EV)[tid] = qf[tid];
+        EV[tid] = p2neg_ag(qf[tid]);
         EV[AH + tid] = hb ? bf[tid] : 0.f;
         EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
         EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
@@ -687,6 +715,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
     // ---- nn.2 over h = relu(acc 2^-(p + q1) + b1) from the accumulators (k-permuted W2)
     {
         const int32_t* const q1 = reinterpret_cast<const int32_t*>(img1 + FB);
+        const float spr1 = p2_ag(-p);
         uint32_t m = 0;
 #pragma unroll
         for (int cb = 0; cb < ACB; ++cb) {
@@ -695,10 +724,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
             const int qn[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                float h = ldexpf(acc[cb][i], -(p + qn[i])) + bb[i];
-                h = h < 0.f ? 0.f : h;
+                // (the staged epilogue's unscale; h >= +0 or NaN: its bits are the max key)
+                const float h = __builtin_elementwise_maximum(
+                    fmaf(acc[cb][i] * p2neg_ag(qn[i]), spr1, bb[i]), 0.f);
                 acc[cb][i] = h;
-                m = max(m, __float_as_uint(fabsf(h)));
+                m = max(m, __float_as_uint(h));
             }
         }
         p = sexp_ag(rowmax4(m));
@@ -727,7 +757,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
     const bool hb = (flags & MIGNN_EPI_BIAS) != 0, ha = (flags & MIGNN_EPI_AFFINE) != 0;
     float* const EV = reinterpret_cast<float*>(lds + OFF_EV);
     if (tid < AH) {
-        reinterpret_cast<int32_t*>(EV)[tid] = reinterpret_cast<const int32_t*>(img2 + FB)[tid];
+        EV[tid] = p2neg_ag(reinterpret_cast<const int32_t*>(img2 + FB)[tid]);
         EV[AH + tid] = hb ? b2[tid] : 0.f;
         EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
         EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
@@ -1103,6 +1133,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
     f16x8 hh[AKP], hl[AKP];
     auto relu_split = [&](int t, int ncb, const float* bias) {
         const int32_t* const q = reinterpret_cast<const int32_t*>(img + t * HIMG + HIMG - AH * 4);
+        const float spr1 = p2_ag(-p);
         uint32_t m = 0;
 #pragma unroll
         for (int cb = 0; cb < ACB; ++cb) {
@@ -1112,10 +1143,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
             const int qn[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                float h = ldexpf(acc[cb][i], -(p + qn[i])) + bb[i];
-                h = h < 0.f ? 0.f : h;
+                // (the staged epilogue's unscale; h >= +0 or NaN: its bits are the max key)
+                const float h = __builtin_elementwise_maximum(
+                    fmaf(acc[cb][i] * p2neg_ag(qn[i]), spr1, bb[i]), 0.f);
                 acc[cb][i] = h;
-                m = max(m, __float_as_uint(fabsf(h)));
+                m = max(m, __float_as_uint(h));
             }
         }
         p = sexp_ag(rowmax4(m));
@@ -1530,7 +1562,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     }
     float* const EV2 = reinterpret_cast<float*>(lds + C::BM * H * 4);
     if (tid < H) {
-        reinterpret_cast<int32_t*>(EV2)[tid] = QF[tid];
+        EV2[tid] = p2neg_ag(QF[tid]);
         EV2[H + tid] = BF[tid];
         EV2[2 * H + tid] = SC[tid];
         EV2[3 * H + tid] = SH[tid];
@@ -1909,7 +1941,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void t
     const bool hb = (flags & MIGNN_EPI_BIAS) != 0, ha = (flags & MIGNN_EPI_AFFINE) != 0;
     float* const EV = reinterpret_cast<float*>(lds + BM * 1024);   // q | bias | scale | shift
     if (tid < AH) {
-        reinterpret_cast<int32_t*>(EV)[tid] = reinterpret_cast<const int32_t*>(img + TF_IMG_FRAG)[tid];
+        EV[tid] = p2neg_ag(reinterpret_cast<const int32_t*>(img + TF_IMG_FRAG)[tid]);
         EV[AH + tid] = hb ? bias[tid] : 0.f;
         EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
         EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
