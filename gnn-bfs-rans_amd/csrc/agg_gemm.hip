@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const float h = ldexpf(acc[cb][i], -(p + qn[i])) + bb[i];
-            h3[cb][i] = h < 0.f ? 0.f : h;
+            h3[cb][i] = relu_nan(h);
         }
     }
     float o[8];

@@ -142,13 +142,16 @@ __device__ __forceinline__ float4 fma4(float s, float4 x, float4 acc) {
 
 // Reference epilogue order (gnn_model.py:184-191 with the conv bias first):
 //   v = acc + bias; v = residual + v; v = v*scale + shift; relu.
+// ReLU in one v_maximum3_f32: NaN-propagating, like torch.relu (-0 -> +0)
+__device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.0f); }
+
 __device__ __forceinline__ float epilogue(float acc, int flags, float bias, float res, float sc,
                                           float sh) {
     float v = acc;
     if (flags & MIGNN_EPI_BIAS) v = v + bias;
     if (flags & MIGNN_EPI_RESIDUAL) v = res + v;
     if (flags & MIGNN_EPI_AFFINE) v = v * sc + sh;
-    if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;  // NaN-propagating, like torch.relu
+    if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
     return v;
 }
 

@@ -840,7 +840,7 @@ __global__ __launch_bounds__((SCfg<H, NC>::NT)) void gcn_f16x3_kernel(
                     for (int r = 0; r < 4; ++r) {
                         float v = ldexpf(acc[ib][jb][r], -(pr[ib] + qw));
                         if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                        if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
+                        if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
                         o[r] = v;
                     }
                     const int lr = (wm * C::IB + ib) * 16 + rr;

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
                         float t = cf[q][K - 1];
 #pragma unroll
                         for (int k = 0; k < K - 1; ++k) t = fmaf(cf[q][k], v[k], t);
-                        o[q] = t < 0.f ? 0.f : t;
+                        o[q] = relu_nan(t);
                     }
                     __builtin_nontemporal_store(
                         f32x4{o[0], o[1], o[2], o[3]},

@@ -867,7 +867,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
                     for (int r = 0; r < 4; ++r) {
                         float v = ldexpf(accm[cb][ib][r], -(pr[ib] + qw[cb]));
                         if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                        if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
+                        if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
                         o[r] = v;
                     }
                     const int lr = (wm * IBW + ib) * 16 + rr;
@@ -893,7 +893,7 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
                 for (int r = 0; r < 4; ++r) {
                     float v = ldexpf(accm[cb][ib][r], -(pr[ib] + qw[cb]));
                     if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                    if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
+                    if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
                     o[r] = v;
                 }
                 const int lr = (wm * IBW + ib) * 16 + rr;

@@ -653,7 +653,7 @@ __global__ __launch_bounds__((TCfg<H, AGG>::NT), (TCfg<H, AGG>::WG_PER_CU)) void
                     for (int r = 0; r < 4; ++r) {
                         float v = ldexpf(accm[ib][jb][r], -(pr[ib] + qw));
                         if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                        if (flags & MIGNN_EPI_RELU) v = v < 0.0f ? 0.0f : v;
+                        if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
                         o[r] = v;
                     }
                     const int lr = ib * 16 + rr;

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void narrow_linear_kernel(const float* __restr
                 if (o < n) {
                     float y = v[o];
                     if (flags & MIGNN_EPI_BIAS) y += bias[o];
-                    if (flags & MIGNN_EPI_RELU) y = y < 0.f ? 0.f : y;
+                    if (flags & MIGNN_EPI_RELU) y = relu_nan(y);
                     c[row * ldc + o] = y;
                 }
         }
