@@ -108,6 +108,17 @@ __device__ __forceinline__ void vm_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier, N < 64 (vmcnt bits 3:0 and 15:14;
+// N = 63: LDS reads only)
+template <int N>
+__device__ __forceinline__ void vm_barrier64() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // sum over the 4 lanes of a row (every lane gets the same value)
 __device__ __forceinline__ float rowsum4(float v) {
     const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -1230,16 +1241,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
 // the row's online exponent, 3 MFMAs per 16x16x32 block.  The 4 W chunks of
 // an x chunk (4 x H/16 column blocks of the linear_f16x3 image of Wcat
 // [H, 4H]) are LDS-DMA'd together, double-buffered, one barrier per x chunk.
+#ifndef GAT_AW
+#define GAT_AW 4
+#endif
 template <int H>
 struct GatCfg {
     static_assert(H == 64 || H == 128, "gat_fused: H in {64, 128}");
-    static constexpr int AW = 8, NT = AW * 64, BM = 16 * AW;
+    // 4 waves x 16 rows per block, two blocks per CU: one block's dependent
+    // CSR -> logit -> row loads run under the other's MFMAs (8 waves x 16
+    // rows, one block per CU: 1.10 ms per 1M-node H = 128 layer)
+    static constexpr int AW = GAT_AW, NT = AW * 64, BM = 16 * AW;
     static constexpr int NCB = H / 16;                 // output column blocks (N = H)
     static constexpr int XC = H / 32;                  // x chunks
     static constexpr int NPB = 16;                     // column blocks per image chunk (padded)
     static constexpr int WCH = NCB * 2 * AFRAG;        // real bytes of one W chunk
     static constexpr int STEPW = 4 * WCH;              // the 4 heads' chunks of one x chunk
-    static constexpr int OFF_AL = 2 * STEPW;           // alphas [AW][16][4][8]
+    static constexpr int REST = AW * 16 * 4 * 8 * 4 + AW * 16 * 4 * 8 + 4 * H * 4 + H * 16;
+    // W buffers: 2 (next step's chunks in flight) unless that leaves no room
+    // for a second block on the CU (H = 128 with 4 waves: 1, refilled after
+    // the step's MFMAs; the other block covers the wait)
+    static constexpr int WB = (AW == 4 && 2 * STEPW + REST > 80 * 1024) ? 1 : 2;
+    static constexpr int OFF_AL = WB * STEPW;          // alphas [AW][16][4][8]
     static constexpr int OFF_ST = OFF_AL + AW * 16 * 4 * 8 * 4;   // (max, sum) [AW][16][4]
     static constexpr int OFF_EPI = OFF_ST + AW * 16 * 4 * 8;       // QF | BF | SC | SH [H]
     static constexpr int OFF_TB = OFF_EPI + 4 * H * 4;  // (layer 0) [W_in | b_in] [H][4]
@@ -1291,7 +1313,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     // W chunks of x chunk t (heads 0..3: image chunks k XC + t) -> buffer t & 1
     auto w_dma = [&](int t) {
         if (t >= C::XC || (flags & MIGNN_SCHED_INTERLEAVED)) return;
-        unsigned char* dst = lds + (t & 1) * C::STEPW;
+        unsigned char* dst = lds + (C::WB == 2 ? (t & 1) : 0) * C::STEPW;
 #pragma unroll
         for (int pc = 0; pc < C::STEPW / 1024 / C::AW; ++pc) {
             const int piece = wave + pc * C::AW;              // 1-KB piece of the step
@@ -1454,7 +1476,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
 #pragma unroll 1
     for (int t = 0; t < C::XC; ++t) {
         chunk_barrier();                           // W chunks of t and this chunk's rows landed
-        w_dma(t + 1);
+        if constexpr (C::WB == 2) w_dma(t + 1);
         // the 4 heads' weighted sums of this x chunk (CSR order)
         f32x4 a[HEADS][2];
 #pragma unroll
@@ -1508,7 +1530,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         // buffers live at once spilled registers)
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < C::XC && !(flags & MIGNN_DIAG_NO_PRODUCE)) gather(t + 1);
-        const unsigned char* wb = wl0 + (t & 1) * C::STEPW;
+        const unsigned char* wb = wl0 + (C::WB == 2 ? (t & 1) : 0) * C::STEPW;
 #pragma unroll
         for (int k = 0; k < HEADS; ++k) {
             uint32_t m = 0;
@@ -1551,6 +1573,12 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
             // (one head's fragments at a time: hoisting the next heads' LDS
             // reads above these MFMAs spilled registers)
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (C::WB == 1) {
+            if (t + 1 < C::XC) {
+                vm_barrier64<63>();                // every wave's W reads done (gathers may fly)
+                w_dma(t + 1);
+            }
         }
     }
     // epilogue (staged, whole-row stores): the W / alpha buffers are free once

@@ -20,6 +20,8 @@ SHAPES = [  # (name, k1, k2, n, residual)
     ("gin_nn0 256->256", 256, 0, 256, False),
     ("gin_nn2 256->256 +res", 256, 0, 256, True),
     ("tf_qt 256->1024", 256, 0, 1024, False),
+    ("tf_qk 256->1028", 256, 0, 1028, False),   # TransformerConv's Q~K with the score constants
+    ("tf_qk 256->1040", 256, 0, 1040, False),
     ("tf_out [1028|256]->256 +res", 1028, 256, 256, True),
     ("gat_out 1024->256 +res", 1024, 0, 256, True),
     ("gat_out 512->128 +res", 512, 0, 128, True),
@@ -41,7 +43,10 @@ def timeit(fn, reps=10):
 def main():
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
+    only = os.environ.get("GB_ONLY", "")
     for name, k1, k2, n, has_res in SHAPES:
+        if only and not any(o in name for o in only.split(",")):
+            continue
         a = torch.randn(M, k1, device=dev, generator=g)
         a2 = torch.randn(M, k2, device=dev, generator=g) if k2 else None
         w = torch.randn(n, k1 + k2, device=dev, generator=g) / (k1 + k2) ** 0.5
@@ -50,8 +55,11 @@ def main():
         out = torch.empty(M, n, device=dev)
         img = f16x3_image(w)
         kw = dict(relu=True, residual=res, a2=a2, out=out)
-        t32 = timeit(lambda: linear(a, w, b, **kw))
-        c32 = out.clone()
+        if os.environ.get("GB_NO32"):
+            t32, c32 = float("nan"), out.clone()
+        else:
+            t32 = timeit(lambda: linear(a, w, b, **kw))
+            c32 = out.clone()
         t16 = timeit(lambda: linear_f16x3(a, img, n, b, **kw))
         d = (out - c32).abs().max().item()
         abl = {}
