@@ -106,8 +106,9 @@ else:
 for k, L in libs.items():
     run(L, Ys[k])
 torch.cuda.synchronize()
-res = {"mode": mode, "n": n, "max_diff": (Ys["cur"] - Ys["prev"]).abs().max().item(),
-       "bitwise_equal": bool(torch.equal(Ys["cur"], Ys["prev"]))}
+res = {"mode": mode, "n": n, "max_diff": (Ys["cur"] - Ys["prev"]).abs().nan_to_num(0.0).max().item(),
+       "nan_rows": {k: int(torch.isnan(v).any(1).sum().item()) for k, v in Ys.items()},
+       "bitwise_equal": bool(torch.equal(Ys["cur"].view(torch.int32), Ys["prev"].view(torch.int32)))}
 times = {k: [] for k in libs}
 for rnd in range(int(os.environ.get("AB_REPS", "5")) + 1):
     for k, L in libs.items():
