@@ -254,6 +254,36 @@ def test_gat_fused_vs_launches_and_fp64(h, flags):
     _check(launches[rb:re], ref[rb:re], mag[rb:re], f"gat launches h={h}")
 
 
+@pytest.mark.parametrize("h", [64, 128])
+def test_gat_fused_coresident_blocks(h):
+    """The fused GAT kernel runs two 4-wave blocks per CU; the small-graph
+    tests above launch fewer blocks than there are CUs.  Here 200k rows
+    (3125 blocks) of the irregular graph (degrees 0-12, hubs) put two blocks
+    on every CU: fused == the launch sequence on every row."""
+    n = 200_000
+    ei = _graph(n, 21)
+    csr = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP)
+    g = torch.Generator(device=DEV).manual_seed(h)
+    x = torch.randn(n, h, device=DEV, generator=g)
+    wlog = torch.randn(8, h, device=DEV, generator=g) / h ** 0.5
+    wcat = torch.randn(h, 4 * h, device=DEV, generator=g) / (2 * h) ** 0.5
+    bias = torch.randn(h, device=DEV, generator=g) * 0.1
+    sc = torch.rand(h, device=DEV, generator=g) + 0.5
+    sh = torch.randn(h, device=DEV, generator=g) * 0.1
+    img = f16x3_image(wcat)
+    outs = []
+    for fused in (1, 0):
+        o = torch.full((n, h), float("nan"), device=DEV)
+        _gat_layer(csr, x, n, 0, n, h, wlog, wcat, img, bias, sc, sh,
+                   15 | (0 if fused else GAT_LAUNCHES), o)
+        outs.append(o)
+    torch.cuda.synchronize()
+    d = (outs[0] - outs[1]).abs().max(1).values
+    scale = max(1.0, outs[1].abs().max().item())
+    assert torch.isfinite(outs[0]).all()
+    assert int((d > 2e-5 * scale).sum()) == 0, (int((d > 2e-5 * scale).sum()), d.max().item())
+
+
 def _tf_layer(fused, csr, x, rb, re, wqk, bqk, wout, bout, sc, sh, flags, out):
     L = _lib.lib()
     P = _lib.ptr
