@@ -10,6 +10,9 @@ sys.path.insert(0, os.path.join(HERE, "tests"))
 import torch  # noqa: E402
 
 from mignn import _lib  # noqa: E402
+
+if os.environ.get("TD_LIB"):                       # an alternative build (experiments)
+    _lib.LIB_PATH = os.environ["TD_LIB"]
 from mignn.gnn_model import build_csr  # noqa: E402
 import test_gpu_fused256 as T  # noqa: E402
 

@@ -363,6 +363,35 @@ def test_transformer_fused_vs_launches_and_fp64(flags):
     assert d <= 2e-5 * max(1.0, ref[rb:re].abs().max().item()), d
 
 
+def test_transformer_fused_many_blocks():
+    """The fused TransformerConv layer against its launch sequence on every
+    row of a 200k-row irregular graph (degrees 0-12, hubs): 1563 blocks,
+    several per CU over the launch -- the small-graph test above launches
+    fewer blocks than there are CUs (a two-blocks-per-CU variant of this
+    kernel went wrong only here)."""
+    n = 200_000
+    ei = _graph(n, 31)
+    csr = build_csr(ei, n, _lib.CSR_VERBATIM)
+    g = torch.Generator(device=DEV).manual_seed(15)
+    x = torch.randn(n, H, device=DEV, generator=g)
+    wqk = torch.randn(4 * H, H, device=DEV, generator=g) / 16
+    bqk = torch.randn(4 * H, device=DEV, generator=g) * 0.1
+    wout = torch.randn(H, 4 * H + 4 + H, device=DEV, generator=g) / (4 * H + 4 + H) ** 0.5
+    bout = torch.randn(H, device=DEV, generator=g) * 0.1
+    sc = torch.rand(H, device=DEV, generator=g) + 0.5
+    sh = torch.randn(H, device=DEV, generator=g) * 0.1
+    outs = []
+    for fused in (True, False):
+        o = torch.full((n, H), float("nan"), device=DEV)
+        _tf_layer(fused, csr, x, 0, n, wqk, bqk, wout, bout, sc, sh, 15, o)
+        outs.append(o)
+    torch.cuda.synchronize()
+    d = (outs[0] - outs[1]).abs().max(1).values
+    scale = max(1.0, outs[1].abs().max().item())
+    assert torch.isfinite(outs[0]).all()
+    assert int((d > 2e-5 * scale).sum()) == 0, (int((d > 2e-5 * scale).sum()), d.max().item())
+
+
 def test_transformer_fused_prep_rejects():
     L = _lib.lib()
     assert L.mignn_transformer_fused_prep_bytes(128, 4) == 0
