@@ -38,7 +38,19 @@ _lib.check(L.mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H,
 nb = L.mignn_gcn_plan_bytes(0, n)
 plan = torch.empty(nb, dtype=torch.uint8, device=dev)
 _lib.check(L.mignn_gcn_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(plan), nb, st), "p")
+if "gat" in kinds:
+    # the fused GAT layer (4 heads, split-fp16 image of Wcat [H, 4H]) on the same mesh
+    from mignn.gnn_model import f16x3_image  # noqa: E402
+    WLOG = torch.randn(8, H, device=dev, generator=g) / H ** 0.5
+    WCAT = torch.randn(H, 4 * H, device=dev, generator=g) / (2 * H) ** 0.5
+    GIMG = f16x3_image(WCAT)
+    GSCR = torch.empty(max(L.mignn_gat_layer_scratch_bytes(n, n, H, 4), 1), dtype=torch.uint8,
+                       device=dev)
 for _ in range(reps):
+    if "gat" in kinds:
+        _lib.check(L.mignn_gat_layer(P(csr.row_ptr), P(csr.col), P(X), H, n, 0, n, H, 4, 0.2,
+                                     P(WLOG), None, 8, P(WCAT), P(GIMG), P(b), P(sc), P(sh), 15,
+                                     P(GSCR), GSCR.numel(), P(Y), H, st), "gat")
     if "pc" in kinds:
         _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                            P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "pc")
