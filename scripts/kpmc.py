@@ -32,12 +32,29 @@ b = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
 Y = torch.empty_like(X)
-nbr = L.mignn_gcn_ring_plan_bytes(0, n, H)
-rplan = torch.empty(nbr, dtype=torch.uint8, device=dev)
-_lib.check(L.mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(rplan), nbr, None, st), "rp")
-nb = L.mignn_gcn_plan_bytes(0, n)
-plan = torch.empty(nb, dtype=torch.uint8, device=dev)
-_lib.check(L.mignn_gcn_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(plan), nb, st), "p")
+if "ring" in kinds:
+    nbr = L.mignn_gcn_ring_plan_bytes(0, n, H)
+    rplan = torch.empty(nbr, dtype=torch.uint8, device=dev)
+    _lib.check(L.mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(rplan), nbr,
+                                     None, st), "rp")
+if "planned" in kinds or "agg" in kinds:
+    nb = L.mignn_gcn_plan_bytes(0, n)
+    plan = torch.empty(nb, dtype=torch.uint8, device=dev)
+    _lib.check(L.mignn_gcn_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(plan), nb, st), "p")
+if "gin" in kinds or "tf" in kinds:
+    # H = 256 fused layers (KP_H=256): GIN (verbatim CSR) and TransformerConv
+    from mignn.gnn_model import f16x3_image, gin_fused_image  # noqa: E402
+    W2 = torch.randn(H, H, device=dev, generator=g) * 0.05
+    GI1, GI2 = f16x3_image(W), gin_fused_image(W2)
+    TWQ = torch.randn(4 * H + 4, H, device=dev, generator=g) / 16
+    TBQ = torch.randn(4 * H + 4, device=dev, generator=g) * 0.05
+    TWO = torch.randn(H, 4 * H + 4 + H, device=dev, generator=g) / (5 * H) ** 0.5
+    TQIMG = f16x3_image(TWQ)
+    TFIMG = torch.empty(L.mignn_transformer_fused_prep_bytes(H, 4), dtype=torch.uint8, device=dev)
+    if "tf" in kinds:
+        _lib.check(L.mignn_transformer_fused_prep(P(TWO), H, 4, P(TFIMG), TFIMG.numel(), st), "prep")
+        TSCR = torch.empty(L.mignn_transformer_layer_scratch_bytes(n, H, 4), dtype=torch.uint8,
+                           device=dev)
 if "gat" in kinds:
     # the fused GAT layer (4 heads, split-fp16 image of Wcat [H, 4H]) on the same mesh
     from mignn.gnn_model import f16x3_image  # noqa: E402
@@ -47,6 +64,14 @@ if "gat" in kinds:
     GSCR = torch.empty(max(L.mignn_gat_layer_scratch_bytes(n, n, H, 4), 1), dtype=torch.uint8,
                        device=dev)
 for _ in range(reps):
+    if "gin" in kinds:
+        _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
+                                           P(GI1), P(b), P(GI2), P(b), P(sc), P(sh), 15, P(Y), H,
+                                           st), "gin")
+    if "tf" in kinds:
+        _lib.check(L.mignn_transformer_layer_fused(
+            P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 4, 1.0 / H ** 0.5, P(TQIMG), P(TBQ),
+            P(TFIMG), P(b), P(sc), P(sh), 15, P(TSCR), TSCR.numel(), P(Y), H, st), "tf")
     if "gat" in kinds:
         _lib.check(L.mignn_gat_layer(P(csr.row_ptr), P(csr.col), P(X), H, n, 0, n, H, 4, 0.2,
                                      P(WLOG), None, 8, P(WCAT), P(GIMG), P(b), P(sc), P(sh), 15,
