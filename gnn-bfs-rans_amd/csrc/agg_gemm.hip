@@ -1240,7 +1240,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
 // weighted sums -- the B operands of W chunks (head k, chunk c) -- split with
 // the row's online exponent, 3 MFMAs per 16x16x32 block.  The 4 W chunks of
 // an x chunk (4 x H/16 column blocks of the linear_f16x3 image of Wcat
-// [H, 4H]) are LDS-DMA'd together, double-buffered, one barrier per x chunk.
+// [H, 4H]) are LDS-DMA'd together (double-buffered where the LDS budget of
+// two blocks per CU allows it: H = 64; H = 128 refills its one buffer after
+// the step's MFMAs), one barrier per x chunk.
 #ifndef GAT_AW
 #define GAT_AW 4
 #endif
