@@ -939,7 +939,7 @@ extern "C" int mignn_device_errors(unsigned int* out, int clear) {
         MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_device_errors), &zero, sizeof(unsigned int), 0,
                                     hipMemcpyHostToDevice));
     }
-    return MIGNN_OK;
+    return win_device_errors(out, clear);
 }
 
 extern "C" int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew,

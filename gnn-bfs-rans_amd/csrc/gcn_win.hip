@@ -1,0 +1,1116 @@
+// Fused GCN layer, window form -- the north-star hot kernel (GCNConv + residual
+// + BatchNorm(eval) + ReLU, reference gnn_model.py:63, :166, :184-191; PyG
+// GCNConv: out_i = sum_{j->i} w_ij h_j + b, w_ij = dinv_i dinv_j over
+// add_remaining_self_loops):
+//
+//   out_i = relu( (x_i + bias + (sum_{e in row i} ew_e x_{col e}) W^T) * scale + shift )
+//
+// Arithmetic: fp32 aggregation, the aggregate split into fp16 hi + lo with a
+// power-of-two row scale, three fp16 MFMA products with fp32 accumulation
+// (~2^-22 relative per product) -- gcn_f16x3.hip's scheme.
+//
+// Why this structure.  Per 64-row tile a fused layer streams 64 rows in and
+// 64 rows out of its CU; what else crosses the CU is the tile's out-of-tile
+// ("ext") neighbour rows.  With 4 x 4 x 4-cell tiles (the block order) that is
+// 96 rows per tile -- 1.5 per own row, L2 -> LDS traffic larger than the own
+// rows themselves, and the measured lever of the ring kernel (gcn_ring.hip:
+// from the zero row its aggregation ran 2.26 -> 1.84 ms).  Here a tile is one
+// z-plane of an 8 x 8-cell column (the column order,
+// mignn_locality_order_cols) and a workgroup walks its column along z, so the
+// previous and the current tile stay in LDS: a row's -z neighbour is in the
+// previous tile, its in-plane neighbours in the current one, its +z neighbour
+// in the next tile -- DMA'd a step ahead anyway, its one term is added at the
+// next step ("phase B": the row's partial sum is carried in registers).  Only
+// the 4 x 8 lateral face rows of a plane are ext rows: 0.5 per own row.
+//
+// Pipeline of step s (tile s = this workgroup's s-th tile; LDS slot s % 3):
+//   B0  ext rows of step s landed (older: own rows of tile s + 1, records)
+//   P1  phase A of tile s (in-window and ext entries, CSR order, the +z entry
+//       held back), phase B of tile s - 1 (its +z term, from tile s), split
+//       of tile s - 1 into the A image, its residual seeds
+//   B2  A image complete, slot (s-1) % 3 and the ext area free
+//       -> DMA ext rows of step s + 1, records of step s + 2, own rows of
+//       tile s + 2 into slot (s+2) % 3 (issued between the MFMAs)
+//   MFMA (tile s - 1, W split in registers)  B3  staging  B4  whole-row stores
+// Every global read of the tile loop is an LDS-DMA counted by hand
+// (global_load_lds_dwordx4); one workgroup per CU at H = 128 (8 waves), two
+// at H = 64.
+//
+// Schedule (the plan header; mignn_gcn_win_plan): rounds of L steps -- in
+// round r workgroup p (XCD-major position) walks tiles [(rG + p) L, +L), a
+// column or a z-segment of one, while its XCD's workgroups walk the next
+// columns of the same y-row -- for the full columns of the order, then the
+// remaining tiles as contiguous chunks.  Any CSR is correct under any order:
+// the plan classifies every entry by where its row is resident at that step.
+// Plan records: 48 B per row -- slots 0..6 {u16 code, f32 w} in CSR order
+// (code = the LDS offset of the neighbour row, >> 1 at H = 128), slot 7 the
+// +z (next-tile) entry; waves with a row outside that form (degree > 8, ext
+// capacity exceeded) take the CSR path (row_ptr / col / ew, global x).
+#include <type_traits>
+
+#include "common.hpp"
+
+namespace mignn {
+namespace {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_w;
+using f16x8w = __attribute__((ext_vector_type(8))) _Float16;
+using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
+
+constexpr int kWRec = 48;                 // bytes per plan record: 8 u16 codes + 8 f32 weights
+constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the next-tile entry
+constexpr int kWHdr = 256;                // plan header bytes
+constexpr uint32_t kWMagic = 0x4E495747u;
+
+template <int H>
+struct WCfg {
+    static_assert(H == 64 || H == 128, "window GCN layer: H in {64, 128}");
+    static constexpr int BM = 64, NW = 8, NT = NW * 64;
+    static constexpr int F = H / 16, CH = F / 4;       // floats / 16-B chunks per lane of a row
+    static constexpr int ROWB = H * 4;
+    static constexpr int X_BYTES = BM * ROWB;
+    static constexpr int NSLOT = 3;                    // own-row slots: tiles s-1, s, s+1
+    static constexpr int KX = 32;                      // ext rows per tile (an 8x8 plane's faces)
+    static constexpr int EXT_BYTES = KX * ROWB;
+    static constexpr int EPW = KX / NW;                // ext rows DMA'd per wave
+    static constexpr int XLW = 8;                      // ext-list group per wave: EPW columns, summary
+    static constexpr int RECW = 8 * kWRec + XLW * 4;   // a wave's records + list in LDS
+    static constexpr int TLANES = RECW / 16;
+    static constexpr int TAB_BYTES = BM * kWRec + NW * XLW * 4;
+    static constexpr int A_BYTES = BM * H * 2;         // hi or lo image (16-B chunks swizzled)
+    // LDS: X[3] | EXT | ZERO (the code-addressed region) | TAB[2] | AH | AL | REXP | EPI
+    static constexpr int OFF_X = 0;
+    static constexpr int OFF_EXT = NSLOT * X_BYTES;
+    static constexpr int OFF_ZERO = OFF_EXT + EXT_BYTES;
+    static constexpr int CODE_END = OFF_ZERO + ROWB;
+    static constexpr int CSH = H == 64 ? 0 : 1;        // code = LDS byte offset >> CSH
+    static constexpr int OFF_TAB = CODE_END;
+    static constexpr int OFF_AH = OFF_TAB + 2 * TAB_BYTES;
+    static constexpr int OFF_AL = OFF_AH + A_BYTES;
+    static constexpr int OFF_REXP = OFF_AL + A_BYTES;
+    static constexpr int OFF_EPI = OFF_REXP + BM * 4;
+    static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
+    static constexpr int OFF_STG = OFF_AH;             // output staging (fp32 rows) over AH | AL
+    static constexpr int WGPC = H == 64 ? 2 : 1;       // workgroups per CU
+    static constexpr int NQ = 2;                       // row quads per wave (8 rows)
+    static constexpr int KC = H / 32;
+    static constexpr int RPP = 1024 / ROWB, LPR = 64 / RPP;   // rows / lanes per row of a DMA piece
+    static constexpr int NPX = X_BYTES / 1024 / NW;    // own-row pieces per wave
+    static constexpr int NPE = EXT_BYTES / 1024 / NW;  // ext pieces per wave
+    static constexpr int LPRW = ROWB / 16, RPI = 64 / LPRW;
+    static constexpr int NST = 8 / RPI;                // row stores per wave (8 rows)
+    static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
+    static_assert(2 * A_BYTES >= BM * ROWB, "staging fits the A images");
+    static_assert(EPW == NPE * RPP && EPW + 1 <= XLW, "ext rows per wave");
+    static_assert((CODE_END >> CSH) <= 65536, "u16 codes");
+    static_assert(RECW % 16 == 0 && TLANES <= 64 && TAB_BYTES % 16 == 0, "records DMA");
+};
+
+// ------------------------------------------------------------------ schedule
+// Plan header (first kWHdr bytes of the plan).  Round / chunk schedule: for
+// s < R1 L, workgroup position p at step s has tile ((s / L) G + p) L + s % L;
+// then tiles [t2, ntiles) as chunks of `chunk` per position.
+struct WinHdr {
+    uint32_t magic;
+    int32_t G, h, L;
+    int32_t R1, chunk, nsteps, Z;
+    int64_t ntiles, t2, rb, re;
+};
+
+struct WinSched {
+    int64_t ntiles, t2;
+    int G, L, R1, chunk;
+};
+
+__host__ __device__ inline int64_t win_tile(const WinSched& S, int p, int64_t s) {
+    if (s < 0) return -1;
+    const int64_t s1 = static_cast<int64_t>(S.R1) * S.L;
+    if (s < s1) return ((s / S.L) * S.G + p) * S.L + s % S.L;
+    const int64_t j = s - s1;
+    if (j >= S.chunk) return -1;
+    const int64_t t = S.t2 + static_cast<int64_t>(p) * S.chunk + j;
+    return t < S.ntiles ? t : -1;
+}
+__host__ __device__ inline void win_where(const WinSched& S, int64_t t, int& p, int64_t& s) {
+    if (t < S.t2) {
+        const int64_t i = t / S.L;
+        p = static_cast<int>(i % S.G);
+        s = (i / S.G) * S.L + t % S.L;
+    } else {
+        const int64_t u = t - S.t2;
+        p = static_cast<int>(u / S.chunk);
+        s = static_cast<int64_t>(S.R1) * S.L + u % S.chunk;
+    }
+}
+
+// the header: schedule parameters from the order's column info (nullable:
+// {1, Z tiles per full column, full columns, ...}, mignn_locality_order_cols)
+__global__ void win_hdr_kernel(WinHdr* hdr, const int32_t* __restrict__ info, int64_t ntiles, int G,
+                               int h, int64_t rb, int64_t re) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t Z = 0, C = 0;
+    if (info != nullptr && info[0] == 1) {
+        Z = info[1];
+        C = info[2];
+    }
+    // contiguous chunks (no column structure)
+    int bestL = 1, bestR1 = 0;
+    int64_t bestChunk = (ntiles + G - 1) / G;
+    double best = 1.25 * static_cast<double>(bestChunk);
+    if (Z > 0 && C > 0) {
+        for (int nseg = 1; nseg <= 16; ++nseg) {
+            if (Z % nseg != 0 || Z / nseg < 4) continue;
+            const int64_t L = Z / nseg;
+            int64_t R1 = (C * nseg) / G;
+            const int64_t rmax = ntiles / (static_cast<int64_t>(G) * L);
+            if (R1 > rmax) R1 = rmax;
+            if (R1 <= 0) continue;
+            const int64_t t2 = R1 * G * L;
+            const int64_t chunk = (ntiles - t2 + G - 1) / G;
+            const double S = static_cast<double>(R1 * L + chunk);
+            // steps, window breaks (one per segment), the chunks' poorer locality
+            const double cost = S * (1.0 + 0.02 * nseg) + 0.25 * static_cast<double>(chunk);
+            if (cost < best) {
+                best = cost;
+                bestL = static_cast<int>(L);
+                bestR1 = static_cast<int>(R1);
+                bestChunk = chunk;
+            }
+        }
+    }
+    hdr->magic = kWMagic;
+    hdr->G = G;
+    hdr->h = h;
+    hdr->L = bestL;
+    hdr->R1 = bestR1;
+    hdr->chunk = static_cast<int32_t>(bestChunk);
+    hdr->nsteps = static_cast<int32_t>(static_cast<int64_t>(bestR1) * bestL + bestChunk);
+    hdr->Z = static_cast<int32_t>(Z);
+    hdr->ntiles = ntiles;
+    hdr->t2 = static_cast<int64_t>(bestR1) * G * bestL;
+    hdr->rb = rb;
+    hdr->re = re;
+}
+
+__device__ inline WinSched win_sched(const WinHdr* h) {
+    WinSched S;
+    S.ntiles = h->ntiles;
+    S.t2 = h->t2;
+    S.G = h->G;
+    S.L = h->L;
+    S.R1 = h->R1;
+    S.chunk = h->chunk;
+    return S;
+}
+
+int win_grid(int64_t ntiles, int wgpc) {
+    static int cus_cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    int& cus = cus_cache[dev & 63];
+    if (cus == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return -1;
+        cus = c < 1 ? 1 : c;
+    }
+    int G = (cus * wgpc / 8) * 8;
+    if (G < 8) G = 8;
+    if (ntiles < G) G = static_cast<int>(((ntiles + 7) / 8) * 8);
+    return G;
+}
+
+// the device word for plan / launch mismatches (mignn_device_errors)
+__device__ unsigned int g_win_errors = 0u;
+
+constexpr int wvm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70 | 0xF00; }   // vmcnt(n)
+constexpr int kWLgkm0 = 0xC07F;
+
+template <int W>
+__device__ __forceinline__ void wwait() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(W);
+    asm volatile("" ::: "memory");
+}
+template <int W>
+__device__ __forceinline__ void wbar() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(W);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ uint32_t wlds(const unsigned char* p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_w)(p)));
+}
+
+__device__ __forceinline__ void wdma(const void* src, uint32_t dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(__builtin_amdgcn_readfirstlane(static_cast<int>(dst)))
+        : "memory");
+}
+
+__device__ __forceinline__ uint64_t wuni(const void* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<int>(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ void wdma_s(const void* base, uint32_t voff, uint32_t dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(wuni(base)), "s"(__builtin_amdgcn_readfirstlane(static_cast<int>(dst)))
+        : "memory");
+}
+
+__device__ __forceinline__ int wsplit_exp(uint32_t mbits) {
+    const int eb = static_cast<int>((mbits >> 23) & 0xffu);
+    return min(140 - eb, 50);
+}
+__device__ __forceinline__ uint32_t wrow_max(uint32_t v) {
+    int t = static_cast<int>(v);
+    t = max(static_cast<uint32_t>(t), static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(t, 0xB1, 0xf, 0xf, false)));
+    t = max(static_cast<uint32_t>(t), static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(t, 0x4E, 0xf, 0xf, false)));
+    t = max(static_cast<uint32_t>(t), static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(t, 0x124, 0xf, 0xf, false)));
+    t = max(static_cast<uint32_t>(t), static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(t, 0x128, 0xf, 0xf, false)));
+    return static_cast<uint32_t>(t);
+}
+__device__ __forceinline__ uint32_t wwave_max(uint32_t v) {
+    const uint32_t t = wrow_max(v);
+    const uint32_t a = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t), 0));
+    const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t), 16));
+    const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t), 32));
+    const uint32_t d = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(t), 48));
+    return max(max(a, b), max(c, d));
+}
+
+// A-image 16-B chunk swizzle of row R (conflict-free fragment reads: the
+// lanes of one ds_read_b128 group cover the 64 banks once)
+template <int H>
+__device__ __forceinline__ int asw(int R) {
+    return H == 64 ? ((R >> 1) & 7) : (R & 15);
+}
+
+__device__ __attribute__((aligned(16))) float g_win_zero_row[256];
+
+// ------------------------------------------------------------------ plan
+// One 64-thread block per tile, a thread per row.  Entry classes at the
+// tile's step: the current tile (slot s % 3), the workgroup's previous tile
+// ((s-1) % 3), the first entry in its next tile ((s+1) % 3, slot 7: phase B),
+// else an ext slot (numbered in row-major order of the tile's ext entries, a
+// wave-wide prefix sum; slot k at LDS ext row k, its column in list entry
+// (k / EPW) * XLW + k % EPW); a row with more than 7 phase-A entries, more
+// than 8 entries or an ext slot past KX makes its wave take the CSR path.
+template <int H>
+__global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict__ row_ptr,
+                                                      const int32_t* __restrict__ col,
+                                                      const float* __restrict__ ew,
+                                                      const WinHdr* __restrict__ hdr,
+                                                      unsigned char* __restrict__ tabs,
+                                                      unsigned long long* __restrict__ stats) {
+    using C = WCfg<H>;
+    const int lr = threadIdx.x;
+    const WinSched S = win_sched(hdr);
+    const int64_t rb = hdr->rb, re = hdr->re, ntiles = hdr->ntiles;
+    __shared__ uint32_t xl[C::NW * C::XLW];
+    const uint32_t zcode = static_cast<uint32_t>(C::OFF_ZERO >> C::CSH);
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        int p;
+        int64_t s;
+        win_where(S, t, p, s);
+        const int64_t tprev = win_tile(S, p, s - 1), tnext = win_tile(S, p, s + 1);
+        const int sc = static_cast<int>(s % 3), sp = static_cast<int>((s + 2) % 3),
+                  sn = static_cast<int>((s + 1) % 3);
+        const int64_t t0 = rb + t * C::BM;
+        const int64_t nloc = re - t0 < C::BM ? re - t0 : C::BM;
+        auto in_tile = [&](int64_t c, int64_t tt, int64_t& off) -> bool {
+            if (tt < 0) return false;
+            const int64_t b0 = rb + tt * C::BM;
+            const int64_t nl = re - b0 < C::BM ? re - b0 : C::BM;
+            off = c - b0;
+            return off >= 0 && off < nl;
+        };
+        auto xcode = [&](int slot, int64_t off) -> uint32_t {
+            const uint32_t o = static_cast<uint32_t>(off);
+            return ((C::OFF_X + slot * C::X_BYTES + o * C::ROWB) | ((o & 7u) << 4)) >> C::CSH;
+        };
+        for (int i = lr; i < C::NW * C::XLW; i += 64) xl[i] = 0u;   // unused: row 0, never read
+        const int64_t r = t0 + lr;
+        int e0 = 0, deg = 0;
+        if (lr < nloc) {
+            e0 = row_ptr[r];
+            deg = row_ptr[r + 1] - e0;
+        }
+        // pass 1: ext entries of the row
+        int next = 0, nA = 0;
+        bool haveN = false;
+        for (int e = 0; e < deg; ++e) {
+            const int64_t c = col[e0 + e];
+            int64_t off;
+            if (in_tile(c, t, off) || in_tile(c, tprev, off)) {
+                ++nA;
+            } else if (!haveN && in_tile(c, tnext, off)) {
+                haveN = true;
+            } else {
+                ++nA;
+                ++next;
+            }
+        }
+        int pre = next;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(pre, d, 64);
+            if (lr >= d) pre += v;
+        }
+        pre -= next;
+        __syncthreads();
+        bool far = deg > 8 || nA > kWA || pre + next > C::KX;
+        uint32_t code[8];
+        uint32_t wb[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            code[q] = zcode;
+            wb[q] = 0u;
+        }
+        if (lr < nloc && deg > 0 && deg <= 8) {
+            int k = pre, a = 0;
+            bool usedN = false;
+            for (int e = 0; e < deg; ++e) {
+                const int64_t c = col[e0 + e];
+                const uint32_t w = __float_as_uint(ew[e0 + e]);
+                int64_t off;
+                uint32_t cd;
+                int slot;
+                if (in_tile(c, t, off)) {
+                    cd = xcode(sc, off);
+                    slot = a++;
+                } else if (in_tile(c, tprev, off)) {
+                    cd = xcode(sp, off);
+                    slot = a++;
+                } else if (!usedN && in_tile(c, tnext, off)) {
+                    usedN = true;
+                    cd = xcode(sn, off);
+                    slot = 7;
+                } else {
+                    if (k < C::KX) {
+                        cd = ((C::OFF_EXT + k * C::ROWB) | ((static_cast<uint32_t>(k) & 7u) << 4)) >> C::CSH;
+                        xl[(k / C::EPW) * C::XLW + k % C::EPW] = static_cast<uint32_t>(c);
+                    } else {
+                        cd = zcode;
+                    }
+                    ++k;
+                    slot = a++;
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (q == slot) {
+                        code[q] = cd;
+                        wb[q] = w;
+                    }
+            }
+        }
+        // summary of the row's wave (8 rows): max phase-A count | any CSR-path row
+        uint32_t md = far ? 0u : static_cast<uint32_t>(nA), af = far ? 1u : 0u;
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1) {
+            md = max(md, static_cast<uint32_t>(__shfl_xor(static_cast<int>(md), d, 8)));
+            af |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(af), d, 8));
+        }
+        if ((lr & 7) == 0) xl[(lr >> 3) * C::XLW + C::EPW] = md | (af << 8);
+        __syncthreads();
+        unsigned char* const base = tabs + t * C::TAB_BYTES;
+        uint4* dst = reinterpret_cast<uint4*>(base + lr * kWRec);
+        dst[0] = make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
+                            code[4] | (code[5] << 16), code[6] | (code[7] << 16));
+        dst[1] = make_uint4(wb[0], wb[1], wb[2], wb[3]);
+        dst[2] = make_uint4(wb[4], wb[5], wb[6], wb[7]);
+        for (int i = lr; i < C::NW * C::XLW; i += 64)
+            reinterpret_cast<uint32_t*>(base + C::BM * kWRec)[i] = xl[i];
+        if (stats != nullptr) {
+            if (far && lr < nloc) atomicAdd(&stats[1], 1ull);
+            const int kt = __shfl(pre + next, 63, 64);
+            if (lr == 63 && kt > C::KX) atomicAdd(&stats[0], 1ull);
+            if (lr == 63) atomicMax(&stats[3], static_cast<unsigned long long>(kt));
+            if (haveN && lr < nloc) atomicAdd(&stats[2], 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- layer
+// MODE: 32 aggregate only (mignn_gcn_aggregate_win: the fp32 sums are the
+// output); timing ablations (mignn_diag_win only): 1 ext rows from the zero
+// row, 4 no MFMAs.  EPIF: the epilogue flags at compile time (15, 11; -1: from
+// `flags`).
+template <int H, int MODE = 0, int EPIF = -1>
+__global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel(
+    const unsigned char* __restrict__ plan, const int32_t* __restrict__ row_ptr,
+    const int32_t* __restrict__ col, const float* __restrict__ ew, const float* __restrict__ x,
+    int64_t ldx, int64_t rb, int64_t re, const float* __restrict__ W,
+    const float* __restrict__ bias, const float* __restrict__ scale,
+    const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+    using C = WCfg<H>;
+    constexpr bool AGG = (MODE & 32) != 0;
+    if constexpr (EPIF >= 0) flags = EPIF;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
+    _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
+    _Float16* const AL = reinterpret_cast<_Float16*>(lds + C::OFF_AL);
+    int* const REXP = reinterpret_cast<int*>(lds + C::OFF_REXP);
+    float* const EPI = reinterpret_cast<float*>(lds + C::OFF_EPI);
+
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const WinHdr* const hdr = reinterpret_cast<const WinHdr*>(plan);
+    {
+        const bool ok = hdr->magic == kWMagic && hdr->G == static_cast<int>(gridDim.x) &&
+                        hdr->h == H && hdr->rb == rb && hdr->re == re;
+        if (!ok) {
+            if (tid == 0)
+                __hip_atomic_fetch_or(&g_win_errors, static_cast<unsigned>(MIGNN_DEVERR_PLAN),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    const WinSched S = win_sched(hdr);
+    const unsigned char* const tabs = plan + kWHdr;
+    const int per_xcd = static_cast<int>(gridDim.x) >> 3;
+    const int p = (static_cast<int>(blockIdx.x) & 7) * per_xcd + (static_cast<int>(blockIdx.x) >> 3);
+    auto tile_of = [&](int64_t s) -> int64_t { return win_tile(S, p, s); };
+    if (tile_of(0) < 0) return;                   // no work (uniform): no DMA issued
+
+    const int gq = lane >> 4, iq = lane & 15;
+    const int hb = (iq >= 4 && iq < 12) ? 1 : 0;
+    const int c0 = (hb ? iq - 4 : (iq < 4 ? iq : iq - 8)) | (hb << 3);
+    const uint32_t coff0 = static_cast<uint32_t>(c0 << 4);
+    auto decode = [&](uint32_t cd) -> uint32_t { return (cd << C::CSH) ^ coff0; };
+
+    // own-row DMA of a tile: SGPR base, per-lane offsets fixed for the launch
+    const uint32_t ldxb = static_cast<uint32_t>(ldx) * 4u;
+    uint32_t xoff[C::NPX];
+#pragma unroll
+    for (int pp = 0; pp < C::NPX; ++pp) {
+        const int pc = pp * C::NW + wave;
+        const int lr = pc * C::RPP + lane / C::LPR;
+        const int pos = lane % C::LPR;
+        xoff[pp] = static_cast<uint32_t>(lr) * ldxb + 16u * static_cast<uint32_t>(pos ^ (lr & 7));
+    }
+    const uint32_t toff = lane < 24 ? static_cast<uint32_t>(wave * 8 * kWRec + 16 * lane)
+                                    : static_cast<uint32_t>(C::BM * kWRec + wave * (C::XLW * 4) + 16 * (lane - 24));
+    // records of tile t (or tile 0: a dummy of the same op count) -> TAB slot q
+    auto dma_tab = [&](int64_t t, int q) {
+        if (lane < C::TLANES)
+            wdma_s(tabs + (t >= 0 ? t : 0) * C::TAB_BYTES, toff,
+                   wlds(lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW));
+    };
+    // own rows of tile t (dummy: tile 0) -> X slot q, piece pp
+    auto dma_own = [&](int64_t t, int q, int pp) {
+        const int64_t tt = t >= 0 ? t : 0;
+        const int64_t t0 = rb + tt * C::BM;
+        const int pc = pp * C::NW + wave;
+        unsigned char* const X = lds + C::OFF_X + q * C::X_BYTES;
+        if (t0 + C::BM <= re) {
+            wdma_s(x + t0 * ldx, xoff[pp], wlds(X + pc * 1024));
+        } else {
+            int l = lane;
+            asm volatile("" : "+v"(l));
+            const int lr = pc * C::RPP + l / C::LPR;
+            const int pos = l % C::LPR;
+            int64_t row = t0 + lr;
+            if (row >= re) row = re - 1;
+            wdma(x + row * ldx + 4 * (pos ^ (lr & 7)), wlds(X + pc * 1024));
+        }
+    };
+    // ext rows of the step whose records sit in TAB slot q (dummy: the zero row)
+    auto ext_src = [&](int q, int i, bool real) -> const unsigned char* {
+        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + 8 * kWRec;
+        int l = lane;
+        asm volatile("" : "+v"(l));
+        const int kk = i * C::RPP + l / C::LPR;
+        const int k = wave * C::EPW + kk;
+        const int pos = l % C::LPR;
+        const uint32_t c = *reinterpret_cast<const uint32_t*>(tab + 4 * kk);
+        return ((MODE & 1) || !real) ? reinterpret_cast<const unsigned char*>(g_win_zero_row + 4 * (pos & 31))
+                                     : reinterpret_cast<const unsigned char*>(x) + static_cast<uint64_t>(c) * ldxb +
+                                           16u * static_cast<uint32_t>(pos ^ (k & 7));
+    };
+    auto ext_dma = [&](int i, const unsigned char* src) {
+        wdma(src, wlds(lds + C::OFF_EXT + (wave * C::EPW + i * C::RPP) * C::ROWB));
+    };
+
+    // ------------------------------------------------------------ prologue
+    for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
+    const int rr = lane & 15, gg = lane >> 4;
+    constexpr int WN = H / 16, WM = C::NW / WN, IBW = (C::BM / 16) / WM;
+    static_assert(WN * WM == C::NW && IBW * WM * 16 == C::BM, "window transform grid");
+    const int wn = wave % WN, wm = wave / WN;
+    const int n0 = 16 * wn;
+    f16x8w wh[C::KC], wl[C::KC];
+    int qw = 0;
+    if constexpr (!AGG) {
+        float wv[C::KC][8];
+        uint32_t m = 0;
+#pragma unroll
+        for (int kc = 0; kc < C::KC; ++kc) {
+            const float* pw = W + static_cast<int64_t>(n0 + rr) * H + 32 * kc + 8 * gg;
+            const float4 a = ld4(pw), b = ld4(pw + 4);
+            float* w8 = wv[kc];
+            w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
+            w8[4] = b.x; w8[5] = b.y; w8[6] = b.z; w8[7] = b.w;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(w8[j])));
+        }
+        qw = wsplit_exp(wwave_max(m));            // one exponent per 16-column block
+#pragma unroll
+        for (int kc = 0; kc < C::KC; ++kc)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float sv = ldexpf(wv[kc][j], qw);
+                const _Float16 hh = static_cast<_Float16>(sv);
+                wh[kc][j] = hh;
+                wl[kc][j] = static_cast<_Float16>(sv - static_cast<float>(hh));
+            }
+        if (wm == 0 && lane < 16) {
+            const int n = n0 + lane;
+            EPI[n] = (flags & MIGNN_EPI_BIAS) ? bias[n] : 0.f;
+            EPI[H + n] = (flags & MIGNN_EPI_AFFINE) ? scale[n] : 1.f;
+            EPI[2 * H + n] = (flags & MIGNN_EPI_AFFINE) ? shift[n] : 0.f;
+        }
+    }
+    const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
+
+    // records and rows of steps 0 and 1, then step 0's ext rows
+    dma_tab(tile_of(0), 0);
+#pragma unroll
+    for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(0), 0, pp);
+    dma_tab(tile_of(1), 1);
+#pragma unroll
+    for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(1), 1, pp);
+    wbar<wvm(0) & kWLgkm0>();                     // (all waves), zero row, EPI
+    {
+        const unsigned char* es[C::NPE];
+#pragma unroll
+        for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(0, i, true);
+#pragma unroll
+        for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
+    }
+
+    // phase-B carry: tile s-1's partial sums and +z entries
+    f32x4 accp[C::NQ][C::CH];
+    uint32_t ncode[C::NQ];
+    float nwt[C::NQ];
+#pragma unroll
+    for (int qd = 0; qd < C::NQ; ++qd) {
+        ncode[qd] = C::OFF_ZERO >> C::CSH;
+        nwt[qd] = 0.f;
+#pragma unroll
+        for (int j = 0; j < C::CH; ++j) accp[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    int64_t cur = tile_of(0), prv = -1;
+    int xs = 0;                                   // X slot of step s (s % 3)
+    for (int64_t s = 0;; ++s) {
+        if (s > 0) {
+            prv = cur;
+            cur = tile_of(s);
+        }
+        if (cur < 0 && prv < 0) break;            // (uniform)
+        const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1
+        const int xn2 = xp;                       // slot of tile s + 2 (= (s-1) % 3)
+        const int tq = static_cast<int>(s & 1);   // TAB slot of step s
+        const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
+        const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
+        const int64_t tp0 = rb + (prv >= 0 ? prv : 0) * C::BM;
+        const int64_t nlocp = prv >= 0 ? (re - tp0 < C::BM ? re - tp0 : C::BM) : 0;
+        const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
+        const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
+        // (B0) this step's ext rows landed (and, older, the own rows of tile
+        //      s + 1 and this step's records); younger: the records of step
+        //      s + 1, the own rows of tile s + 2, the last step's stores
+        if (s == 0) wbar<wvm(0) & kWLgkm0>();
+        else if (s == 1) wbar<wvm(1 + C::NPX) & kWLgkm0>();
+        else wbar<wvm(1 + C::NPX + C::NST) & kWLgkm0>();
+
+        // ---- (P1) phase A of tile s
+        f32x4 accn[C::NQ][C::CH];
+        uint32_t ncn[C::NQ];
+        float nwn[C::NQ];
+#pragma unroll
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            ncn[qd] = C::OFF_ZERO >> C::CSH;
+            nwn[qd] = 0.f;
+#pragma unroll
+            for (int j = 0; j < C::CH; ++j) accn[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (cur >= 0) {
+            const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
+            const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+                *reinterpret_cast<const int*>(RW + 8 * kWRec + 4 * C::EPW)));
+            const int maxa = static_cast<int>(summ & 0xffu);
+            const bool far = ((summ >> 8) & 1u) != 0u;
+            if (!far) {
+                uint4 cds[C::NQ], w03[C::NQ], w47[C::NQ];
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    const unsigned char* rec = RW + (4 * qd + gq) * kWRec;
+                    cds[qd] = *reinterpret_cast<const uint4*>(rec);
+                    w03[qd] = *reinterpret_cast<const uint4*>(rec + 16);
+                    w47[qd] = *reinterpret_cast<const uint4*>(rec + 32);
+                }
+                auto codeof = [&](int qd, int u) -> uint32_t {
+                    const uint32_t d = u < 2 ? cds[qd].x : u < 4 ? cds[qd].y : u < 6 ? cds[qd].z : cds[qd].w;
+                    return (u & 1) ? (d >> 16) : (d & 0xffffu);
+                };
+                auto wof = [&](int qd, int u) -> float {
+                    const uint32_t d = u == 0 ? w03[qd].x : u == 1 ? w03[qd].y : u == 2 ? w03[qd].z
+                                     : u == 3 ? w03[qd].w : u == 4 ? w47[qd].x : u == 5 ? w47[qd].y
+                                     : u == 6 ? w47[qd].z : w47[qd].w;
+                    return __uint_as_float(d);
+                };
+                // slots in batches (H = 128: 0..2, 3..5, 6): loads of a batch first
+                auto batch = [&](auto U0, auto NB) {
+                    constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
+                    f32x4 vv[C::NQ][nb][C::CH];
+#pragma unroll
+                    for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                        for (int uu = 0; uu < nb; ++uu) {
+                            const uint32_t a = decode(codeof(qd, u0 + uu));
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+                                vv[qd][uu][j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+                        }
+#pragma unroll
+                    for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                        for (int uu = 0; uu < nb; ++uu) {
+                            const float w = wof(qd, u0 + uu);
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(w, vv[qd][uu][j][r], accn[qd][j][r]);
+                        }
+                };
+                if constexpr (H == 128) {
+                    if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
+                    if (maxa > 3) batch(std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
+                    if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
+                } else {   // (batches of 2: the 128-VGPR budget of 4 waves per SIMD)
+                    if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+                    if (maxa > 2) batch(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
+                    if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
+                    if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
+                }
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    ncn[qd] = codeof(qd, 7);
+                    nwn[qd] = wof(qd, 7);
+                }
+            } else {
+                // CSR path: every entry of the wave's rows in CSR order, the
+                // current tile from LDS, everything else from x (L2); the full
+                // sum (no phase B)
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    const int lrow = 8 * wave + 4 * qd + gq;
+                    if (lrow < nloc) {
+                        const int64_t row = t0 + lrow;
+                        const int eb = row_ptr[row], ee = row_ptr[row + 1];
+                        for (int e = eb; e < ee; e += 4) {
+                            int cj[4];
+                            float wj[4];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const bool v = e + k < ee;
+                                cj[k] = v ? col[e + k] : -1;
+                                wj[k] = v ? ew[e + k] : 0.f;
+                            }
+                            f32x4 vv[4][C::CH];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const int64_t off = static_cast<int64_t>(cj[k]) - t0;
+                                if (cj[k] < 0) {
+#pragma unroll
+                                    for (int j = 0; j < C::CH; ++j) vv[k][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                                } else if (off >= 0 && off < nloc) {
+                                    const uint32_t o = static_cast<uint32_t>(off);
+                                    const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
+#pragma unroll
+                                    for (int j = 0; j < C::CH; ++j)
+                                        vv[k][j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+                                } else {
+                                    const float* rp = x + static_cast<int64_t>(cj[k]) * ldx + 4 * c0;
+#pragma unroll
+                                    for (int j = 0; j < C::CH; ++j)
+                                        vv[k][j] = *reinterpret_cast<const f32x4*>(rp + 64 * j);
+                                }
+                            }
+#pragma unroll
+                            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                                for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                                    for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vv[k][j][r], accn[qd][j][r]);
+                        }
+                    }
+                }
+            }
+        }
+
+        // ---- (P1) phase B of tile s - 1, its split and residual seeds
+        constexpr int NSEED = AGG ? 1 : IBW;
+        f32x4 seed[NSEED];
+        if (prv >= 0) {
+#pragma unroll
+            for (int qd = 0; qd < C::NQ; ++qd) {
+                const uint32_t a = decode(ncode[qd]);
+#pragma unroll
+                for (int j = 0; j < C::CH; ++j) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) accp[qd][j][r] = fmaf(nwt[qd], v[r], accp[qd][j][r]);
+                }
+            }
+            if constexpr (!AGG) {
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) m = max(m, __float_as_uint(fabsf(accp[qd][j][r])));
+                    m = wrow_max(m);
+                    const int pe = wsplit_exp(m);
+                    const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
+                    const int lrow = 8 * wave + 4 * qd + gq;
+                    const int sw = asw<H>(lrow);
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j) {
+                        f16x4w hv, lv;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float sv = accp[qd][j][r] * sc;
+                            const _Float16 hh = static_cast<_Float16>(sv);
+                            hv[r] = hh;
+                            lv[r] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                        }
+                        const int cc = c0 + 16 * j;             // the lane's 16-B fp32 chunk
+                        const int ao = lrow * H + 8 * ((cc >> 1) ^ sw) + 4 * (cc & 1);
+                        *reinterpret_cast<f16x4w*>(&AH[ao]) = hv;
+                        *reinterpret_cast<f16x4w*>(&AL[ao]) = lv;
+                    }
+                    if (iq == 0) {
+                        // (the row index recomputed from an opaque lane: hoisted
+                        // out of the step loop it is a register too many at H = 64)
+                        int lo = lane;
+                        asm volatile("" : "+v"(lo));
+                        REXP[8 * wave + 4 * qd + (lo >> 4)] = pe;
+                    }
+                }
+                // residual + bias of my output block (tile s-1's rows of my
+                // row group, my 16 columns), before slot (s-1) % 3 is refilled
+                const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[n0 + 4 * gg]);
+#pragma unroll
+                for (int ib = 0; ib < IBW; ++ib) {
+                    const int lr = (wm * IBW + ib) * 16 + rr;
+                    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (has_res) {
+                        const int ch = (n0 >> 2) + gg;
+                        rv = *reinterpret_cast<const float4*>(XP + lr * C::ROWB + ((ch ^ (lr & 7)) << 4));
+                    }
+                    seed[ib] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
+                }
+            }
+        }
+        // (B2) A image complete; every read of slot (s-1) % 3, the ext area
+        // and this step's records done
+        wbar<kWLgkm0>();
+        // the records of step s + 1 landed (younger: the own rows of tile s + 1
+        // and the last step's stores)
+        if (s == 0) wwait<wvm(0)>();
+        else if (s == 1) wwait<wvm(C::NPX)>();
+        else wwait<wvm(C::NPX + C::NST)>();
+        const int64_t tn1 = tile_of(s + 1), tn2 = tile_of(s + 2);
+        const unsigned char* es[C::NPE];
+#pragma unroll
+        for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
+        // DMA piece q of this step: ext rows of step s + 1, the records of step
+        // s + 2 (into this step's TAB slot), the own rows of tile s + 2
+        auto dma_piece = [&](int q) {
+            if (q < C::NPE) ext_dma(q, es[q]);
+            else if (q == C::NPE) dma_tab(tn2, tq);
+            else dma_own(tn2, xn2, q - C::NPE - 1);
+        };
+        constexpr int NPC = C::NPE + 1 + C::NPX;
+
+        if (prv >= 0) {
+            if constexpr (AGG) {
+#pragma unroll
+                for (int q = 0; q < NPC; ++q) dma_piece(q);
+                static_assert(!AGG || C::NQ * C::CH == C::NST, "aggregate stores keep the per-step store count");
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j) {
+                        // (a partial tile is the last of its workgroup: fewer stores
+                        // there change no later wait)
+                        const int lrow = 8 * wave + 4 * qd + gq;
+                        if (lrow < nlocp)
+                            __builtin_nontemporal_store(accp[qd][j], reinterpret_cast<f32x4*>(out + (tp0 + lrow) * ldo + 4 * (c0 + 16 * j)));
+                    }
+            } else {
+                // (3) transform: my 16 output columns x my row blocks
+                int pr[IBW];
+                f32x4 accm[IBW];
+#pragma unroll
+                for (int ib = 0; ib < IBW; ++ib) {
+                    pr[ib] = REXP[(wm * IBW + ib) * 16 + rr];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) accm[ib][r] = ldexpf(seed[ib][r], pr[ib] + qw);
+                }
+                {
+                    const int sw = asw<H>(rr);
+                    auto frag = [&](int t, f16x8w& bh, f16x8w& bl) {
+                        const int kc = t / IBW, ib = t % IBW;
+                        const int R = (wm * IBW + ib) * 16 + rr;
+                        const int ao = R * H + 8 * ((4 * kc + gg) ^ sw);
+                        bh = *reinterpret_cast<const f16x8w*>(&AH[ao]);
+                        bl = *reinterpret_cast<const f16x8w*>(&AL[ao]);
+                    };
+                    __builtin_amdgcn_sched_barrier(0);
+                    constexpr int PD = 1, NF = PD + 1, NTT = C::KC * IBW;
+                    f16x8w fh[NF], fl[NF];
+#pragma unroll
+                    for (int t = 0; t < PD && t < NTT; ++t) frag(t, fh[t], fl[t]);
+#pragma unroll
+                    for (int t = 0; t < NTT; ++t) {
+                        const int kc = t / IBW, ib = t % IBW;
+                        if (t < NPC) dma_piece(t);
+                        if (MODE & 4) continue;
+                        if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
+                        accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fh[t % NF], accm[ib], 0, 0, 0);
+                        accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fl[t % NF], accm[ib], 0, 0, 0);
+                        accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[kc], fh[t % NF], accm[ib], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int t = NTT; t < NPC; ++t) dma_piece(t);
+                }
+                // (B3) every wave done with the A image: stage there
+                wbar<kWLgkm0>();
+                {
+                    const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 4 * gg]);
+                    const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + n0 + 4 * gg]);
+#pragma unroll
+                    for (int ib = 0; ib < IBW; ++ib) {
+                        float o[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float v = ldexpf(accm[ib][r], -(pr[ib] + qw));
+                            if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
+                            if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
+                            o[r] = v;
+                        }
+                        const int lr = (wm * IBW + ib) * 16 + rr;
+                        const int ch = (n0 >> 2) + gg;
+                        *reinterpret_cast<f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4)) =
+                            f32x4{o[0], o[1], o[2], o[3]};
+                    }
+                }
+                // (B4) staged: my 8 rows out, whole rows
+                wbar<kWLgkm0>();
+                {
+                    const int ch = lane % C::LPRW;
+                    f32x4 v[C::NST];
+#pragma unroll
+                    for (int i = 0; i < C::NST; ++i) {
+                        const int lr = 8 * wave + i * C::RPI + lane / C::LPRW;
+                        v[i] = *reinterpret_cast<const f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4));
+                    }
+#pragma unroll
+                    for (int i = 0; i < C::NST; ++i) {
+                        const int lr = 8 * wave + i * C::RPI + lane / C::LPRW;
+                        if (lr < nlocp)
+                            __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NPC; ++q) dma_piece(q);
+        }
+        // carry tile s into phase B
+#pragma unroll
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            ncode[qd] = ncn[qd];
+            nwt[qd] = nwn[qd];
+#pragma unroll
+            for (int j = 0; j < C::CH; ++j) accp[qd][j] = accn[qd][j];
+        }
+        xs = xs == 2 ? 0 : xs + 1;
+    }
+    wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
+}
+
+template <int H, int MODE, int EPIF>
+void launch_win_k(int G, hipStream_t st, const void* plan, const int32_t* row_ptr,
+                  const int32_t* col, const float* ew, const float* x, int64_t ldx, int64_t rb,
+                  int64_t re, const float* w, const float* bias, const float* scale,
+                  const float* shift, int flags, float* out, int64_t ldo) {
+    hipLaunchKernelGGL((gcn_win_kernel<H, MODE, EPIF>), dim3(G), dim3(WCfg<H>::NT), 0, st,
+                       static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb, re, w,
+                       bias, scale, shift, flags, out, ldo);
+}
+
+template <int H, int MODE>
+void launch_win_h(int G, hipStream_t st, const void* plan, const int32_t* row_ptr,
+                  const int32_t* col, const float* ew, const float* x, int64_t ldx, int64_t rb,
+                  int64_t re, const float* w, const float* bias, const float* scale,
+                  const float* shift, int flags, float* out, int64_t ldo) {
+    constexpr int kBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE | MIGNN_EPI_RELU;
+    constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
+    if (MODE == 0 && flags == kBN)
+        launch_win_k<H, MODE, kBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+    else if (MODE == 0 && flags == kNoBN)
+        launch_win_k<H, MODE, kNoBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+    else
+        launch_win_k<H, MODE, -1>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+}
+
+template <int MODE = 0>
+int launch_win(int h, const void* plan, const int32_t* row_ptr, const int32_t* col,
+               const float* ew, const float* x, int64_t ldx, int64_t rb, int64_t re,
+               const float* w, const float* bias, const float* scale, const float* shift,
+               int flags, float* out, int64_t ldo, hipStream_t st) {
+    const int64_t ntiles = (re - rb + 63) / 64;
+    const int G = win_grid(ntiles, h == 128 ? WCfg<128>::WGPC : WCfg<64>::WGPC);
+    MIGNN_REQUIRE(G > 0, "gcn_win: device query failed");
+    if (h == 128)
+        launch_win_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+    else
+        launch_win_h<64, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+    return launch_status("gcn_win_kernel");
+}
+
+}  // namespace
+
+int win_device_errors(unsigned int* out, int clear) {
+    unsigned int v = 0u;
+    MIGNN_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_win_errors), sizeof(unsigned int), 0,
+                                  hipMemcpyDeviceToHost));
+    *out |= v;
+    if (clear) {
+        const unsigned int zero = 0u;
+        MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_win_errors), &zero, sizeof(unsigned int), 0,
+                                    hipMemcpyHostToDevice));
+    }
+    return MIGNN_OK;
+}
+
+}  // namespace mignn
+
+using namespace mignn;
+
+extern "C" size_t mignn_gcn_win_plan_bytes(int64_t row_begin, int64_t row_end, int h) {
+    if (row_end <= row_begin || (h != 64 && h != 128)) return 0;
+    const int64_t ntiles = (row_end - row_begin + 63) / 64;
+    return kWHdr + static_cast<size_t>(ntiles) * (h == 128 ? WCfg<128>::TAB_BYTES : WCfg<64>::TAB_BYTES);
+}
+
+extern "C" int mignn_gcn_win_plan(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                                  int64_t rb, int64_t re, int h, const int32_t* order_info,
+                                  void* plan, size_t plan_bytes, unsigned long long* stats,
+                                  void* stream) {
+    MIGNN_REQUIRE(row_ptr && col && ew && plan, "gcn_win_plan: null pointer");
+    MIGNN_REQUIRE(h == 64 || h == 128, "gcn_win_plan: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_win_plan: bad row range");
+    MIGNN_REQUIRE(aligned16(plan), "gcn_win_plan: unaligned plan");
+    if (re == rb) return MIGNN_OK;
+    MIGNN_REQUIRE(plan_bytes >= mignn_gcn_win_plan_bytes(rb, re, h), "gcn_win_plan: plan buffer too small");
+    const int64_t ntiles = (re - rb + 63) / 64;
+    const int G = win_grid(ntiles, h == 128 ? WCfg<128>::WGPC : WCfg<64>::WGPC);
+    MIGNN_REQUIRE(G > 0, "gcn_win_plan: device query failed");
+    hipStream_t st = as_stream(stream);
+    WinHdr* hdr = static_cast<WinHdr*>(plan);
+    hipLaunchKernelGGL(win_hdr_kernel, dim3(1), dim3(64), 0, st, hdr, order_info, ntiles, G, h, rb, re);
+    int rc = launch_status("win_hdr_kernel");
+    if (rc) return rc;
+    unsigned char* tabs = static_cast<unsigned char*>(plan) + kWHdr;
+    const unsigned grid = static_cast<unsigned>(ntiles < (1 << 20) ? ntiles : (1 << 20));
+    if (h == 128)
+        hipLaunchKernelGGL(win_plan_kernel<128>, dim3(grid), dim3(64), 0, st, row_ptr, col, ew, hdr, tabs, stats);
+    else
+        hipLaunchKernelGGL(win_plan_kernel<64>, dim3(grid), dim3(64), 0, st, row_ptr, col, ew, hdr, tabs, stats);
+    return launch_status("win_plan_kernel");
+}
+
+extern "C" int mignn_gcn_layer_win(const void* plan, const int32_t* row_ptr, const int32_t* col,
+                                   const float* ew, const float* x, int64_t ldx, int64_t rb,
+                                   int64_t re, int h, const float* w, const float* bias,
+                                   const float* scale, const float* shift, int flags, float* out,
+                                   int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(plan && row_ptr && col && ew && x && w && out, "gcn_layer_win: null pointer");
+    MIGNN_REQUIRE(h == 64 || h == 128, "gcn_layer_win: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(aligned16(x) && aligned16(out) && aligned16(plan) && aligned16(w),
+                  "gcn_layer_win: unaligned");
+    MIGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && ldx >= h && ldo >= h, "gcn_layer_win: bad strides");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_layer_win: bad row range");
+    MIGNN_REQUIRE(x != out, "gcn_layer_win: in-place not supported (neighbours read x)");
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer_win: unknown flags 0x%x", flags);
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bias, "gcn_layer_win: bias");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gcn_layer_win: affine");
+    if (re == rb) return MIGNN_OK;
+    return launch_win(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out,
+                      ldo, as_stream(stream));
+}
+
+extern "C" int mignn_gcn_aggregate_win(const void* plan, const int32_t* row_ptr, const int32_t* col,
+                                       const float* ew, const float* x, int64_t ldx, int64_t rb,
+                                       int64_t re, int h, float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(plan && row_ptr && col && ew && x && out, "gcn_aggregate_win: null pointer");
+    MIGNN_REQUIRE(h == 64 || h == 128, "gcn_aggregate_win: h must be 64 or 128 (got %d)", h);
+    MIGNN_REQUIRE(aligned16(x) && aligned16(out) && aligned16(plan), "gcn_aggregate_win: unaligned");
+    MIGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && ldx >= h && ldo >= h,
+                  "gcn_aggregate_win: bad strides");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_aggregate_win: bad row range");
+    MIGNN_REQUIRE(x != out, "gcn_aggregate_win: in-place not supported (neighbours read x)");
+    if (re == rb) return MIGNN_OK;
+    return launch_win<32>(h, plan, row_ptr, col, ew, x, ldx, rb, re, nullptr, nullptr, nullptr,
+                          nullptr, 0, out, ldo, as_stream(stream));
+}
+
+#ifdef MIGNN_DIAG
+extern "C" int mignn_diag_win(int mode, const void* plan, const int32_t* row_ptr,
+                              const int32_t* col, const float* ew, const float* x, int64_t ldx,
+                              int64_t rb, int64_t re, int h, const float* w, const float* bias,
+                              const float* scale, const float* shift, int flags, float* out,
+                              int64_t ldo, void* stream) {
+    hipStream_t st = as_stream(stream);
+    switch (mode) {
+        case 0: return launch_win<0>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        case 1: return launch_win<1>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        case 4: return launch_win<4>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        case 32: return launch_win<32>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        case 33: return launch_win<33>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        default: break;
+    }
+    set_error("diag_win: unknown mode %d", mode);
+    return MIGNN_ERR_ARG;
+}
+#endif

@@ -149,7 +149,22 @@ __global__ __launch_bounds__(kB) void spacing_kernel(const float* __restrict__ p
     }
 }
 
-// per-axis spacing h (edge mean, else extent / cbrt(n)), cells per axis
+// key range of the block order (order_keys_kernel) / of the column order
+// (order_col_keys_kernel, remainder columns included) for a cell grid
+__device__ double block_key_range(const int64_t cells[3]) {
+    return static_cast<double>(((cells[1] + 3) / 4 + 3) / 4) *
+           static_cast<double>(((cells[0] + 3) / 4 + 3) / 4) *
+           static_cast<double>((cells[2] + 3) / 4) * 1024.0;
+}
+__device__ double col_key_range(const int64_t cells[3]) {
+    const double full = static_cast<double>(cells[0] >> 3) * static_cast<double>(cells[1] >> 3);
+    const double all = static_cast<double>((cells[0] + 7) >> 3) * static_cast<double>((cells[1] + 7) >> 3);
+    return (full + all) * static_cast<double>(cells[2]) * 64.0;
+}
+
+// per-axis spacing h (edge mean, else extent / cbrt(n)), cells per axis;
+// coarsened until the order's key range fits 32 bits
+template <bool COLS = false>
 __device__ void order_grid(const OrderStats* st, int64_t n, float lo[3], float inv_h[3],
                            int64_t cells[3]) {
     const double fallback = cbrt(static_cast<double>(n > 0 ? n : 1));
@@ -163,11 +178,9 @@ __device__ void order_grid(const OrderStats* st, int64_t n, float lo[3], float i
         ih[a] = 1.0 / h;
         cells[a] = static_cast<int64_t>(fmin(ext * ih[a] + 0.5, 1.0e15)) + 1;
     }
-    // coarsen until the panel key range (order_keys_kernel) fits 32 bits
+    // coarsen until the key range fits 32 bits
     for (int it = 0; it < 8; ++it) {
-        const double range = static_cast<double>(((cells[1] + 3) / 4 + 3) / 4) *
-                             static_cast<double>(((cells[0] + 3) / 4 + 3) / 4) *
-                             static_cast<double>((cells[2] + 3) / 4) * 1024.0;
+        const double range = COLS ? col_key_range(cells) : block_key_range(cells);
         if (range < 4294967295.0) break;
         const double f = cbrt(range / 2147483648.0) * 1.01;
         for (int a = 0; a < 3; ++a) {
@@ -208,6 +221,63 @@ __global__ __launch_bounds__(kB) void order_keys_kernel(const float* __restrict_
         const uint64_t blk = ((static_cast<uint64_t>(ty >> 2) * npx + (tx >> 2)) * ntz + tz) * 16 +
                              (ty & 3) * 4 + (tx & 3);
         const uint64_t key = blk * 64 + (c[2] & 3) * 16 + (c[1] & 3) * 4 + (c[0] & 3);
+        keys[i] = static_cast<uint32_t>(key);
+        ids[i] = static_cast<int32_t>(i);
+    }
+}
+
+// Column order (mignn_locality_order_cols; the window GCN kernel gcn_win.hip):
+// cells grouped into 8 x 8 columns along the third axis, a column's cells in
+// (z, y, x) order so that each 64-row tile of a full column is one z-plane and
+// its -z / +z neighbours are the previous / next tile.  Full columns
+// (bx < cells_x / 8, by < cells_y / 8) first, in row-major (by, bx) order --
+// a workgroup walks one column along z while its XCD's workgroups walk the
+// next columns of the same y-row (gcn_win.hip's schedule) -- then the
+// remainder columns of the ragged x / y edges in the same (column, z, y, x)
+// order.  key = (col * nz + cz) * 64 + (cy & 7) * 8 + (cx & 7) (+ the full
+// columns' key range for the remainder).  info[0..3] = {1, nz, full
+// columns, full columns per y-row}: the plan's schedule parameters.
+__global__ __launch_bounds__(kB) void order_col_keys_kernel(const float* __restrict__ pos,
+                                                            int64_t ldp, int64_t n,
+                                                            const OrderStats* st,
+                                                            uint32_t* __restrict__ keys,
+                                                            int32_t* __restrict__ ids,
+                                                            int32_t* __restrict__ info) {
+    __shared__ float s_lo[3], s_ih[3];
+    __shared__ int64_t s_cells[3];
+    if (threadIdx.x == 0) {
+        float lo[3], ih[3];
+        int64_t cells[3];
+        order_grid<true>(st, n, lo, ih, cells);
+        for (int a = 0; a < 3; ++a) { s_lo[a] = lo[a]; s_ih[a] = ih[a]; s_cells[a] = cells[a]; }
+        if (blockIdx.x == 0 && info != nullptr) {
+            const int64_t fx = cells[0] >> 3, fy = cells[1] >> 3;
+            info[0] = 1;
+            info[1] = static_cast<int32_t>(cells[2]);
+            info[2] = static_cast<int32_t>(fx * fy);
+            info[3] = static_cast<int32_t>(fx);
+        }
+    }
+    __syncthreads();
+    const int64_t nz = s_cells[2];
+    const int64_t fx = s_cells[0] >> 3, fy = s_cells[1] >> 3;
+    const int64_t ax = (s_cells[0] + 7) >> 3;            // columns per y-row, remainder included
+    const uint64_t full_range = static_cast<uint64_t>(fx * fy) * nz * 64;
+    for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
+        int64_t c[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = (pos[i * ldp + a] - s_lo[a]) * s_ih[a] + 0.5f;
+            int64_t q = v >= 0.f ? static_cast<int64_t>(v) : 0;   // NaN -> 0
+            c[a] = q < s_cells[a] ? q : s_cells[a] - 1;
+        }
+        const int64_t bx = c[0] >> 3, by = c[1] >> 3;
+        const uint64_t inner = static_cast<uint64_t>((c[1] & 7) * 8 + (c[0] & 7));
+        uint64_t key;
+        if (bx < fx && by < fy)
+            key = (static_cast<uint64_t>(by * fx + bx) * nz + c[2]) * 64 + inner;
+        else
+            key = full_range + (static_cast<uint64_t>(by * ax + bx) * nz + c[2]) * 64 + inner;
         keys[i] = static_cast<uint32_t>(key);
         ids[i] = static_cast<int32_t>(i);
     }
@@ -256,10 +326,29 @@ extern "C" size_t mignn_locality_order_scratch_bytes(int64_t n) {
     return order_layout(n, &L) == MIGNN_OK ? L.total : 0;
 }
 
+static int locality_order_impl(const float* pos, int64_t ldp, int64_t n, const int64_t* edge_index,
+                               int64_t E, int32_t* perm, int32_t* inv, int32_t* info, bool cols,
+                               void* scratch, size_t scratch_bytes, void* stream);
+
 extern "C" int mignn_locality_order(const float* pos, int64_t ldp, int64_t n,
                                     const int64_t* edge_index, int64_t E, int32_t* perm,
                                     int32_t* inv, void* scratch, size_t scratch_bytes,
                                     void* stream) {
+    return locality_order_impl(pos, ldp, n, edge_index, E, perm, inv, nullptr, false, scratch,
+                               scratch_bytes, stream);
+}
+
+extern "C" int mignn_locality_order_cols(const float* pos, int64_t ldp, int64_t n,
+                                         const int64_t* edge_index, int64_t E, int32_t* perm,
+                                         int32_t* inv, int32_t* info, void* scratch,
+                                         size_t scratch_bytes, void* stream) {
+    return locality_order_impl(pos, ldp, n, edge_index, E, perm, inv, info, true, scratch,
+                               scratch_bytes, stream);
+}
+
+static int locality_order_impl(const float* pos, int64_t ldp, int64_t n, const int64_t* edge_index,
+                               int64_t E, int32_t* perm, int32_t* inv, int32_t* info, bool cols,
+                               void* scratch, size_t scratch_bytes, void* stream) {
     MIGNN_REQUIRE(n >= 0 && E >= 0 && n < (int64_t(1) << 31), "locality_order: bad sizes");
     MIGNN_REQUIRE(ldp >= 3, "locality_order: pos needs 3 columns (ldp %lld)", (long long)ldp);
     MIGNN_REQUIRE((pos && perm && inv && scratch) || n == 0, "locality_order: null pointer");
@@ -290,9 +379,15 @@ extern "C" int mignn_locality_order(const float* pos, int64_t ldp, int64_t n,
                            dim3(kB), 0, st, pos, ldp, n, edge_index, E, stats);
         if ((rc = launch_status("spacing_kernel"))) return rc;
     }
-    hipLaunchKernelGGL(order_keys_kernel, dim3(grid_for(n, kB, 8192)), dim3(kB), 0, st, pos, ldp,
-                       n, stats, keys_in, ids);
-    if ((rc = launch_status("order_keys_kernel"))) return rc;
+    if (cols) {
+        hipLaunchKernelGGL(order_col_keys_kernel, dim3(grid_for(n, kB, 8192)), dim3(kB), 0, st, pos,
+                           ldp, n, stats, keys_in, ids, info);
+        if ((rc = launch_status("order_col_keys_kernel"))) return rc;
+    } else {
+        hipLaunchKernelGGL(order_keys_kernel, dim3(grid_for(n, kB, 8192)), dim3(kB), 0, st, pos,
+                           ldp, n, stats, keys_in, ids);
+        if ((rc = launch_status("order_keys_kernel"))) return rc;
+    }
     size_t temp = L.temp_bytes;
     hipError_t err = rocprim::radix_sort_pairs(base + L.temp, temp, keys_in, keys_out, ids, perm,
                                                static_cast<size_t>(n), 0u, 32u, st);

@@ -77,6 +77,12 @@ SIGNATURES = {
                                      _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gcn_aggregate_ring": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int,
                                          _P, c_int64, _P]),
+    "mignn_gcn_win_plan_bytes": (c_size_t, [c_int64, c_int64, c_int]),
+    "mignn_gcn_win_plan": (c_int, [_P, _P, _P, c_int64, c_int64, c_int, _P, _P, c_size_t, _P, _P]),
+    "mignn_gcn_layer_win": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
+                                    _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_aggregate_win": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int,
+                                        _P, c_int64, _P]),
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
     "mignn_mlp_head_prep": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, c_int, c_int, _P, c_size_t,
                                     _P]),
@@ -88,6 +94,8 @@ SIGNATURES = {
     "mignn_locality_order_scratch_bytes": (c_size_t, [c_int64]),
     "mignn_locality_order": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P, _P, c_size_t,
                                      _P]),
+    "mignn_locality_order_cols": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P, _P, _P,
+                                          c_size_t, _P]),
     "mignn_gcn_layer0_coords": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,
                                         c_int, _P, c_int64, _P]),
     "mignn_mesh_graph_scratch_bytes": (c_size_t, [c_int64, c_int64]),
@@ -178,6 +186,8 @@ DIAG_SIGNATURES = {
     "mignn_diag_ring_trace": (c_int, [_P]),
     "mignn_diag_ring": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_diag_win": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
+                               _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_diag_set_gat_fused": (c_int, [c_int]),
     "mignn_diag_set_fused_flags": (c_int, [c_int]),
     "mignn_diag_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,
@@ -251,7 +261,9 @@ def check(rc: int, what: str):
 
 
 DEVERR_SPIN = 1
-_DEVERR_NAMES = {DEVERR_SPIN: "a bounded in-kernel wait (LDS hand-off) ran out"}
+DEVERR_PLAN = 2
+_DEVERR_NAMES = {DEVERR_SPIN: "a bounded in-kernel wait (LDS hand-off) ran out",
+                 DEVERR_PLAN: "a window-kernel launch did not match its plan header"}
 
 
 def device_errors(clear: bool = True) -> int:

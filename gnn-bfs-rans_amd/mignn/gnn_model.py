@@ -57,7 +57,7 @@ HEADS = 4  # gnn_model.py:67, :79
 # (H = 64: the ring kernel, two workgroups per CU, 1.39-1.41 ms vs the tile
 # kernel's 1.57-1.59 per 10M-row layer; H = 128: the producer / consumer
 # kernel -- the ring kernel ties it per layer but needs a 0.49 ms plan per graph)
-GCN_KERNEL_AUTO = {64: "ring", 128: "pc"}
+GCN_KERNEL_AUTO = {64: "win", 128: "win"}
 
 
 # ---------------------------------------------------------------------------
@@ -134,13 +134,14 @@ class Csr:
     ids inside the CSR are the internal ids: internal row p is caller node
     perm[p], caller node v is internal row inv[v]."""
     __slots__ = ("row_ptr", "col", "dinv", "ew", "info", "num_nodes", "num_edges", "edge_index",
-                 "perm", "inv", "pos", "key_tensor", "plans")
+                 "perm", "inv", "pos", "key_tensor", "plans", "order_info")
 
     def __init__(self, row_ptr, col, dinv, info, num_nodes, num_edges, edge_index, ew=None):
         self.row_ptr, self.col, self.dinv, self.info = row_ptr, col, dinv, info
         self.num_nodes, self.num_edges, self.edge_index = num_nodes, num_edges, edge_index
         self.ew = ew
         self.perm = self.inv = self.pos = None
+        self.order_info = None   # int32[4] of the column order (mignn_locality_order_cols)
         self.key_tensor = None   # the caller's edge_index the cache key was made from
         self.plans: Dict[Tuple[str, int, int, int], torch.Tensor] = {}
 
@@ -158,6 +159,26 @@ class Csr:
                                              _lib.ptr(self.ew), row_begin, row_end, h,
                                              _lib.ptr(plan), nb, None,
                                              _lib.stream(self.col.device)), "mignn_gcn_ring_plan")
+            self.plans[key] = plan
+        return plan
+
+    def win_plan(self, h: int, row_begin: int, row_end: int) -> torch.Tensor:
+        """The window kernel's plan of rows [row_begin, row_end) for hidden
+        width h (mignn_gcn_win_plan: header with this device's grid and the
+        schedule -- the column schedule when the CSR is in the column order
+        and the plan covers every row -- and a 48-B record per row), built on
+        first use and kept with the CSR (it copies the ew weights)."""
+        key = ("win", h, row_begin, row_end)
+        plan = self.plans.get(key)
+        if plan is None:
+            L = _lib.lib()
+            nb = L.mignn_gcn_win_plan_bytes(row_begin, row_end, h)
+            plan = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.col.device)
+            info = self.order_info if (row_begin == 0 and row_end == self.num_nodes) else None
+            _lib.check(L.mignn_gcn_win_plan(_lib.ptr(self.row_ptr), _lib.ptr(self.col),
+                                            _lib.ptr(self.ew), row_begin, row_end, h,
+                                            _lib.ptr(info), _lib.ptr(plan), nb, None,
+                                            _lib.stream(self.col.device)), "mignn_gcn_win_plan")
             self.plans[key] = plan
         return plan
 
@@ -189,11 +210,13 @@ class Csr:
                                              _lib.stream(self.col.device)), "mignn_gcn_norm")
 
 
-def locality_order(pos: torch.Tensor, edge_index: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def locality_order(pos: torch.Tensor, edge_index: torch.Tensor, cols: bool = False):
     """(perm, inv) of mignn_locality_order: 4x4x4-cell blocks (one 64-row tile
     of the fused layer each) in panels of 4x4 block columns swept along the
     third axis, from the cell centres `pos` [N, >=3]; perm[new] = old id,
-    inv[old] = new."""
+    inv[old] = new.  cols=True: the column order of the window GCN kernel
+    (mignn_locality_order_cols: 8x8-cell columns, z inside) and its info,
+    (perm, inv, info)."""
     dev = pos.device
     n = int(pos.shape[0])
     p = pos if (pos.dtype == torch.float32 and pos.stride(1) == 1) else pos.float().contiguous()
@@ -207,6 +230,13 @@ def locality_order(pos: torch.Tensor, edge_index: torch.Tensor) -> Tuple[torch.T
     if nbytes == 0:
         raise _lib.MignnError("locality order scratch query failed: " + _lib.last_error())
     scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    if cols:
+        info = torch.zeros(4, dtype=torch.int32, device=dev)
+        _lib.check(L.mignn_locality_order_cols(_lib.ptr(p), p.stride(0), n, _lib.ptr(ei),
+                                               int(ei.shape[1]), _lib.ptr(perm), _lib.ptr(inv),
+                                               _lib.ptr(info), _lib.ptr(scratch), nbytes,
+                                               _lib.stream(dev)), "mignn_locality_order_cols")
+        return perm[:n], inv[:n], info
     _lib.check(L.mignn_locality_order(_lib.ptr(p), p.stride(0), n, _lib.ptr(ei), int(ei.shape[1]),
                                       _lib.ptr(perm), _lib.ptr(inv), _lib.ptr(scratch), nbytes,
                                       _lib.stream(dev)), "mignn_locality_order")
@@ -252,27 +282,33 @@ class _CsrCache:
         self.entries: Dict[Tuple, Csr] = {}
 
     @staticmethod
-    def _build(edge_index, num_nodes, mode, pos):
+    def _build(edge_index, num_nodes, mode, pos, cols=False):
         if pos is None:
             return build_csr(edge_index, num_nodes, mode)
-        perm, inv = locality_order(pos, edge_index)
+        info = None
+        if cols:
+            perm, inv, info = locality_order(pos, edge_index, cols=True)
+        else:
+            perm, inv = locality_order(pos, edge_index)
         csr = build_csr(edge_index, num_nodes, mode, relabel=inv)
-        csr.perm, csr.inv, csr.pos = perm, inv, pos
+        csr.perm, csr.inv, csr.pos, csr.order_info = perm, inv, pos, info
         return csr
 
     def get(self, edge_index: torch.Tensor, num_nodes: int, mode: int,
-            pos: Optional[torch.Tensor] = None) -> Csr:
+            pos: Optional[torch.Tensor] = None, cols: bool = False) -> Csr:
+        """cols: the column order (the window GCN kernel's) instead of the
+        block order, when a locality order is requested (pos given)."""
         if self.capacity <= 0:        # caching off: rebuild every forward
-            return self._build(edge_index, num_nodes, mode, pos)
+            return self._build(edge_index, num_nodes, mode, pos, cols)
         key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
                tuple(edge_index.stride()), edge_index.dtype, int(num_nodes), mode,
                str(edge_index.device))
         if pos is not None:
-            key += (pos.data_ptr(), pos._version, tuple(pos.shape), tuple(pos.stride()))
+            key += (pos.data_ptr(), pos._version, tuple(pos.shape), tuple(pos.stride()), bool(cols))
         hit = self.entries.get(key)
         if hit is not None:
             return hit
-        csr = self._build(edge_index, num_nodes, mode, pos)
+        csr = self._build(edge_index, num_nodes, mode, pos, cols)
         # the key holds the caller's storage address: keep that tensor (not
         # only the int64 copy build_csr may have made of an int32 or strided
         # edge_index) alive so the allocator cannot hand its address to the
@@ -436,7 +472,7 @@ class FlowGNN(nn.Module):
         # csrc/gcn_f16x3.hip) or "auto" (the fastest measured per H,
         # GCN_KERNEL_AUTO); read once here, not per forward
         self.gcn_kernel = os.environ.get("MIGNN_GCN_KERNEL", "auto")
-        if self.gcn_kernel not in ("tile", "ring", "pc", "auto"):
+        if self.gcn_kernel not in ("tile", "ring", "pc", "win", "auto"):
             raise ValueError(
                 f"MIGNN_GCN_KERNEL must be auto, tile, ring or pc, got {self.gcn_kernel!r}")
         # kernel-route switches (A/B studies; the defaults are the measured
@@ -493,7 +529,7 @@ class FlowGNN(nn.Module):
         buf_b = torch.empty_like(buf_a)
         mode = CSR_ONE_SELF_LOOP if self.layer_type in ("GCN", "GAT") else CSR_VERBATIM
         pos = xin if self._use_reorder(xin) else None
-        csr = self._csr.get(edge_index, num_nodes, mode, pos)
+        csr = self._csr.get(edge_index, num_nodes, mode, pos, cols=self._column_order())
         self._prepare_plans(csr, 0, num_nodes)
         cur, nxt = buf_a, buf_b
         first = 0
@@ -925,6 +961,14 @@ class FlowGNN(nn.Module):
     def _gcn_kernel(self, H: int) -> str:
         return self.gcn_kernel if self.gcn_kernel != "auto" else GCN_KERNEL_AUTO.get(H, "pc")
 
+    def _column_order(self) -> bool:
+        """The locality order of this model's graphs: the column order when
+        its GCN layers run the window kernel (one z-plane of an 8x8 column
+        per tile), the block order otherwise."""
+        H = self.hidden_dim
+        return (self.layer_type == "GCN" and H in (64, 128) and self.precision == "f16x3"
+                and self._gcn_kernel(H) == "win")
+
     def _prepare_plans(self, csr: "Csr", row_begin: int, row_end: int):
         """Build the per-graph plan of the GCN layer kernel before the layer
         loop (part of the graph setup, with the CSR; not inside a layer)."""
@@ -932,7 +976,9 @@ class FlowGNN(nn.Module):
         if self.layer_type != "GCN" or H not in (64, 128) or self.precision != "f16x3":
             return
         kern = self._gcn_kernel(H)
-        if kern == "ring":
+        if kern == "win":
+            csr.win_plan(H, row_begin, row_end)
+        elif kern == "ring":
             csr.ring_plan(H, row_begin, row_end)
         elif kern == "tile":
             csr.gcn_plan(H, row_begin, row_end)
@@ -1019,7 +1065,14 @@ class FlowGNN(nn.Module):
         if self.layer_type == "GCN":
             w, b = layer.lin.weight, layer.bias
             kern = self._gcn_kernel(H)
-            if H in (64, 128) and self.precision == "f16x3" and kern == "ring":
+            if H in (64, 128) and self.precision == "f16x3" and kern == "win":
+                # the hot kernel: window walk over the CSR's window plan
+                plan = csr.win_plan(H, rb, re)
+                _lib.check(L.mignn_gcn_layer_win(
+                    P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
+                    P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),
+                    "mignn_gcn_layer_win")
+            elif H in (64, 128) and self.precision == "f16x3" and kern == "ring":
                 # the hot kernel: persistent ring over the CSR's ring plan
                 plan = csr.ring_plan(H, rb, re)
                 _lib.check(L.mignn_gcn_layer_ring(

@@ -44,7 +44,10 @@ const char* mignn_last_error(void);
  * fused layer kernel (gcn_f16x3.hip's LDS hand-offs) ran out -- that
  * launch's output is wrong.  Reads (synchronously, after the device is idle)
  * and optionally clears the word of the current device into *out. */
-enum { MIGNN_DEVERR_SPIN = 1 };
+/* MIGNN_DEVERR_PLAN = a window-kernel launch whose plan header does not match
+ * it (another grid size, width or row range: mignn_gcn_win_plan was built for
+ * a different launch); the launch writes nothing. */
+enum { MIGNN_DEVERR_SPIN = 1, MIGNN_DEVERR_PLAN = 2 };
 int mignn_device_errors(unsigned int* out, int clear);
 
 /* ------------------------------------------------------------------------
@@ -100,6 +103,15 @@ size_t mignn_locality_order_scratch_bytes(int64_t n);
 int mignn_locality_order(const float* pos, int64_t ldp, int64_t n, const int64_t* edge_index,
                          int64_t num_edges, int32_t* perm, int32_t* inv, void* scratch,
                          size_t scratch_bytes, void* stream);
+/* Column order (the window GCN kernel's): cells grouped into 8 x 8 columns
+ * along the third axis, a column's cells in (z, y, x) order -- every 64-row
+ * tile of a full column is one z-plane -- full columns first in row-major
+ * (y, x) column order, then the ragged edges' columns.  info (nullable,
+ * device int32[4]) = {1, planes per column, full columns, full columns per
+ * row}: pass it to mignn_gcn_win_plan.  Same scratch as mignn_locality_order. */
+int mignn_locality_order_cols(const float* pos, int64_t ldp, int64_t n, const int64_t* edge_index,
+                              int64_t num_edges, int32_t* perm, int32_t* inv, int32_t* info,
+                              void* scratch, size_t scratch_bytes, void* stream);
 int mignn_csr_build(const int64_t* edge_index, /* [2, E] int64, contiguous */
                     int64_t num_edges, int64_t num_nodes, int mode,
                     int32_t* row_ptr, int32_t* col, float* dinv, int64_t* info,
@@ -325,6 +337,35 @@ int mignn_gcn_layer_ring(const void* plan, const int32_t* row_ptr, const int32_t
 int mignn_gcn_aggregate_ring(const void* plan, const int32_t* row_ptr, const int32_t* col,
                              const float* ew, const float* x, int64_t ldx, int64_t row_begin,
                              int64_t row_end, int h, float* out, int64_t ldo, void* stream);
+/* Window form of the same layer (csrc/gcn_win.hip), the product route at
+ * H = 64 and 128: a tile is a 64-row slice of the node order; a workgroup
+ * walks consecutive tiles (in the column order of mignn_locality_order_cols:
+ * one z-plane of an 8 x 8-cell column after another), keeping the previous
+ * and the current tile in LDS, so only a plane's lateral faces are
+ * out-of-tile rows.  The plan (mignn_gcn_win_plan, size
+ * mignn_gcn_win_plan_bytes; device memory, 16-B aligned) carries a header
+ * with the launch grid and schedule, checked by the layer kernel
+ * (MIGNN_DEVERR_PLAN on a mismatch), and a 48-B record per row.
+ * order_info (nullable: the int32[4] info of mignn_locality_order_cols for
+ * the whole graph, row_begin = 0) selects the column schedule.  Build the plan
+ * on the device that runs the layer.  Sum order: a row's entries in CSR order
+ * except its one next-tile entry, added last.  stats (nullable, device
+ * uint64[4]): tiles over the out-of-tile capacity, rows on the CSR path, rows
+ * with a next-tile entry, max out-of-tile entries of a tile. */
+size_t mignn_gcn_win_plan_bytes(int64_t row_begin, int64_t row_end, int h);
+int mignn_gcn_win_plan(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                       int64_t row_begin, int64_t row_end, int h, const int32_t* order_info,
+                       void* plan, size_t plan_bytes, unsigned long long* stats, void* stream);
+int mignn_gcn_layer_win(const void* plan, const int32_t* row_ptr, const int32_t* col,
+                        const float* ew, const float* x, int64_t ldx, int64_t row_begin,
+                        int64_t row_end, int h, const float* w, const float* bias,
+                        const float* scale, const float* shift, int flags, float* out,
+                        int64_t ldo, void* stream);
+/* The GCN aggregation alone by the window kernel (same plan): out_i =
+ * sum_e ew_e x_{col e}, fp32 (the SURVEY 8(d) "aggregate kernel alone"). */
+int mignn_gcn_aggregate_win(const void* plan, const int32_t* row_ptr, const int32_t* col,
+                            const float* ew, const float* x, int64_t ldx, int64_t row_begin,
+                            int64_t row_end, int h, float* out, int64_t ldo, void* stream);
 /* The GCN aggregation alone over the plan: out_i = sum_e ew_e x_{col e}
  * (= mignn_gcn_aggregate's D^-1/2 (A + I) D^-1/2 x with ew from dinv), fp32;
  * the SURVEY 8(d) "aggregate kernel alone" of the north-star target. */

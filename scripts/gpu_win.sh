@@ -1,0 +1,11 @@
+#!/bin/bash
+# window GCN kernel: GPU parity tests, then the hot-kernel timing study
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_win.py -x -v --timeout 240 --timeout-method thread \
+    > gpurun_out/win_tests.log 2>&1 || { tail -30 gpurun_out/win_tests.log; exit 1; }
+tail -3 gpurun_out/win_tests.log
+WB_MODES=${WB_MODES:-1,4,33} timeout -k 10 400 python -u scripts/win_bench.py \
+    > gpurun_out/win_bench.json 2> gpurun_out/win_bench.err || { tail -20 gpurun_out/win_bench.err; exit 1; }
+cat gpurun_out/win_bench.json

@@ -1,0 +1,148 @@
+"""Hot-kernel timing (round 5): the window GCN layer (mignn_gcn_layer_win, the
+column order) against the producer / consumer kernel (mignn_gcn_layer_f16x3)
+and the ring kernel (mignn_gcn_layer_ring), both in the block order, on the
+bench mesh (250x200x200 periodic hex, 10M nodes); the aggregate alone of the
+window and ring kernels; the window plan build; window ablations
+(mignn_diag_win modes: 1 ext rows from the zero row, 4 no MFMAs, 33
+aggregate with ext from the zero row).  HIP events on the launch stream,
+interleaved rounds, median.  Env: WB_H (comma list, 128,64), WB_GRID,
+WB_REPS, WB_MODES (comma list of diag modes), WB_OLD (0: skip pc / ring).
+Prints one JSON object."""
+import json
+import os
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "gnn-bfs-rans_amd"))
+import torch  # noqa: E402
+
+from mignn import _lib  # noqa: E402
+from mignn.gnn_model import build_csr, locality_order  # noqa: E402
+from mignn.synthetic import grid_graph  # noqa: E402
+
+dev = torch.device("cuda", 0)
+nx, ny, nz = (int(v) for v in os.environ.get("WB_GRID", "250,200,200").split(","))
+pos, ei = grid_graph(nx, ny, nz, device=dev)
+n = pos.shape[0]
+old = os.environ.get("WB_OLD", "1") != "0"
+_, inv_c, info = locality_order(pos, ei, cols=True)
+csr_c = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv_c)
+csr_b = None
+if old:
+    _, inv_b = locality_order(pos, ei)
+    csr_b = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv_b)
+del ei, pos
+nnz = int(csr_c.row_ptr[-1].item())
+L = _lib.diag_lib()
+P = _lib.ptr
+st = _lib.stream()
+reps = int(os.environ.get("WB_REPS", "7"))
+res = {"grid": [nx, ny, nz], "n": n, "nnz": nnz, "order_info": info.tolist(), "by_h": {}}
+
+
+def timed(cases):
+    times = {k: [] for k in cases}
+    for rnd in range(reps + 1):
+        for k, f in cases.items():
+            f()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                f()
+            e1.record()
+            e1.synchronize()
+            if rnd > 0:
+                times[k].append(e0.elapsed_time(e1) / 3)
+    return {k: round(statistics.median(v), 4) for k, v in times.items()}
+
+
+for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(n, H, device=dev, generator=g)
+    W = torch.randn(H, H, device=dev, generator=g) * 0.05
+    b = torch.randn(H, device=dev, generator=g) * 0.05
+    sc = torch.rand(H, device=dev, generator=g) + 0.5
+    sh = torch.randn(H, device=dev, generator=g) * 0.1
+    nbw = L.mignn_gcn_win_plan_bytes(0, n, H)
+    wplan = torch.empty(nbw, dtype=torch.uint8, device=dev)
+    wstats = torch.zeros(4, dtype=torch.int64, device=dev)
+    Yw, Ywa, Yd = torch.empty_like(X), torch.empty_like(X), torch.empty_like(X)
+
+    def mk_wplan(s_=None):
+        _lib.check(L.mignn_gcn_win_plan(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), 0, n, H, P(info),
+                                        P(wplan), nbw, s_, st), "wplan")
+
+    def win():
+        _lib.check(L.mignn_gcn_layer_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
+                                         H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yw), H, st), "win")
+
+    def win_agg():
+        _lib.check(L.mignn_gcn_aggregate_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
+                                             P(X), H, 0, n, H, P(Ywa), H, st), "win_agg")
+
+    mk_wplan(P(wstats))
+    torch.cuda.synchronize()
+    hdr = wplan[:64].cpu()
+    res.setdefault("win_plan_stats", {})[H] = wstats.tolist()
+    res.setdefault("win_header", {})[H] = hdr[:32].view(torch.int32).tolist() + hdr[32:64].view(torch.int64).tolist()
+    cases = {"win_plan": mk_wplan, "win": win, "win_aggregate": win_agg}
+    for m in [int(v) for v in os.environ.get("WB_MODES", "").split(",") if v]:
+        def fw(m=m):
+            _lib.check(L.mignn_diag_win(m, P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
+                                        H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yd), H, st), "dwin")
+        cases[f"win_mode{m}"] = fw
+    if old:
+        Y0, Yr, Yra = torch.empty_like(X), torch.empty_like(X), torch.empty_like(X)
+        nbr = L.mignn_gcn_ring_plan_bytes(0, n, H)
+        rplan = torch.empty(nbr, dtype=torch.uint8, device=dev)
+
+        def pc():
+            _lib.check(L.mignn_gcn_layer_f16x3(P(csr_b.row_ptr), P(csr_b.col), P(csr_b.ew), P(X), H, 0, n,
+                                               H, P(W), P(b), P(sc), P(sh), 15, P(Y0), H, st), "pc")
+
+        def ring():
+            _lib.check(L.mignn_gcn_layer_ring(P(rplan), P(csr_b.row_ptr), P(csr_b.col), P(csr_b.ew), P(X),
+                                              H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yr), H, st),
+                       "ring")
+
+        def ring_agg():
+            _lib.check(L.mignn_gcn_aggregate_ring(P(rplan), P(csr_b.row_ptr), P(csr_b.col), P(csr_b.ew),
+                                                  P(X), H, 0, n, H, P(Yra), H, st), "ring_agg")
+        _lib.check(L.mignn_gcn_ring_plan(P(csr_b.row_ptr), P(csr_b.col), P(csr_b.ew), 0, n, H, P(rplan),
+                                         nbr, None, st), "rplan")
+        cases.update({"pc_f16x3": pc, "ring": ring, "ring_aggregate": ring_agg})
+    # correctness on the bench mesh: the window layer vs the same layer on
+    # the block-order CSR by the pc kernel (rows matched through the orders)
+    win()
+    win_agg()
+    torch.cuda.synchronize()
+    out = {"win_deterministic": None}
+    Yw2 = Yw.clone()
+    win()
+    torch.cuda.synchronize()
+    out["win_deterministic"] = bool(torch.equal(Yw, Yw2))
+    del Yw2
+    if old:
+        pc()
+        torch.cuda.synchronize()
+        # internal row of node v: inv_c[v] (column order), inv_b[v] (block order);
+        # X is indexed by internal rows of each order, so compare on a common X:
+        # rerun pc on the column-order CSR (the kernel is order-agnostic)
+        _lib.check(L.mignn_gcn_layer_f16x3(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X), H, 0, n,
+                                           H, P(W), P(b), P(sc), P(sh), 15, P(Y0), H, st), "pc_c")
+        torch.cuda.synchronize()
+        out["win_vs_pc_max_diff"] = (Yw - Y0).abs().max().item()
+        out["pc_out_absmax"] = Y0.abs().max().item()
+        pc()
+        torch.cuda.synchronize()
+    ms = timed(cases)
+    by = 4 * (2 * n * H + (n + 1) + nnz + n)     # algorithmic bytes of the layer
+    out.update({"ms": ms, "frac_of_8TBps": {k: round(by / (v * 1e-3) / 8e12, 4)
+                                             for k, v in ms.items() if "plan" not in k}})
+    res["by_h"][H] = out
+    print(json.dumps({H: out}), file=sys.stderr, flush=True)
+    del X, Yw, Ywa, Yd, wplan
+    torch.cuda.empty_cache()
+print(json.dumps(res), flush=True)
