@@ -41,8 +41,11 @@ Extra objects on the same JSON line:
                  mignn.dist.FlowGNNShard per rank with the RCCL halo
   cpu_baseline : the CPU oracle (pure-torch restatement of the reference
                  forward, the same op pattern PyG runs on the CPU) timed on
-                 this box's host cores (every CPU this process may run on) on a
-                 bounded 1M-node sample of the headline model (rank 0, N=1).
+                 this box's host cores (the fastest thread count of a sweep)
+                 on the headline workload itself -- GCN L4 H128 on the
+                 250x200x200 mesh, one timed forward in this run (rank 0,
+                 N=1); a 1M-node sample (median of 2, with its accuracy vs
+                 fp64) beside it.
   bfs_mesh     : configs[1]'s model on the reference BFS mesh (train-path
                  graph, 12,225 nodes / 48,330 edges) -- edges/s, max-abs /
                  mean-abs error of the raw [N,7] output vs the committed
@@ -122,6 +125,8 @@ def parse():
     p.add_argument("--no-bfs", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="skip the mesh->graph builder leg")
     p.add_argument("--cpu-grid", default="100,100,100")
+    p.add_argument("--cpu-sample-only", action="store_true",
+                   help="CPU baseline on the --cpu-grid sample only (not the headline mesh)")
     p.add_argument("--no-train", action="store_true", help="skip the training-step leg")
     p.add_argument("--train-grid", default="100,100,100")
     p.add_argument("--no-legs", action="store_true", help="skip the other-config legs")
@@ -525,9 +530,10 @@ LEGS = {
 LEG_CONFIG = {"gcn_h64": "SURVEY 8d H=64 HBM-target layer", "shuffled": "configs[1] model, shuffled order",
               "gat": "configs[2]", "transformer": "configs[3]",
               "gin": "configs[4] model, one GPU's shard of the 100M mesh"}
-# bounded CPU samples of each leg's model (a few seconds of oracle work each;
-# the CPU path is O(L E H + L N H^2) with no cache effects at these sizes, so
-# its edges/s is taken as size-independent and stated as such)
+# bounded CPU samples of each leg's model (a few seconds of oracle work each,
+# timed on a smaller mesh than the leg's: the CPU rate is not size-independent
+# -- the headline's 10M-node CPU forward runs at ~0.7x its 1M-node rate -- so
+# each leg's cpu_baseline names its sample size)
 LEG_CPU_SAMPLE = {"gcn_h64": (100, 100, 100), "shuffled": (80, 80, 80), "gat": (60, 60, 60),
                   "transformer": (40, 40, 32), "gin": (50, 50, 40)}
 
@@ -657,8 +663,7 @@ def eval_leg(name, dev, precision, steps, warmup, cpu_threads=None):
             "sample": f"{lt} L{L} H{H} forward on the {cdims[0]}x{cdims[1]}x{cdims[2]} periodic "
                       f"mesh ({xc.shape[0]} nodes, {eic.shape[1]} edges"
                       + (", shuffled" if shuffle is not None else "") + "), torch-CPU oracle "
-                      "fp32, one timed run; edges/s taken as size-independent (not timed at "
-                      "the leg's full size)",
+                      "fp32, one timed run on this bounded sample (not the leg's full size)",
             "gpu_over_cpu": round(out["edges_per_s"] / (L * eic.shape[1] / tc), 1)}
     return out
 
@@ -905,7 +910,10 @@ def graph_build_leg(dev, nx, ny, nz, with_cpu):
 
 
 def cpu_leg(model, sd, cfg, args, dev, cpu_threads):
-    """The CPU oracle on a bounded sample of the same workload (1M-node mesh)."""
+    """The CPU oracle on the headline workload itself (args.grid, one timed
+    forward: ~80 s on 32 host threads at 10M nodes) and, beside it, on a
+    1M-node sample (median of 2 after a warm-up, with the accuracy of both
+    fp32 paths against fp64 there)."""
     from oracle import flowgnn_oracle as orc
     from mignn.synthetic import grid_graph
 
@@ -913,6 +921,18 @@ def cpu_leg(model, sd, cfg, args, dev, cpu_threads):
     avail = cpu_threads["cpus_available"]
     sweep = cpu_threads["sweep_s_40x40x40"]
     torch.set_num_threads(threads)
+    full = None
+    if not args.cpu_sample_only:
+        nx, ny, nz = (int(v) for v in args.grid.split(","))
+        xf, eif = (t.cpu() for t in grid_graph(nx, ny, nz, device=dev))
+        progress(f"cpu baseline: the headline forward on {xf.shape[0]} nodes (one timed run)")
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            orc.flowgnn_forward(sd, cfg, xf, eif, None, dtype=torch.float32)
+        tf = time.perf_counter() - t0
+        full = {"value": cfg["num_layers"] * eif.shape[1] / tf, "s_per_forward": round(tf, 3),
+                "nodes": int(xf.shape[0]), "edges": int(eif.shape[1])}
+        del xf, eif
     cx, cy, cz = (int(v) for v in args.cpu_grid.split(","))
     xg, eig = grid_graph(cx, cy, cz, device=dev)
     with torch.no_grad():
@@ -942,16 +962,25 @@ def cpu_leg(model, sd, cfg, args, dev, cpu_threads):
                 break
     except OSError:
         pass
-    return {"value": cfg["num_layers"] * ei.shape[1] / t, "unit": "edges/s", "cores": threads,
+    sample_1m = {"value": cfg["num_layers"] * ei.shape[1] / t, "s_per_forward": round(t, 3),
+                 "sample": f"{cx}x{cy}x{cz} periodic mesh ({x.shape[0]} nodes, {ei.shape[1]} "
+                           f"edges), median of 2 after 1 warm-up",
+                 "accuracy": acc}
+    wl = (f"{cfg['layer_type']} L{cfg['num_layers']} H{cfg['hidden_dim']} forward, torch-CPU oracle "
+          f"fp32 (the reference forward's op pattern), {threads} threads")
+    if full is not None:
+        value, s_fwd = full["value"], full["s_per_forward"]
+        sample = (f"{wl}, on the headline mesh itself ({args.grid.replace(',', 'x')}: "
+                  f"{full['nodes']} nodes, {full['edges']} edges), one timed forward in this run "
+                  f"(after the thread sweep's warm-up)")
+    else:
+        value, s_fwd = sample_1m["value"], sample_1m["s_per_forward"]
+        sample = f"{wl}, on the {cx}x{cy}x{cz} sample only (--cpu-sample-only)"
+    return {"value": value, "unit": "edges/s", "cores": threads,
             "os_cpu_count": os.cpu_count(), "cpus_available": avail,
             "thread_sweep_s_40x40x40": sweep,
-            "kind": "port",
-            "sample": f"{cfg['layer_type']} L{cfg['num_layers']} H{cfg['hidden_dim']} forward on "
-                      f"the {cx}x{cy}x{cz} periodic mesh ({x.shape[0]} nodes, {ei.shape[1]} edges), "
-                      f"torch-CPU oracle fp32, median of 2 after 1 warm-up; the CPU path is "
-                      f"O(L E H) with no cache effects at this size, so its edges/s is taken as "
-                      f"size-independent (extrapolated to the 10M headline mesh, not timed there)",
-            "s_per_forward": round(t, 3), "cpu_model": cpu_model, "accuracy_1M": acc,
+            "kind": "port", "sample": sample, "s_per_forward": s_fwd, "cpu_model": cpu_model,
+            "sample_1M": sample_1m, "accuracy_1M": acc,
             "full_size": cpu_full_record()}
 
 

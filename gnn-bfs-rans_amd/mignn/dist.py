@@ -37,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 TAG_HALO = 17
+TAG_EXTRA = 18          # the second per-layer exchange (sharded GAT: ghost logits)
 
 
 # ---------------------------------------------------------------------------
@@ -248,13 +249,24 @@ class DistExchange:
     def __init__(self, group=None):
         self.group = group
         self._staged = None
+        # per-peer pack buffers, allocated once per (peer, width, dtype,
+        # device) and reused by every layer (a layer's sends complete --
+        # wait() -- before the next layer packs)
+        self._pack: Dict[tuple, torch.Tensor] = {}
 
     def _stage(self, buf) -> bool:
         if self._staged is None:
             self._staged = dist.get_backend(self.group) != "nccl"
         return self._staged and buf.is_cuda
 
-    def start(self, shards, bufs):
+    def _pack_buf(self, q, n, buf):
+        key = (q, n, buf.shape[1], buf.dtype, str(buf.device))
+        pk = self._pack.get(key)
+        if pk is None:
+            pk = self._pack[key] = torch.empty((n, buf.shape[1]), dtype=buf.dtype, device=buf.device)
+        return pk
+
+    def start(self, shards, bufs, tag: int = TAG_HALO):
         (sh,), (buf,) = shards, bufs
         lay = sh.layout
         stage = self._stage(buf)
@@ -262,10 +274,9 @@ class DistExchange:
         for q in lay.peers():
             if q in lay.send_idx:
                 idx = lay.send_idx[q]
-                pk = torch.empty((idx.numel(), buf.shape[1]), dtype=buf.dtype, device=buf.device)
+                pk = self._pack_buf(q, idx.numel(), buf)
                 _gather_rows(buf, idx, pk)
-                ops.append(dist.P2POp(dist.isend, pk.cpu() if stage else pk, q, self.group,
-                                      TAG_HALO))
+                ops.append(dist.P2POp(dist.isend, pk.cpu() if stage else pk, q, self.group, tag))
             sl = lay.ghost_slice(q)
             if sl.stop > sl.start:
                 dst = buf[sl]
@@ -273,7 +284,7 @@ class DistExchange:
                     host = torch.empty(dst.shape, dtype=dst.dtype)
                     unstage.append((dst, host))
                     dst = host
-                ops.append(dist.P2POp(dist.irecv, dst, q, self.group, TAG_HALO))
+                ops.append(dist.P2POp(dist.irecv, dst, q, self.group, tag))
         return (dist.batch_isend_irecv(ops) if ops else [], unstage)
 
     def wait(self, handle):
@@ -289,7 +300,7 @@ class LocalExchange:
     into the receiving shard's ghost slice (the stream orders the copies
     before the boundary rows' launches)."""
 
-    def start(self, shards, bufs):
+    def start(self, shards, bufs, tag: int = TAG_HALO):
         for r, sh in enumerate(shards):
             for q, idx in sh.layout.send_idx.items():
                 dst = bufs[q][shards[q].layout.ghost_slice(r)]
@@ -326,7 +337,9 @@ class Shard:
     def halo_extra(self, i: int) -> Optional[torch.Tensor]:
         """A second per-row tensor whose ghost rows travel with layer i's
         feature halo (sharded GAT: the logits the previous layer's epilogue
-        formed), or None."""
+        formed), or None.  Must be decided by the model configuration and i
+        alone -- the same on every rank -- since every rank posts (or skips)
+        the second exchange on its own (tag TAG_EXTRA)."""
         return None
 
     def end_layer(self, i: int) -> None:
@@ -360,7 +373,9 @@ def sharded_forward(shards: List[Shard], exchange, xs_own: List[torch.Tensor]) -
     for i in range(first, shards[0].num_layers):
         h = exchange.start(shards, cur)
         extra = [sh.halo_extra(i) for sh in shards]
-        h2 = exchange.start(shards, extra) if all(e is not None for e in extra) else None
+        if any(e is not None for e in extra) and not all(e is not None for e in extra):
+            raise RuntimeError(f"layer {i}: halo_extra differs between shards")
+        h2 = exchange.start(shards, extra, tag=TAG_EXTRA) if extra[0] is not None else None
         for sh, x, o in zip(shards, cur, nxt):
             sh.before_halo(i, x)
             sh.layer(i, x, o, 0, sh.layout.n_int)
@@ -377,13 +392,17 @@ def sharded_forward(shards: List[Shard], exchange, xs_own: List[torch.Tensor]) -
 
 class FlowGNNShard(Shard):
     """GPU shard: FlowGNN's native layers on the rank-local CSR (owned rows
-    in the interior/boundary locality order, then the ghosts).  The route is
-    the one FlowGNN.forward takes on one GPU: layer 0 composed with
-    input_proj from the coordinates (GCN, GIN H=256, GAT, TransformerConv:
-    FlowGNN._layer0_kind) with the ghost coordinates exchanged once per
-    layout, so layer 0 moves no feature halo; GAT layers form the next
-    layer's logits in their epilogue and the ghost rows' logits travel with
-    the feature halo (no logit GEMV)."""
+    in the interior/boundary locality order, then the ghosts).  Layer 0 is
+    composed with input_proj from the coordinates as on one GPU (GCN, GIN
+    H=256, GAT, TransformerConv: FlowGNN._layer0_kind), with the ghost
+    coordinates exchanged once per layout, so layer 0 moves no feature halo.
+    One difference from the 1-GPU route: sharded GAT forms every next
+    layer's logits in the layer's epilogue -- layer 0's collapsed kernel
+    included (mignn_gat_layer0_coords with logits_next) -- and the ghost
+    rows' logits travel in a second exchange (tag TAG_EXTRA), so no rank runs
+    a logit GEMV on ghost rows; the 1-GPU forward forms layer 1's logits by
+    a GEMV (measured faster there).  The two routes agree up to fp32
+    summation order."""
 
     def __init__(self, model, layout: RangeLayout, x_own: torch.Tensor):
         self.model, self.layout = model, layout

@@ -105,6 +105,59 @@ class OracleShard(Shard):
         return y[self.layout.inv]                       # local order -> owned (global) order
 
 
+class ChainedGatShard(OracleShard):
+    """OracleShard for GAT whose layers take their attention logits from a
+    [n_total, 8] tensor: layer i's owned rows' logits are formed from the
+    previous layer's output rows (layer 0's from input_proj), and the ghost
+    rows' logits arrive by the second halo exchange (halo_extra, tag
+    TAG_EXTRA) -- FlowGNNShard's sharded GAT route, in float64."""
+
+    def _logits(self, i, rows):
+        p = f"gnn_layers.{i}."
+        W = self.sd[orc.gat_weight(self.sd, p)]
+        C = W.shape[0] // 4
+        h = (rows @ W.T).view(-1, 4, C)
+        return torch.cat([(h * self.sd[p + "att_src"]).sum(-1), (h * self.sd[p + "att_dst"]).sum(-1)], 1)
+
+    def first_layer(self, x_own, buf):
+        r = super().first_layer(x_own, buf)
+        n = self.layout.n_own
+        self.lg = torch.full((self.layout.n_total, 8), float("nan"), dtype=torch.float64)
+        self.lg[:n] = self._logits(0, buf[:n])
+        self.lg_next = torch.full_like(self.lg, float("nan"))
+        return r
+
+    def halo_extra(self, i):
+        return self.lg
+
+    def layer(self, i, x, out, rb, re):
+        if re <= rb:
+            return
+        sel = (self.dst >= rb) & (self.dst < re)
+        s, d = self.src[sel], self.dst[sel] - rb
+        n = re - rb
+        p = f"gnn_layers.{i}."
+        sd = self.sd
+        W = sd[orc.gat_weight(sd, p)]
+        C = W.shape[0] // 4
+        h = (x @ W.T).view(-1, 4, C)
+        assert not torch.isnan(self.lg[s]).any()           # ghost logits landed
+        e = torch.nn.functional.leaky_relu(self.lg[s, :4] + self.lg[d + rb, 4:], 0.2)
+        alpha = orc.segment_softmax(e, d, n)
+        xn = torch.zeros(n, 4, C, dtype=x.dtype).index_add_(
+            0, d, h[s] * alpha.unsqueeze(-1)).mean(1) + sd[p + "bias"]
+        b = f"batch_norms.{i}.module."
+        y = orc.batch_norm_eval(x[rb:re] + xn, sd[b + "weight"], sd[b + "bias"],
+                                sd[b + "running_mean"], sd[b + "running_var"])
+        out[rb:re] = torch.relu(y)
+        if i + 1 < self.num_layers:
+            self.lg_next[rb:re] = self._logits(i + 1, out[rb:re])
+
+    def end_layer(self, i):
+        self.lg, self.lg_next = self.lg_next, self.lg
+        self.lg_next.fill_(float("nan"))
+
+
 def _graph(shuffle):
     x, ei = grid_graph_np(NX, NY, NZ)
     x, ei = torch.from_numpy(x), torch.from_numpy(ei)
@@ -135,12 +188,13 @@ def _worker(rank, world, port, layer_type, shuffle, outdir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     torch.set_num_threads(1)
-    cfg, sd = _cfg(layer_type)
+    chained = layer_type == "GAT_chained"
+    cfg, sd = _cfg("GAT" if chained else layer_type)
     x, ei = _graph(shuffle)
     b = range_bounds(x.shape[0], world)
     mine = ei[:, (ei[1] >= b[rank]) & (ei[1] < b[rank + 1])]       # my in-edges, global ids
     lay = RangeLayout(mine, b, rank, DistRequests())
-    sh = OracleShard(sd, cfg, lay)
+    sh = (ChainedGatShard if chained else OracleShard)(sd, cfg, lay)
     ex = DistExchange()
     sh.setup(ex)
     (y,) = sharded_forward([sh], ex, [x[b[rank]:b[rank + 1]].double()])
@@ -151,13 +205,15 @@ def _worker(rank, world, port, layer_type, shuffle, outdir):
 
 @pytest.mark.parametrize("shuffle", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("layer_type", ["GCN", "GIN", "GAT", "Transformer"])
+@pytest.mark.parametrize("layer_type", ["GCN", "GIN", "GAT", "Transformer", "GAT_chained"])
 def test_sharded_forward_matches_single_process(world, layer_type, shuffle):
+    """GAT_chained: the sharded GAT route's second exchange (ghost logits,
+    tag TAG_EXTRA) posted beside the feature halo at every layer."""
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), layer_type, shuffle, d), nprocs=world,
                  join=True)
         ys = [torch.load(os.path.join(d, f"y{r}.pt"), weights_only=True) for r in range(world)]
-    cfg, sd = _cfg(layer_type)
+    cfg, sd = _cfg("GAT" if layer_type == "GAT_chained" else layer_type)
     x, ei = _graph(shuffle)
     ref = orc.flowgnn_forward(sd, cfg, x, ei, None, dtype=torch.float64)
     got = torch.cat(ys, 0)

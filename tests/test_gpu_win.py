@@ -111,7 +111,9 @@ def test_gcn_layer_win(H, case):
     """vs fp64 and vs the producer / consumer kernel: in-window, ext-area,
     next-tile and CSR-path (shuffled order, hub rows) entries, row ranges,
     partial tiles, strides, every node order."""
-    dims = {"small": (13, 11, 3), "strided": (23, 7, 5)}.get(case, (40, 30, 20))
+    # (the column orders: a grid whose workgroups walk 4 tiles -- next-tile entries)
+    dims = {"small": (13, 11, 3), "strided": (23, 7, 5), "cols": (64, 48, 40),
+            "hub_cols": (64, 48, 40)}.get(case, (40, 30, 20))
     csr, n, info = _graph("natural" if case in ("small", "strided") else case, dims)
     g, W, b, sc, sh = _weights(H, H + 3)
     ld = H + 12 if case == "strided" else H
