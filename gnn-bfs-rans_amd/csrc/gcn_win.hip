@@ -62,10 +62,16 @@ constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the ne
 constexpr int kWHdr = 256;                // plan header bytes
 constexpr uint32_t kWMagic = 0x4E495747u;
 
+// H = 128: the A-image kernel (gcn_win_kernel).  8 waves per workgroup, one
+// workgroup per CU.  (16 waves -- four per SIMD, RPW = 4 -- measured slower:
+// 3.27 vs 2.94 ms per 10M-row layer, the aggregate alone faster: 2.16 vs
+// 2.26 ms)
 template <int H>
 struct WCfg {
-    static_assert(H == 64 || H == 128, "window GCN layer: H in {64, 128}");
+    static_assert(H == 128, "window GCN layer, A-image form: H = 128");
+    static constexpr int SWZ = 7;                      // own / ext row swizzle: chunk ^ (row & SWZ)
     static constexpr int BM = 64, NW = 8, NT = NW * 64;
+    static constexpr int RPW = BM / NW;                // rows per wave (quad layout: RPW / 4 quads)
     static constexpr int F = H / 16, CH = F / 4;       // floats / 16-B chunks per lane of a row
     static constexpr int ROWB = H * 4;
     static constexpr int X_BYTES = BM * ROWB;
@@ -73,8 +79,9 @@ struct WCfg {
     static constexpr int KX = 32;                      // ext rows per tile (an 8x8 plane's faces)
     static constexpr int EXT_BYTES = KX * ROWB;
     static constexpr int EPW = KX / NW;                // ext rows DMA'd per wave
-    static constexpr int XLW = 8;                      // ext-list group per wave: EPW columns, summary
-    static constexpr int RECW = 8 * kWRec + XLW * 4;   // a wave's records + list in LDS
+    static constexpr int XLW = (EPW + 4) / 4 * 4;      // ext-list group per wave: EPW columns, summary
+    static constexpr int RECW = RPW * kWRec + XLW * 4; // a wave's records + list in LDS
+    static constexpr int RLANES = RPW * kWRec / 16;    // lanes of the records' DMA
     static constexpr int TLANES = RECW / 16;
     static constexpr int TAB_BYTES = BM * kWRec + NW * XLW * 4;
     static constexpr int A_BYTES = BM * H * 2;         // hi or lo image (16-B chunks swizzled)
@@ -92,18 +99,63 @@ struct WCfg {
     static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
     static constexpr int OFF_STG = OFF_AH;             // output staging (fp32 rows) over AH | AL
     static constexpr int WGPC = H == 64 ? 2 : 1;       // workgroups per CU
-    static constexpr int NQ = 2;                       // row quads per wave (8 rows)
+    static constexpr int NQ = RPW / 4;                 // row quads per wave
     static constexpr int KC = H / 32;
     static constexpr int RPP = 1024 / ROWB, LPR = 64 / RPP;   // rows / lanes per row of a DMA piece
     static constexpr int NPX = X_BYTES / 1024 / NW;    // own-row pieces per wave
     static constexpr int NPE = EXT_BYTES / 1024 / NW;  // ext pieces per wave
     static constexpr int LPRW = ROWB / 16, RPI = 64 / LPRW;
-    static constexpr int NST = 8 / RPI;                // row stores per wave (8 rows)
+    static constexpr int NST = RPW / RPI;              // row stores per wave
     static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
     static_assert(2 * A_BYTES >= BM * ROWB, "staging fits the A images");
     static_assert(EPW == NPE * RPP && EPW + 1 <= XLW, "ext rows per wave");
     static_assert((CODE_END >> CSH) <= 65536, "u16 codes");
     static_assert(RECW % 16 == 0 && TLANES <= 64 && TAB_BYTES % 16 == 0, "records DMA");
+};
+
+// H = 64: the wave-independent kernel (gcn_win64_kernel).  4 waves of 16 rows
+// per workgroup, two workgroups per CU (2 waves per SIMD, 256 VGPRs): each
+// wave aggregates its rows straight into the MFMA B-operand layout (lane
+// (r, g): row r, columns 32 kc + 8 g .. +7), splits and transforms them with
+// W in registers and stages its own output rows -- no A image, no cross-wave
+// hand-off, two barriers per step.  Rows are swizzled by (row & 15) so that
+// the 16 rows of a wave's b128 reads land on distinct banks.
+template <>
+struct WCfg<64> {
+    static constexpr int H = 64, SWZ = 15;
+    static constexpr int BM = 64, NW = 4, NT = NW * 64;
+    static constexpr int RPW = BM / NW;                // 16
+    static constexpr int ROWB = H * 4;
+    static constexpr int X_BYTES = BM * ROWB;
+    static constexpr int NSLOT = 3;
+    static constexpr int KX = 32;
+    static constexpr int EXT_BYTES = KX * ROWB;
+    static constexpr int EPW = KX / NW;                // 8
+    static constexpr int XLW = (EPW + 4) / 4 * 4;      // 12
+    static constexpr int RECW = RPW * kWRec + XLW * 4;
+    static constexpr int RLANES = RPW * kWRec / 16;
+    static constexpr int TLANES = RECW / 16;
+    static constexpr int TAB_BYTES = BM * kWRec + NW * XLW * 4;
+    static constexpr int STG_BYTES = RPW * ROWB;       // a wave's output staging
+    // LDS: X[3] | EXT | ZERO (code-addressed) | TAB[2] | STG[NW] | EPI
+    static constexpr int OFF_X = 0;
+    static constexpr int OFF_EXT = NSLOT * X_BYTES;
+    static constexpr int OFF_ZERO = OFF_EXT + EXT_BYTES;
+    static constexpr int CODE_END = OFF_ZERO + ROWB;
+    static constexpr int CSH = 0;
+    static constexpr int OFF_TAB = CODE_END;
+    static constexpr int OFF_STG = OFF_TAB + 2 * TAB_BYTES;
+    static constexpr int OFF_EPI = OFF_STG + NW * STG_BYTES;
+    static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
+    static constexpr int WGPC = 2;
+    static constexpr int RPP = 1024 / ROWB, LPR = 64 / RPP;   // 4 rows of 16 lanes per DMA piece
+    static constexpr int NPX = X_BYTES / 1024 / NW;    // 4
+    static constexpr int NPE = EXT_BYTES / 1024 / NW;  // 2
+    static constexpr int NST = RPW / RPP;              // 4 whole-row stores per wave
+    static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
+    static_assert(EPW == NPE * RPP && EPW + 1 <= XLW, "ext rows per wave");
+    static_assert(CODE_END <= 65536, "u16 codes");
+    static_assert(RECW % 16 == 0 && TLANES <= 64 && TAB_BYTES % 16 == 0 && OFF_STG % 16 == 0, "records DMA");
 };
 
 // ------------------------------------------------------------------ schedule
@@ -307,6 +359,29 @@ __device__ __forceinline__ int asw(int R) {
 
 __device__ __attribute__((aligned(16))) float g_win_zero_row[256];
 
+// diagnostic timeline (mignn_diag_win_trace): s_memtime stamps of waves 0
+// and 4 of workgroups 0..7, steps 0..63 -> trace[((b * 64 + s) * 2 + w/4) * 16 + point]
+#ifdef MIGNN_DIAG
+__device__ unsigned long long* g_win_trace = nullptr;
+#endif
+struct WTrace {
+    unsigned long long* tr;   // null: tracing off (the product build)
+    uint32_t lo, hi;
+    int lane;
+    __device__ __forceinline__ void stamp(int pt) {
+        if (tr == nullptr) return;
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        lo = lane == pt ? static_cast<uint32_t>(t) : lo;
+        hi = lane == pt ? static_cast<uint32_t>(t >> 32) : hi;
+    }
+    __device__ __forceinline__ void flush(int wave, int64_t s) {
+        if (tr == nullptr || blockIdx.x >= 8 || s < 0 || s >= 64 || (wave != 0 && wave != 4)) return;
+        if (lane < 8)
+            tr[((blockIdx.x * 64 + s) * 2 + (wave >> 2)) * 16 + lane] =
+                (static_cast<unsigned long long>(hi) << 32) | lo;
+    }
+};
+
 // ------------------------------------------------------------------ plan
 // One 64-thread block per tile, a thread per row.  Entry classes at the
 // tile's step: the current tile (slot s % 3), the workgroup's previous tile
@@ -346,7 +421,7 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
         };
         auto xcode = [&](int slot, int64_t off) -> uint32_t {
             const uint32_t o = static_cast<uint32_t>(off);
-            return ((C::OFF_X + slot * C::X_BYTES + o * C::ROWB) | ((o & 7u) << 4)) >> C::CSH;
+            return ((C::OFF_X + slot * C::X_BYTES + o * C::ROWB) | ((o & C::SWZ) << 4)) >> C::CSH;
         };
         for (int i = lr; i < C::NW * C::XLW; i += 64) xl[i] = 0u;   // unused: row 0, never read
         const int64_t r = t0 + lr;
@@ -407,7 +482,7 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
                     slot = 7;
                 } else {
                     if (k < C::KX) {
-                        cd = ((C::OFF_EXT + k * C::ROWB) | ((static_cast<uint32_t>(k) & 7u) << 4)) >> C::CSH;
+                        cd = ((C::OFF_EXT + k * C::ROWB) | ((static_cast<uint32_t>(k) & C::SWZ) << 4)) >> C::CSH;
                         xl[(k / C::EPW) * C::XLW + k % C::EPW] = static_cast<uint32_t>(c);
                     } else {
                         cd = zcode;
@@ -423,14 +498,14 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
                     }
             }
         }
-        // summary of the row's wave (8 rows): max phase-A count | any CSR-path row
+        // summary of the row's wave (RPW rows): max phase-A count | any CSR-path row
         uint32_t md = far ? 0u : static_cast<uint32_t>(nA), af = far ? 1u : 0u;
 #pragma unroll
-        for (int d = 1; d < 8; d <<= 1) {
-            md = max(md, static_cast<uint32_t>(__shfl_xor(static_cast<int>(md), d, 8)));
-            af |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(af), d, 8));
+        for (int d = 1; d < C::RPW; d <<= 1) {
+            md = max(md, static_cast<uint32_t>(__shfl_xor(static_cast<int>(md), d, C::RPW)));
+            af |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(af), d, C::RPW));
         }
-        if ((lr & 7) == 0) xl[(lr >> 3) * C::XLW + C::EPW] = md | (af << 8);
+        if ((lr % C::RPW) == 0) xl[(lr / C::RPW) * C::XLW + C::EPW] = md | (af << 8);
         __syncthreads();
         unsigned char* const base = tabs + t * C::TAB_BYTES;
         uint4* dst = reinterpret_cast<uint4*>(base + lr * kWRec);
@@ -457,7 +532,7 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
 // row, 4 no MFMAs.  EPIF: the epilogue flags at compile time (15, 11; -1: from
 // `flags`).
 template <int H, int MODE = 0, int EPIF = -1>
-__global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel(
+__global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void gcn_win_kernel(
     const unsigned char* __restrict__ plan, const int32_t* __restrict__ row_ptr,
     const int32_t* __restrict__ col, const float* __restrict__ ew, const float* __restrict__ x,
     int64_t ldx, int64_t rb, int64_t re, const float* __restrict__ W,
@@ -494,6 +569,11 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
     const int p = (static_cast<int>(blockIdx.x) & 7) * per_xcd + (static_cast<int>(blockIdx.x) >> 3);
     auto tile_of = [&](int64_t s) -> int64_t { return win_tile(S, p, s); };
     if (tile_of(0) < 0) return;                   // no work (uniform): no DMA issued
+#ifdef MIGNN_DIAG
+    WTrace wtr{(blockIdx.x < 8 && (wave == 0 || wave == 4)) ? g_win_trace : nullptr, 0u, 0u, lane};
+#else
+    WTrace wtr{nullptr, 0u, 0u, lane};
+#endif
 
     const int gq = lane >> 4, iq = lane & 15;
     const int hb = (iq >= 4 && iq < 12) ? 1 : 0;
@@ -511,8 +591,9 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
         const int pos = lane % C::LPR;
         xoff[pp] = static_cast<uint32_t>(lr) * ldxb + 16u * static_cast<uint32_t>(pos ^ (lr & 7));
     }
-    const uint32_t toff = lane < 24 ? static_cast<uint32_t>(wave * 8 * kWRec + 16 * lane)
-                                    : static_cast<uint32_t>(C::BM * kWRec + wave * (C::XLW * 4) + 16 * (lane - 24));
+    const uint32_t toff = lane < C::RLANES
+                              ? static_cast<uint32_t>(wave * C::RPW * kWRec + 16 * lane)
+                              : static_cast<uint32_t>(C::BM * kWRec + wave * (C::XLW * 4) + 16 * (lane - C::RLANES));
     // records of tile t (or tile 0: a dummy of the same op count) -> TAB slot q
     auto dma_tab = [&](int64_t t, int q) {
         if (lane < C::TLANES)
@@ -539,7 +620,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
     };
     // ext rows of the step whose records sit in TAB slot q (dummy: the zero row)
     auto ext_src = [&](int q, int i, bool real) -> const unsigned char* {
-        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + 8 * kWRec;
+        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::RPW * kWRec;
         int l = lane;
         asm volatile("" : "+v"(l));
         const int kk = i * C::RPP + l / C::LPR;
@@ -556,7 +637,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
 
     // ------------------------------------------------------------ prologue
     for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
-    const int rr = lane & 15, gg = lane >> 4;
+    const int rr0 = lane & 15, gg0 = lane >> 4;
     constexpr int WN = H / 16, WM = C::NW / WN, IBW = (C::BM / 16) / WM;
     static_assert(WN * WM == C::NW && IBW * WM * 16 == C::BM, "window transform grid");
     const int wn = wave % WN, wm = wave / WN;
@@ -568,7 +649,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
         uint32_t m = 0;
 #pragma unroll
         for (int kc = 0; kc < C::KC; ++kc) {
-            const float* pw = W + static_cast<int64_t>(n0 + rr) * H + 32 * kc + 8 * gg;
+            const float* pw = W + static_cast<int64_t>(n0 + rr0) * H + 32 * kc + 8 * gg0;
             const float4 a = ld4(pw), b = ld4(pw + 4);
             float* w8 = wv[kc];
             w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
@@ -631,6 +712,12 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
             cur = tile_of(s);
         }
         if (cur < 0 && prv < 0) break;            // (uniform)
+        const int rr = rr0, gg = gg0;
+        const int iql = iq;
+        // (the REXP row recomputed from an opaque lane: hoisted out of the
+        // step loop it is a register too many at H = 64)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
         const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1
         const int xn2 = xp;                       // slot of tile s + 2 (= (s-1) % 3)
         const int tq = static_cast<int>(s & 1);   // TAB slot of step s
@@ -643,10 +730,13 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
         // (B0) this step's ext rows landed (and, older, the own rows of tile
         //      s + 1 and this step's records); younger: the records of step
         //      s + 1, the own rows of tile s + 2, the last step's stores
+        wtr.flush(wave, s - 1);
+        wtr.stamp(0);
         if (s == 0) wbar<wvm(0) & kWLgkm0>();
         else if (s == 1) wbar<wvm(1 + C::NPX) & kWLgkm0>();
         else wbar<wvm(1 + C::NPX + C::NST) & kWLgkm0>();
 
+        wtr.stamp(1);
         // ---- (P1) phase A of tile s
         f32x4 accn[C::NQ][C::CH];
         uint32_t ncn[C::NQ];
@@ -661,7 +751,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
         if (cur >= 0) {
             const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
             const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-                *reinterpret_cast<const int*>(RW + 8 * kWRec + 4 * C::EPW)));
+                *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
             const int maxa = static_cast<int>(summ & 0xffu);
             const bool far = ((summ >> 8) & 1u) != 0u;
             if (!far) {
@@ -683,7 +773,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
                                      : u == 6 ? w47[qd].z : w47[qd].w;
                     return __uint_as_float(d);
                 };
-                // slots in batches (H = 128: 0..2, 3..5, 6): loads of a batch first
+                // slots in batches of 2: loads of a batch first
                 auto batch = [&](auto U0, auto NB) {
                     constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
                     f32x4 vv[C::NQ][nb][C::CH];
@@ -707,16 +797,11 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
                                 for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(w, vv[qd][uu][j][r], accn[qd][j][r]);
                         }
                 };
-                if constexpr (H == 128) {
-                    if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
-                    if (maxa > 3) batch(std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
-                    if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
-                } else {   // (batches of 2: the 128-VGPR budget of 4 waves per SIMD)
-                    if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
-                    if (maxa > 2) batch(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
-                    if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
-                    if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
-                }
+                // (batches of 2: the 128-VGPR budget of 4 waves per SIMD)
+                if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+                if (maxa > 2) batch(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
+                if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
+                if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
 #pragma unroll
                 for (int qd = 0; qd < C::NQ; ++qd) {
                     ncn[qd] = codeof(qd, 7);
@@ -728,7 +813,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
                 // sum (no phase B)
 #pragma unroll
                 for (int qd = 0; qd < C::NQ; ++qd) {
-                    const int lrow = 8 * wave + 4 * qd + gq;
+                    const int lrow = C::RPW * wave + 4 * qd + gq;
                     if (lrow < nloc) {
                         const int64_t row = t0 + lrow;
                         const int eb = row_ptr[row], ee = row_ptr[row + 1];
@@ -773,6 +858,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
             }
         }
 
+        wtr.stamp(2);
         // ---- (P1) phase B of tile s - 1, its split and residual seeds
         constexpr int NSEED = AGG ? 1 : IBW;
         f32x4 seed[NSEED];
@@ -798,7 +884,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
                     m = wrow_max(m);
                     const int pe = wsplit_exp(m);
                     const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
-                    const int lrow = 8 * wave + 4 * qd + gq;
+                    const int lrow = C::RPW * wave + 4 * qd + gq;
                     const int sw = asw<H>(lrow);
 #pragma unroll
                     for (int j = 0; j < C::CH; ++j) {
@@ -815,12 +901,10 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
                         *reinterpret_cast<f16x4w*>(&AH[ao]) = hv;
                         *reinterpret_cast<f16x4w*>(&AL[ao]) = lv;
                     }
-                    if (iq == 0) {
+                    if (iql == 0) {
                         // (the row index recomputed from an opaque lane: hoisted
                         // out of the step loop it is a register too many at H = 64)
-                        int lo = lane;
-                        asm volatile("" : "+v"(lo));
-                        REXP[8 * wave + 4 * qd + (lo >> 4)] = pe;
+                        REXP[C::RPW * wave + 4 * qd + (ln >> 4)] = pe;
                     }
                 }
                 // residual + bias of my output block (tile s-1's rows of my
@@ -840,7 +924,9 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
         }
         // (B2) A image complete; every read of slot (s-1) % 3, the ext area
         // and this step's records done
+        wtr.stamp(3);
         wbar<kWLgkm0>();
+        wtr.stamp(4);
         // the records of step s + 1 landed (younger: the own rows of tile s + 1
         // and the last step's stores)
         if (s == 0) wwait<wvm(0)>();
@@ -870,7 +956,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
                     for (int j = 0; j < C::CH; ++j) {
                         // (a partial tile is the last of its workgroup: fewer stores
                         // there change no later wait)
-                        const int lrow = 8 * wave + 4 * qd + gq;
+                        const int lrow = C::RPW * wave + 4 * qd + gq;
                         if (lrow < nlocp)
                             __builtin_nontemporal_store(accp[qd][j], reinterpret_cast<f32x4*>(out + (tp0 + lrow) * ldo + 4 * (c0 + 16 * j)));
                     }
@@ -912,6 +998,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
 #pragma unroll
                     for (int t = NTT; t < NPC; ++t) dma_piece(t);
                 }
+                wtr.stamp(5);
                 // (B3) every wave done with the A image: stage there
                 wbar<kWLgkm0>();
                 {
@@ -934,22 +1021,24 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
                     }
                 }
                 // (B4) staged: my 8 rows out, whole rows
+                wtr.stamp(6);
                 wbar<kWLgkm0>();
                 {
                     const int ch = lane % C::LPRW;
                     f32x4 v[C::NST];
 #pragma unroll
                     for (int i = 0; i < C::NST; ++i) {
-                        const int lr = 8 * wave + i * C::RPI + lane / C::LPRW;
+                        const int lr = C::RPW * wave + i * C::RPI + lane / C::LPRW;
                         v[i] = *reinterpret_cast<const f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4));
                     }
 #pragma unroll
                     for (int i = 0; i < C::NST; ++i) {
-                        const int lr = 8 * wave + i * C::RPI + lane / C::LPRW;
+                        const int lr = C::RPW * wave + i * C::RPI + lane / C::LPRW;
                         if (lr < nlocp)
                             __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
                     }
                 }
+                wtr.stamp(7);
             }
         } else {
 #pragma unroll
@@ -968,14 +1057,451 @@ __global__ __launch_bounds__(WCfg<H>::NT, 2 * WCfg<H>::WGPC) void gcn_win_kernel
     wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
 }
 
+// max over the 4 lanes of a row of the B layout (l, l ^ 16, l ^ 32, l ^ 48)
+__device__ __forceinline__ uint32_t wrow4_max(uint32_t m) {
+    const auto r16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+    m = max(static_cast<uint32_t>(r16[0]), static_cast<uint32_t>(r16[1]));
+    const auto r32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+    return max(static_cast<uint32_t>(r32[0]), static_cast<uint32_t>(r32[1]));
+}
+
+// ------------------------------------------------------------ layer, H = 64
+// Step s of a wave (rows 16 w .. 16 w + 15 of the tiles; lane (r, g) holds
+// fp32 chunks 8 kc + 2 g + {0, 1} of row r, kc = 0, 1):
+//   B0  ext rows of step s landed (older: own rows of tile s, the records)
+//   phase A of tile s (in-window / ext entries from LDS, the +z entry held
+//   back); the residual of tile s - 1 (slot (s-1) % 3) into registers
+//   B1  slot (s-1) % 3, the ext area and this step's records free
+//       -> DMA ext rows of step s + 1, records of step s + 2, own rows of
+//       tile s + 2
+//   phase B of tile s - 1 (its +z term, from tile s), split (row exponent
+//   over the row's 4 lanes), 24 MFMAs 16x16x32 f16 (W split in registers),
+//   epilogue, the wave's 16 rows staged in its own LDS region, whole-row
+//   stores.
+// MODE: 32 aggregate only; diag 1 ext rows from the zero row, 4 no MFMAs.
+template <int MODE = 0, int EPIF = -1>
+__global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
+    const unsigned char* __restrict__ plan, const int32_t* __restrict__ row_ptr,
+    const int32_t* __restrict__ col, const float* __restrict__ ew, const float* __restrict__ x,
+    int64_t ldx, int64_t rb, int64_t re, const float* __restrict__ W,
+    const float* __restrict__ bias, const float* __restrict__ scale,
+    const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+    using C = WCfg<64>;
+    constexpr int H = 64;
+    constexpr bool AGG = (MODE & 32) != 0;
+    if constexpr (EPIF >= 0) flags = EPIF;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
+    float* const EPI = reinterpret_cast<float*>(lds + C::OFF_EPI);
+
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const WinHdr* const hdr = reinterpret_cast<const WinHdr*>(plan);
+    {
+        const bool ok = hdr->magic == kWMagic && hdr->G == static_cast<int>(gridDim.x) &&
+                        hdr->h == H && hdr->rb == rb && hdr->re == re;
+        if (!ok) {
+            if (tid == 0)
+                __hip_atomic_fetch_or(&g_win_errors, static_cast<unsigned>(MIGNN_DEVERR_PLAN),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    const WinSched S = win_sched(hdr);
+    const unsigned char* const tabs = plan + kWHdr;
+    const int per_xcd = static_cast<int>(gridDim.x) >> 3;
+    const int p = (static_cast<int>(blockIdx.x) & 7) * per_xcd + (static_cast<int>(blockIdx.x) >> 3);
+    auto tile_of = [&](int64_t s) -> int64_t { return win_tile(S, p, s); };
+    if (tile_of(0) < 0) return;                   // no work (uniform): no DMA issued
+#ifdef MIGNN_DIAG
+    WTrace wtr{(blockIdx.x < 8 && wave == 0) ? g_win_trace : nullptr, 0u, 0u, lane};
+#else
+    WTrace wtr{nullptr, 0u, 0u, lane};
+#endif
+
+    const int r = lane & 15, g = lane >> 4;
+    const int lrow = C::RPW * wave + r;           // the lane's row in a tile (lrow & 15 == r)
+    // the lane's 16-B chunks of a row: k = 2 kc + hf -> chunk 8 kc + 2 g + hf
+    uint32_t coff[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) coff[k] = static_cast<uint32_t>((8 * (k >> 1) + 2 * g + (k & 1)) << 4);
+
+    // own-row DMA: SGPR base, per-lane offsets fixed for the launch
+    const uint32_t ldxb = static_cast<uint32_t>(ldx) * 4u;
+    uint32_t xoff[C::NPX];
+#pragma unroll
+    for (int pp = 0; pp < C::NPX; ++pp) {
+        const int pc = pp * C::NW + wave;
+        const int lr = pc * C::RPP + lane / C::LPR;
+        const int pos = lane % C::LPR;
+        xoff[pp] = static_cast<uint32_t>(lr) * ldxb + 16u * static_cast<uint32_t>(pos ^ (lr & C::SWZ));
+    }
+    const uint32_t toff = lane < C::RLANES
+                              ? static_cast<uint32_t>(wave * C::RPW * kWRec + 16 * lane)
+                              : static_cast<uint32_t>(C::BM * kWRec + wave * (C::XLW * 4) + 16 * (lane - C::RLANES));
+    auto dma_tab = [&](int64_t t, int q) {
+        if (lane < C::TLANES)
+            wdma_s(tabs + (t >= 0 ? t : 0) * C::TAB_BYTES, toff,
+                   wlds(lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW));
+    };
+    auto dma_own = [&](int64_t t, int q, int pp) {
+        const int64_t tt = t >= 0 ? t : 0;
+        const int64_t t0 = rb + tt * C::BM;
+        const int pc = pp * C::NW + wave;
+        unsigned char* const X = lds + C::OFF_X + q * C::X_BYTES;
+        if (t0 + C::BM <= re) {
+            wdma_s(x + t0 * ldx, xoff[pp], wlds(X + pc * 1024));
+        } else {
+            int l = lane;
+            asm volatile("" : "+v"(l));
+            const int lr = pc * C::RPP + l / C::LPR;
+            const int pos = l % C::LPR;
+            int64_t row = t0 + lr;
+            if (row >= re) row = re - 1;
+            wdma(x + row * ldx + 4 * (pos ^ (lr & C::SWZ)), wlds(X + pc * 1024));
+        }
+    };
+    auto ext_src = [&](int q, int i, bool real) -> const unsigned char* {
+        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::RPW * kWRec;
+        int l = lane;
+        asm volatile("" : "+v"(l));
+        const int kk = i * C::RPP + l / C::LPR;
+        const int k = wave * C::EPW + kk;
+        const int pos = l % C::LPR;
+        const uint32_t c = *reinterpret_cast<const uint32_t*>(tab + 4 * kk);
+        return ((MODE & 1) || !real) ? reinterpret_cast<const unsigned char*>(g_win_zero_row + 4 * pos)
+                                     : reinterpret_cast<const unsigned char*>(x) + static_cast<uint64_t>(c) * ldxb +
+                                           16u * static_cast<uint32_t>(pos ^ (k & C::SWZ));
+    };
+    auto ext_dma = [&](int i, const unsigned char* src) {
+        wdma(src, wlds(lds + C::OFF_EXT + (wave * C::EPW + i * C::RPP) * C::ROWB));
+    };
+
+    // ------------------------------------------------------------ prologue
+    for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
+    // W split in registers: A fragment (cb, kc) of lane l = W[16 cb + (l & 15)]
+    // [32 kc + 8 (l >> 4) .. +7], one exponent per 16-column block
+    f16x8w wh[4][2], wl[4][2];
+    int qw[4] = {0, 0, 0, 0};
+    if constexpr (!AGG) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            float wv[2][8];
+            uint32_t m = 0;
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) {
+                const float* pw = W + static_cast<int64_t>(16 * cb + r) * H + 32 * kc + 8 * g;
+                const float4 a = ld4(pw), b = ld4(pw + 4);
+                float* w8 = wv[kc];
+                w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
+                w8[4] = b.x; w8[5] = b.y; w8[6] = b.z; w8[7] = b.w;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(w8[j])));
+            }
+            qw[cb] = wsplit_exp(wwave_max(m));
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float sv = ldexpf(wv[kc][j], qw[cb]);
+                    const _Float16 hh = static_cast<_Float16>(sv);
+                    wh[cb][kc][j] = hh;
+                    wl[cb][kc][j] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                }
+        }
+        if (tid < H) {
+            EPI[tid] = (flags & MIGNN_EPI_BIAS) ? bias[tid] : 0.f;
+            EPI[H + tid] = (flags & MIGNN_EPI_AFFINE) ? scale[tid] : 1.f;
+            EPI[2 * H + tid] = (flags & MIGNN_EPI_AFFINE) ? shift[tid] : 0.f;
+        }
+    }
+    const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
+    unsigned char* const STG = lds + C::OFF_STG + wave * C::STG_BYTES;
+
+    dma_tab(tile_of(0), 0);
+#pragma unroll
+    for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(0), 0, pp);
+    dma_tab(tile_of(1), 1);
+#pragma unroll
+    for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(1), 1, pp);
+    wbar<wvm(0) & kWLgkm0>();
+    {
+        const unsigned char* es[C::NPE];
+#pragma unroll
+        for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(0, i, true);
+#pragma unroll
+        for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
+    }
+
+    f32x4 accp[4];
+    uint32_t ncode = C::OFF_ZERO;
+    float nwt = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) accp[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int64_t cur = tile_of(0), prv = -1;
+    int xs = 0;
+    for (int64_t s = 0;; ++s) {
+        if (s > 0) {
+            prv = cur;
+            cur = tile_of(s);
+        }
+        if (cur < 0 && prv < 0) break;            // (uniform)
+        const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1 (and of tile s + 2)
+        const int tq = static_cast<int>(s & 1);
+        const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
+        const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
+        const int64_t tp0 = rb + (prv >= 0 ? prv : 0) * C::BM;
+        const int64_t nlocp = prv >= 0 ? (re - tp0 < C::BM ? re - tp0 : C::BM) : 0;
+        const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
+        const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
+        wtr.flush(wave, s - 1);
+        wtr.stamp(0);
+        // (B0) younger than this step's ext rows: the records of step s + 1,
+        // the own rows of tile s + 1, the last step's stores
+        if (s == 0) wbar<wvm(0) & kWLgkm0>();
+        else if (s == 1) wbar<wvm(1 + C::NPX) & kWLgkm0>();
+        else wbar<wvm(1 + C::NPX + C::NST) & kWLgkm0>();
+        wtr.stamp(1);
+
+        // ---- phase A of tile s
+        f32x4 accn[4];
+        uint32_t ncn = C::OFF_ZERO;
+        float nwn = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) accn[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (cur >= 0) {
+            const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
+            const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+                *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
+            const int maxa = static_cast<int>(summ & 0xffu);
+            const bool far = ((summ >> 8) & 1u) != 0u;
+            if (!far) {
+                const unsigned char* rec = RW + r * kWRec;
+                const uint4 cds = *reinterpret_cast<const uint4*>(rec);
+                const uint4 w03 = *reinterpret_cast<const uint4*>(rec + 16);
+                const uint4 w47 = *reinterpret_cast<const uint4*>(rec + 32);
+                auto codeof = [&](int u) -> uint32_t {
+                    const uint32_t d = u < 2 ? cds.x : u < 4 ? cds.y : u < 6 ? cds.z : cds.w;
+                    return (u & 1) ? (d >> 16) : (d & 0xffffu);
+                };
+                auto wof = [&](int u) -> float {
+                    const uint32_t d = u == 0 ? w03.x : u == 1 ? w03.y : u == 2 ? w03.z : u == 3 ? w03.w
+                                     : u == 4 ? w47.x : u == 5 ? w47.y : u == 6 ? w47.z : w47.w;
+                    return __uint_as_float(d);
+                };
+                auto batch = [&](auto U0, auto NB) {
+                    constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
+                    f32x4 vv[nb][4];
+#pragma unroll
+                    for (int uu = 0; uu < nb; ++uu) {
+                        const uint32_t cd = codeof(u0 + uu);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) vv[uu][k] = *reinterpret_cast<const f32x4*>(lds + (cd ^ coff[k]));
+                    }
+#pragma unroll
+                    for (int uu = 0; uu < nb; ++uu) {
+                        const float w = wof(u0 + uu);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) accn[k][t] = fmaf(w, vv[uu][k][t], accn[k][t]);
+                    }
+                };
+                if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+                if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
+                if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
+                ncn = codeof(7);
+                nwn = wof(7);
+            } else if (lrow < nloc) {
+                // CSR path: the full sum in CSR order, the current tile from
+                // LDS, every other row from x (L2)
+                const int64_t row = t0 + lrow;
+                const int eb = row_ptr[row], ee = row_ptr[row + 1];
+                for (int e = eb; e < ee; e += 4) {
+                    int cj[4];
+                    float wj[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool v = e + u < ee;
+                        cj[u] = v ? col[e + u] : -1;
+                        wj[u] = v ? ew[e + u] : 0.f;
+                    }
+                    f32x4 vv[4][4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int64_t off = static_cast<int64_t>(cj[u]) - t0;
+                        if (cj[u] < 0) {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) vv[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        } else if (off >= 0 && off < nloc) {
+                            const uint32_t o = static_cast<uint32_t>(off);
+                            const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB) | ((o & C::SWZ) << 4);
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) vv[u][k] = *reinterpret_cast<const f32x4*>(lds + (a ^ coff[k]));
+                        } else {
+                            const float* rp = x + static_cast<int64_t>(cj[u]) * ldx;
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) vv[u][k] = *reinterpret_cast<const f32x4*>(rp + (coff[k] >> 2));
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) accn[k][t] = fmaf(wj[u], vv[u][k][t], accn[k][t]);
+                }
+            }
+        }
+        // residual + bias of tile s - 1 (row lrow, columns 16 cb + 4 g ..), read
+        // before slot (s-1) % 3 is refilled
+        f32x4 seed[4];
+        if constexpr (!AGG) {
+            if (prv >= 0) {
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) {
+                    const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[16 * cb + 4 * g]);
+                    f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (has_res)
+                        rv = *reinterpret_cast<const f32x4*>(XP + lrow * C::ROWB + (((4 * cb + g) ^ r) << 4));
+                    seed[cb] = rv + bo;
+                }
+            }
+        }
+        wtr.stamp(2);
+        // (B1) slot (s-1) % 3, the ext area and this step's records free
+        wbar<kWLgkm0>();
+        wtr.stamp(3);
+        if (s == 0) wwait<wvm(0)>();
+        else if (s == 1) wwait<wvm(C::NPX)>();
+        else wwait<wvm(C::NPX + C::NST)>();
+        {
+            const int64_t tn1 = tile_of(s + 1), tn2 = tile_of(s + 2);
+            const unsigned char* es[C::NPE];
+#pragma unroll
+            for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
+#pragma unroll
+            for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
+            dma_tab(tn2, tq);
+#pragma unroll
+            for (int pp = 0; pp < C::NPX; ++pp) dma_own(tn2, xp, pp);
+        }
+
+        if (prv >= 0) {
+            // ---- phase B of tile s - 1 (its +z term, from tile s in slot s % 3)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(lds + (ncode ^ coff[k]));
+#pragma unroll
+                for (int t = 0; t < 4; ++t) accp[k][t] = fmaf(nwt, v[t], accp[k][t]);
+            }
+            if constexpr (AGG) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *reinterpret_cast<f32x4*>(STG + r * C::ROWB + (((coff[k] >> 4) ^ r) << 4)) = accp[k];
+            } else {
+                // split: one power-of-two scale per row (its 4 lanes)
+                uint32_t m = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) m = max(m, __float_as_uint(fabsf(accp[k][t])));
+                const int pe = wsplit_exp(wrow4_max(m));
+                const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
+                f16x8w bh[2], bl[2];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const float sv = accp[k][t] * sc;
+                        const _Float16 hh = static_cast<_Float16>(sv);
+                        bh[k >> 1][4 * (k & 1) + t] = hh;
+                        bl[k >> 1][4 * (k & 1) + t] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                    }
+                f32x4 acc[4];
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (!(MODE & 4)) {
+#pragma unroll
+                    for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+                        for (int cb = 0; cb < 4; ++cb) {
+                            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], bh[kc], acc[cb], 0, 0, 0);
+                            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], bl[kc], acc[cb], 0, 0, 0);
+                            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cb][kc], bh[kc], acc[cb], 0, 0, 0);
+                        }
+                }
+                wtr.stamp(4);
+                // epilogue (gnn_model.py:184-191: conv + bias, + x, BN, ReLU):
+                // lane (r, g) holds row r, columns 16 cb + 4 g + t
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) {
+                    const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + 16 * cb + 4 * g]);
+                    const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + 16 * cb + 4 * g]);
+                    f32x4 o;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        float v = ldexpf(acc[cb][t], -(pe + qw[cb])) + seed[cb][t];
+                        if (flags & MIGNN_EPI_AFFINE) v = v * so[t] + ho[t];
+                        if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
+                        o[t] = v;
+                    }
+                    *reinterpret_cast<f32x4*>(STG + r * C::ROWB + (((4 * cb + g) ^ r) << 4)) = o;
+                }
+            }
+            // the wave's 16 rows out, whole rows (its own staging region: LDS
+            // ops of one wave complete in order, no barrier)
+            {
+                const int ch = lane & 15;
+                f32x4 v[C::NST];
+#pragma unroll
+                for (int i = 0; i < C::NST; ++i) {
+                    const int sr = i * C::RPP + (lane >> 4);
+                    v[i] = *reinterpret_cast<const f32x4*>(STG + sr * C::ROWB + ((ch ^ sr) << 4));
+                }
+#pragma unroll
+                for (int i = 0; i < C::NST; ++i) {
+                    const int lr = C::RPW * wave + i * C::RPP + (lane >> 4);
+                    // (a partial tile is the last of its workgroup: fewer
+                    // stores there change no later wait)
+                    if (lr < nlocp)
+                        __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
+                }
+            }
+            wtr.stamp(5);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) accp[k] = accn[k];
+        ncode = ncn;
+        nwt = nwn;
+        xs = xs == 2 ? 0 : xs + 1;
+    }
+    wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
+}
+
+#ifdef MIGNN_DIAG
+int win_trace_set(void* buf) {
+    MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_win_trace), &buf, sizeof(buf)));
+    return MIGNN_OK;
+}
+#endif
+
 template <int H, int MODE, int EPIF>
 void launch_win_k(int G, hipStream_t st, const void* plan, const int32_t* row_ptr,
                   const int32_t* col, const float* ew, const float* x, int64_t ldx, int64_t rb,
                   int64_t re, const float* w, const float* bias, const float* scale,
                   const float* shift, int flags, float* out, int64_t ldo) {
-    hipLaunchKernelGGL((gcn_win_kernel<H, MODE, EPIF>), dim3(G), dim3(WCfg<H>::NT), 0, st,
-                       static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb, re, w,
-                       bias, scale, shift, flags, out, ldo);
+    if constexpr (H == 64)
+        hipLaunchKernelGGL((gcn_win64_kernel<MODE, EPIF>), dim3(G), dim3(WCfg<64>::NT), 0, st,
+                           static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb, re, w,
+                           bias, scale, shift, flags, out, ldo);
+    else
+        hipLaunchKernelGGL((gcn_win_kernel<H, MODE, EPIF>), dim3(G), dim3(WCfg<H>::NT), 0, st,
+                           static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb, re, w,
+                           bias, scale, shift, flags, out, ldo);
 }
 
 template <int H, int MODE>
@@ -1096,6 +1622,8 @@ extern "C" int mignn_gcn_aggregate_win(const void* plan, const int32_t* row_ptr,
 }
 
 #ifdef MIGNN_DIAG
+extern "C" int mignn_diag_win_trace(void* buf) { return win_trace_set(buf); }
+
 extern "C" int mignn_diag_win(int mode, const void* plan, const int32_t* row_ptr,
                               const int32_t* col, const float* ew, const float* x, int64_t ldx,
                               int64_t rb, int64_t re, int h, const float* w, const float* bias,

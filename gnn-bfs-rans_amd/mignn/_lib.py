@@ -186,6 +186,7 @@ DIAG_SIGNATURES = {
     "mignn_diag_ring_trace": (c_int, [_P]),
     "mignn_diag_ring": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_diag_win_trace": (c_int, [_P]),
     "mignn_diag_win": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_diag_set_gat_fused": (c_int, [c_int]),

@@ -54,10 +54,11 @@ from ._lib import (CSR_ONE_SELF_LOOP, CSR_TRANSPOSE, CSR_VERBATIM, EPI_AFFINE, E
 HEADS = 4  # gnn_model.py:67, :79
 # the split-fp16 GCN layer kernel of FlowGNN.gcn_kernel = "auto", per hidden
 # width: the fastest measured on the bench mesh
-# (H = 64: the ring kernel, two workgroups per CU, 1.39-1.41 ms vs the tile
-# kernel's 1.57-1.59 per 10M-row layer; H = 128: the producer / consumer
-# kernel -- the ring kernel ties it per layer but needs a 0.49 ms plan per graph)
-GCN_KERNEL_AUTO = {64: "win", 128: "win"}
+# (H = 64: the window kernel in its wave-independent form, 1.31 ms vs the ring
+# kernel's 1.37 per 10M-row layer on the same box; H = 128: the producer /
+# consumer kernel -- the window and ring kernels tie it per layer (3.07, 3.04
+# vs 3.04 ms) but need a 0.46-0.49 ms plan per graph)
+GCN_KERNEL_AUTO = {64: "win", 128: "pc"}
 
 
 # ---------------------------------------------------------------------------
@@ -958,8 +959,14 @@ class FlowGNN(nn.Module):
             pos.stride(0), self.input_dim, rb, re, _lib.ptr(self._layer0_coef()), self.hidden_dim,
             _lib.ptr(out), out.stride(0), _stream(pos)), "mignn_gcn_layer0_coords")
 
-    def _gcn_kernel(self, H: int) -> str:
-        return self.gcn_kernel if self.gcn_kernel != "auto" else GCN_KERNEL_AUTO.get(H, "pc")
+    def _gcn_kernel(self, H: int, csr: Optional["Csr"] = None) -> str:
+        """The GCN layer kernel at width H; with `csr`: the kernel for that
+        graph -- under "auto" the window kernel only on a CSR in the column
+        order (a shard's block-ordered range takes the ring kernel instead)."""
+        k = self.gcn_kernel if self.gcn_kernel != "auto" else GCN_KERNEL_AUTO.get(H, "pc")
+        if k == "win" and self.gcn_kernel == "auto" and csr is not None and csr.order_info is None:
+            k = "ring"
+        return k
 
     def _column_order(self) -> bool:
         """The locality order of this model's graphs: the column order when
@@ -975,7 +982,7 @@ class FlowGNN(nn.Module):
         H = self.hidden_dim
         if self.layer_type != "GCN" or H not in (64, 128) or self.precision != "f16x3":
             return
-        kern = self._gcn_kernel(H)
+        kern = self._gcn_kernel(H, csr)
         if kern == "win":
             csr.win_plan(H, row_begin, row_end)
         elif kern == "ring":
@@ -1064,7 +1071,7 @@ class FlowGNN(nn.Module):
             return
         if self.layer_type == "GCN":
             w, b = layer.lin.weight, layer.bias
-            kern = self._gcn_kernel(H)
+            kern = self._gcn_kernel(H, csr)
             if H in (64, 128) and self.precision == "f16x3" and kern == "win":
                 # the hot kernel: window walk over the CSR's window plan
                 plan = csr.win_plan(H, rb, re)

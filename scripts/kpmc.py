@@ -32,6 +32,16 @@ b = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
 Y = torch.empty_like(X)
+if "win" in kinds or "winagg" in kinds:
+    # the window kernel on the column-order CSR of the same mesh
+    _pos, _ei = grid_graph(250, 200, 200, device=dev)
+    _, inv_c, info_c = locality_order(_pos, _ei, cols=True)
+    csr_c = build_csr(_ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv_c)
+    del _pos, _ei
+    nbw = L.mignn_gcn_win_plan_bytes(0, n, H)
+    wplan = torch.empty(nbw, dtype=torch.uint8, device=dev)
+    _lib.check(L.mignn_gcn_win_plan(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), 0, n, H, P(info_c),
+                                    P(wplan), nbw, None, st), "wp")
 if "ring" in kinds:
     nbr = L.mignn_gcn_ring_plan_bytes(0, n, H)
     rplan = torch.empty(nbr, dtype=torch.uint8, device=dev)
@@ -79,6 +89,12 @@ for _ in range(reps):
     if "pc" in kinds:
         _lib.check(L.mignn_gcn_layer_f16x3(P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H, 0, n, H,
                                            P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "pc")
+    if "win" in kinds:
+        _lib.check(L.mignn_gcn_layer_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X), H,
+                                         0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "win")
+    if "winagg" in kinds:
+        _lib.check(L.mignn_gcn_aggregate_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
+                                             H, 0, n, H, P(Y), H, st), "winagg")
     if "ring" in kinds:
         _lib.check(L.mignn_gcn_layer_ring(P(rplan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
                                           0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "ring")

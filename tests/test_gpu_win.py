@@ -134,8 +134,10 @@ def test_gcn_layer_win(H, case):
         assert err < 1e-5, (rb, re, err, stats.tolist())
         assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
         assert torch.isnan(out[:, H:]).all()
+        # (the kernels round the residual / bias in a different order: a few
+        # ulps of the output apart, both within the fp64 bound above)
         d = (out[rb:re, :H] - old[rb:re, :H]).abs().max().item()
-        assert d < 2e-6, (rb, re, d)
+        assert d < 2e-6 * max(1.0, old[rb:re, :H].abs().max().item()), (rb, re, d)
         # the aggregate alone by the window kernel
         agg = torch.full((n, ld), float("nan"), device=DEV)
         _lib.check(L.mignn_gcn_aggregate_win(
