@@ -255,6 +255,26 @@ __device__ inline WinSched win_sched(const WinHdr* h) {
     return S;
 }
 
+// the tile of step s = q L + m (0 <= m < L): the kernels walk (q, m) one
+// step at a time -- win_tile's 64-bit s / L, s % L are long scalar sequences
+struct WinCursor {
+    int s, q, m;
+    __device__ __forceinline__ void next(int L) {
+        ++s;
+        if (++m == L) {
+            m = 0;
+            ++q;
+        }
+    }
+};
+__device__ __forceinline__ int64_t win_tile_c(const WinSched& S, int p, const WinCursor& c) {
+    if (c.q < S.R1) return static_cast<int64_t>(c.q * S.G + p) * S.L + c.m;
+    const int j = c.s - S.R1 * S.L;
+    if (j >= S.chunk) return -1;
+    const int64_t t = S.t2 + static_cast<int64_t>(p) * S.chunk + j;
+    return t < S.ntiles ? t : -1;
+}
+
 int win_grid(int64_t ntiles, int wgpc) {
     static int cus_cache[64] = {0};
     int dev = 0;
@@ -704,14 +724,15 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         for (int j = 0; j < C::CH; ++j) accp[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-    int64_t cur = tile_of(0), prv = -1;
+    // schedule: cur / nx1 = tiles of steps s / s + 1, the cursor at s + 2
+    int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
+    WinCursor c2{0, 0, 0};
+    c2.next(S.L);
+    c2.next(S.L);
     int xs = 0;                                   // X slot of step s (s % 3)
-    for (int64_t s = 0;; ++s) {
-        if (s > 0) {
-            prv = cur;
-            cur = tile_of(s);
-        }
+    for (int s = 0;; ++s) {
         if (cur < 0 && prv < 0) break;            // (uniform)
+        const int64_t nx2 = win_tile_c(S, p, c2);
         const int rr = rr0, gg = gg0;
         const int iql = iq;
         // (the REXP row recomputed from an opaque lane: hoisted out of the
@@ -932,7 +953,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         if (s == 0) wwait<wvm(0)>();
         else if (s == 1) wwait<wvm(C::NPX)>();
         else wwait<wvm(C::NPX + C::NST)>();
-        const int64_t tn1 = tile_of(s + 1), tn2 = tile_of(s + 2);
+        const int64_t tn1 = nx1, tn2 = nx2;
         const unsigned char* es[C::NPE];
 #pragma unroll
         for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
@@ -1053,6 +1074,10 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             for (int j = 0; j < C::CH; ++j) accp[qd][j] = accn[qd][j];
         }
         xs = xs == 2 ? 0 : xs + 1;
+        prv = cur;
+        cur = nx1;
+        nx1 = nx2;
+        c2.next(S.L);
     }
     wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
 }
@@ -1122,7 +1147,15 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
 #endif
 
     const int r = lane & 15, g = lane >> 4;
-    const int lrow = C::RPW * wave + r;           // the lane's row in a tile (lrow & 15 == r)
+    // the wave row of lane (r, g): lanes r in {0-3, 12-15} take the even rows,
+    // r in {4-11} the odd ones.  A ds_read_b128 lane group holds the first
+    // set at chunk 2 g and the second at 2 g + 2 (or the reverse), so with
+    // the (row & 15) swizzle the in-plane neighbours (row offsets 0, +-1,
+    // +-8) land on 16 distinct 16-B bank slots -- with rows in lane order
+    // the +-1 neighbours are 2-way conflicts (SQ_LDS_BANK_CONFLICT 26 % of
+    // the LDS cycles).  The MFMA is indifferent: B-operand column r is row rw.
+    const int rw = (2 * r + ((r >= 4 && r < 12) ? 9 : 0)) & 15;
+    const int lrow = C::RPW * wave + rw;          // the lane's row in a tile (lrow & 15 == rw)
     // the lane's 16-B chunks of a row: k = 2 kc + hf -> chunk 8 kc + 2 g + hf
     uint32_t coff[4];
 #pragma unroll
@@ -1241,14 +1274,15 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) accp[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    int64_t cur = tile_of(0), prv = -1;
+    // schedule: cur / nx1 = tiles of steps s / s + 1, the cursor at s + 2
+    int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
+    WinCursor c2{0, 0, 0};
+    c2.next(S.L);
+    c2.next(S.L);
     int xs = 0;
-    for (int64_t s = 0;; ++s) {
-        if (s > 0) {
-            prv = cur;
-            cur = tile_of(s);
-        }
+    for (int s = 0;; ++s) {
         if (cur < 0 && prv < 0) break;            // (uniform)
+        const int64_t nx2 = win_tile_c(S, p, c2);
         const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1 (and of tile s + 2)
         const int tq = static_cast<int>(s & 1);
         const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
@@ -1259,12 +1293,23 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
         wtr.flush(wave, s - 1);
         wtr.stamp(0);
-        // (B0) younger than this step's ext rows: the records of step s + 1,
-        // the own rows of tile s + 1, the last step's stores
+        // (B0) this step's ext rows and the records of step s + 1 landed;
+        // younger: the own rows of tile s + 1, the last step's stores
         if (s == 0) wbar<wvm(0) & kWLgkm0>();
-        else if (s == 1) wbar<wvm(1 + C::NPX) & kWLgkm0>();
-        else wbar<wvm(1 + C::NPX + C::NST) & kWLgkm0>();
+        else if (s == 1) wbar<wvm(C::NPX) & kWLgkm0>();
+        else wbar<wvm(C::NPX + C::NST) & kWLgkm0>();
         wtr.stamp(1);
+        // reads with no dependence on this step's arithmetic, first: the ext
+        // list of step s + 1 (its DMA goes out after B1) and tile s - 1's +z
+        // rows (phase B, slot s % 3)
+        const unsigned char* es[C::NPE];
+#pragma unroll
+        for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, nx1 >= 0);
+        f32x4 pbv[4];
+        if (prv >= 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) pbv[k] = *reinterpret_cast<const f32x4*>(lds + (ncode ^ coff[k]));
+        }
 
         // ---- phase A of tile s
         f32x4 accn[4];
@@ -1279,7 +1324,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
             const int maxa = static_cast<int>(summ & 0xffu);
             const bool far = ((summ >> 8) & 1u) != 0u;
             if (!far) {
-                const unsigned char* rec = RW + r * kWRec;
+                const unsigned char* rec = RW + rw * kWRec;
                 const uint4 cds = *reinterpret_cast<const uint4*>(rec);
                 const uint4 w03 = *reinterpret_cast<const uint4*>(rec + 16);
                 const uint4 w47 = *reinterpret_cast<const uint4*>(rec + 32);
@@ -1310,28 +1355,30 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
                             for (int t = 0; t < 4; ++t) accn[k][t] = fmaf(w, vv[uu][k][t], accn[k][t]);
                     }
                 };
-                if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+                // (batches of 2 slots: the 256-VGPR budget)
+                if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+                if (maxa > 2) batch(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
                 if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
                 if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
                 ncn = codeof(7);
                 nwn = wof(7);
             } else if (lrow < nloc) {
                 // CSR path: the full sum in CSR order, the current tile from
-                // LDS, every other row from x (L2)
+                // LDS, every other row from x (L2); 2 entries at a time (registers)
                 const int64_t row = t0 + lrow;
                 const int eb = row_ptr[row], ee = row_ptr[row + 1];
-                for (int e = eb; e < ee; e += 4) {
-                    int cj[4];
-                    float wj[4];
+                for (int e = eb; e < ee; e += 2) {
+                    int cj[2];
+                    float wj[2];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
+                    for (int u = 0; u < 2; ++u) {
                         const bool v = e + u < ee;
                         cj[u] = v ? col[e + u] : -1;
                         wj[u] = v ? ew[e + u] : 0.f;
                     }
-                    f32x4 vv[4][4];
+                    f32x4 vv[2][4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
+                    for (int u = 0; u < 2; ++u) {
                         const int64_t off = static_cast<int64_t>(cj[u]) - t0;
                         if (cj[u] < 0) {
 #pragma unroll
@@ -1348,7 +1395,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
                         }
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
+                    for (int u = 0; u < 2; ++u)
 #pragma unroll
                         for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -1366,7 +1413,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
                     const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[16 * cb + 4 * g]);
                     f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
                     if (has_res)
-                        rv = *reinterpret_cast<const f32x4*>(XP + lrow * C::ROWB + (((4 * cb + g) ^ r) << 4));
+                        rv = *reinterpret_cast<const f32x4*>(XP + lrow * C::ROWB + (((4 * cb + g) ^ rw) << 4));
                     seed[cb] = rv + bo;
                 }
             }
@@ -1375,14 +1422,9 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         // (B1) slot (s-1) % 3, the ext area and this step's records free
         wbar<kWLgkm0>();
         wtr.stamp(3);
-        if (s == 0) wwait<wvm(0)>();
-        else if (s == 1) wwait<wvm(C::NPX)>();
-        else wwait<wvm(C::NPX + C::NST)>();
+        wtr.stamp(6);
         {
-            const int64_t tn1 = tile_of(s + 1), tn2 = tile_of(s + 2);
-            const unsigned char* es[C::NPE];
-#pragma unroll
-            for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
+            const int64_t tn2 = nx2;
 #pragma unroll
             for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
             dma_tab(tn2, tq);
@@ -1391,17 +1433,15 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         }
 
         if (prv >= 0) {
-            // ---- phase B of tile s - 1 (its +z term, from tile s in slot s % 3)
+            // ---- phase B of tile s - 1 (its +z term, read after B0)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const f32x4 v = *reinterpret_cast<const f32x4*>(lds + (ncode ^ coff[k]));
+            for (int k = 0; k < 4; ++k)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) accp[k][t] = fmaf(nwt, v[t], accp[k][t]);
-            }
+                for (int t = 0; t < 4; ++t) accp[k][t] = fmaf(nwt, pbv[k][t], accp[k][t]);
             if constexpr (AGG) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    *reinterpret_cast<f32x4*>(STG + r * C::ROWB + (((coff[k] >> 4) ^ r) << 4)) = accp[k];
+                    *reinterpret_cast<f32x4*>(STG + rw * C::ROWB + (((coff[k] >> 4) ^ rw) << 4)) = accp[k];
             } else {
                 // split: one power-of-two scale per row (its 4 lanes)
                 uint32_t m = 0;
@@ -1436,7 +1476,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
                 }
                 wtr.stamp(4);
                 // epilogue (gnn_model.py:184-191: conv + bias, + x, BN, ReLU):
-                // lane (r, g) holds row r, columns 16 cb + 4 g + t
+                // lane (r, g) holds row rw, columns 16 cb + 4 g + t
 #pragma unroll
                 for (int cb = 0; cb < 4; ++cb) {
                     const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + 16 * cb + 4 * g]);
@@ -1449,7 +1489,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
                         if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
                         o[t] = v;
                     }
-                    *reinterpret_cast<f32x4*>(STG + r * C::ROWB + (((4 * cb + g) ^ r) << 4)) = o;
+                    *reinterpret_cast<f32x4*>(STG + rw * C::ROWB + (((4 * cb + g) ^ rw) << 4)) = o;
                 }
             }
             // the wave's 16 rows out, whole rows (its own staging region: LDS
@@ -1478,6 +1518,10 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         ncode = ncn;
         nwt = nwn;
         xs = xs == 2 ? 0 : xs + 1;
+        prv = cur;
+        cur = nx1;
+        nx1 = nx2;
+        c2.next(S.L);
     }
     wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
 }

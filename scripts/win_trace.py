@@ -56,7 +56,7 @@ _lib.check(L.mignn_diag_win_trace(None), "trace")
 t = tr.view(8, 64, 2, 16).cpu()
 res = {"H": H, "mode": mode}
 if H == 64:
-    pts = [0, 1, 2, 3, 4, 5] if not mode & 32 else [0, 1, 2, 3, 5]
+    pts = [0, 1, 2, 3, 6, 4, 5] if not mode & 32 else [0, 1, 2, 3, 6, 5]
 else:
     pts = [0, 1, 2, 3, 4, 5, 6, 7] if not mode & 32 else [0, 1, 2, 3, 4]
 for wv in ((0,) if H == 64 else (0, 1)):
