@@ -328,9 +328,12 @@ def main():
                      "seeded random weights",
             "nodes_per_gpu": N_local, "edges_per_gpu": E_local, "global_batch": 1,
             "parallelism": "single" if world == 1 else f"node_range{world}+rccl_halo",
-            "internal_node_order": ("locality (4x4x4-cell blocks in panels of 4x4 block "
-                                    "columns, mignn_locality_order; part of the per-step graph "
-                                    "setup)" if world == 1 else
+            "internal_node_order": (("locality: 8x8-cell columns, z inside "
+                                     "(mignn_locality_order_cols, the window GCN kernel's order)"
+                                     if model._column_order() else
+                                     "locality: 4x4x4-cell blocks in panels of 4x4 block columns "
+                                     "(mignn_locality_order)") + "; part of the per-step graph setup"
+                                    if world == 1 else
                                     "locality order inside each rank's range, interior rows "
                                     "first; the partition layout (ghost / send lists, the "
                                     "order) and the rank-local CSR are rebuilt inside every "
@@ -480,7 +483,6 @@ def aggregate_roofline(model, x, steps):
 
 
 GCN_KERNEL_NAMES = {"pc": "gcn_f16x3_kernel<%d> (mignn_gcn_layer_f16x3)",
-                    "tile": "gcn_tile_kernel<%d> (mignn_gcn_layer_planned)",
                     "ring": "gcn_ring_kernel<%d> (mignn_gcn_layer_ring)",
                     "win": "gcn_win_kernel<%d> / gcn_win64_kernel at H = 64 (mignn_gcn_layer_win)"}
 

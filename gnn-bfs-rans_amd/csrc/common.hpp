@@ -186,6 +186,8 @@ int head256(const float* x, int64_t ldx, int64_t n, const void* img, int out_dim
             int64_t ldo, const int32_t* out_rows, void* stream);
 // the window GCN kernel's device error word, OR-ed into *out (gcn_win.hip)
 int win_device_errors(unsigned int* out, int clear);
+// the ring GCN kernel's device error word, OR-ed into *out (gcn_ring.hip)
+int ring_device_errors(unsigned int* out, int clear);
 int tile_linear(const float* a, int64_t lda, int64_t m, int k, const float* w, int n,
                 const float* bias, const float* residual, int64_t ldr, const float* scale,
                 const float* shift, int flags, float* c, int64_t ldc, hipStream_t st,

@@ -939,7 +939,8 @@ extern "C" int mignn_device_errors(unsigned int* out, int clear) {
         MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_device_errors), &zero, sizeof(unsigned int), 0,
                                     hipMemcpyHostToDevice));
     }
-    return win_device_errors(out, clear);
+    const int rc = win_device_errors(out, clear);
+    return rc ? rc : ring_device_errors(out, clear);
 }
 
 extern "C" int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const float* ew,

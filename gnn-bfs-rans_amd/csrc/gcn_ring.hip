@@ -121,6 +121,17 @@ __host__ __device__ inline int ring_parity(int64_t tile, int64_t ntiles, int G) 
     return static_cast<int>(((tile % chunk) / per_xcd) & 1);
 }
 
+// plan header (the first kRHdr bytes): the grid the schedule was built for,
+// checked by the kernel (a mismatch: MIGNN_DEVERR_PLAN, no rows written)
+constexpr int kRHdr = 256;
+constexpr uint32_t kRMagic = 0x474E4952u;
+struct RingHdr {
+    uint32_t magic;
+    int32_t G, h, pad;
+    int64_t rb, re;
+};
+__device__ unsigned int g_ring_errors = 0u;
+
 int ring_grid(int64_t ntiles, int wgpc) {
     static int cus_cache[64] = {0};
     int dev = 0;
@@ -259,6 +270,16 @@ __global__ __launch_bounds__(RCfg<H>::BM) void ring_plan_kernel(const int32_t* _
     using C = RCfg<H>;
     const int lr = threadIdx.x;
     __shared__ uint32_t xl[C::NW * C::XLW];
+    if (blockIdx.x == 0 && lr == 0) {
+        RingHdr* const hd = reinterpret_cast<RingHdr*>(plan);
+        hd->magic = kRMagic;
+        hd->G = G;
+        hd->h = H;
+        hd->pad = 0;
+        hd->rb = rb;
+        hd->re = re;
+    }
+    plan += kRHdr;
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int64_t t0 = rb + t * C::BM;
         const int64_t r = t0 + lr;
@@ -381,6 +402,18 @@ __global__ __launch_bounds__(RCfg<H>::NT, RCfg<H>::WGPC) void gcn_ring_kernel(
     asm volatile("" : "+v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
+    {
+        const RingHdr* const hd = reinterpret_cast<const RingHdr*>(plan);
+        const bool ok = hd->magic == kRMagic && hd->G == static_cast<int>(gridDim.x) && hd->h == H &&
+                        hd->rb == row_begin && hd->re == row_end;
+        if (!ok) {
+            if (tid == 0)
+                __hip_atomic_fetch_or(&g_ring_errors, static_cast<unsigned>(MIGNN_DEVERR_PLAN),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    plan += kRHdr;
     const int64_t nrows = row_end - row_begin;
     const int64_t ntiles = (nrows + C::BM - 1) / C::BM;
     const int G = gridDim.x;
@@ -968,6 +1001,20 @@ int launch_ring(int h, const void* plan, const int32_t* row_ptr, const int32_t* 
 }
 
 }  // namespace
+
+int ring_device_errors(unsigned int* out, int clear) {
+    unsigned int v = 0u;
+    MIGNN_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ring_errors), sizeof(unsigned int), 0,
+                                  hipMemcpyDeviceToHost));
+    *out |= v;
+    if (clear) {
+        const unsigned int zero = 0u;
+        MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ring_errors), &zero, sizeof(unsigned int), 0,
+                                    hipMemcpyHostToDevice));
+    }
+    return MIGNN_OK;
+}
+
 }  // namespace mignn
 
 using namespace mignn;
@@ -976,7 +1023,7 @@ extern "C" size_t mignn_gcn_ring_plan_bytes(int64_t row_begin, int64_t row_end, 
     if (row_end <= row_begin || (h != 64 && h != 128)) return 0;
     const int bm = h == 128 ? RCfg<128>::BM : RCfg<64>::BM;
     const int64_t ntiles = (row_end - row_begin + bm - 1) / bm;
-    return static_cast<size_t>(ntiles) * (h == 128 ? RCfg<128>::TAB_BYTES : RCfg<64>::TAB_BYTES);
+    return kRHdr + static_cast<size_t>(ntiles) * (h == 128 ? RCfg<128>::TAB_BYTES : RCfg<64>::TAB_BYTES);
 }
 
 extern "C" int mignn_gcn_ring_plan(const int32_t* row_ptr, const int32_t* col, const float* ew,

@@ -65,12 +65,6 @@ SIGNATURES = {
                                 c_int, _P, c_int64, _P]),
     "mignn_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                       _P, _P, c_int, _P, c_int64, _P]),
-    "mignn_gcn_plan_bytes": (c_size_t, [c_int64, c_int64]),
-    "mignn_gcn_plan": (c_int, [_P, _P, _P, c_int64, c_int64, c_int, _P, c_size_t, _P]),
-    "mignn_gcn_layer_planned": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
-                                        _P, _P, _P, c_int, _P, c_int64, _P]),
-    "mignn_gcn_aggregate_planned": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int,
-                                            _P, c_int64, _P]),
     "mignn_gcn_ring_plan_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "mignn_gcn_ring_plan": (c_int, [_P, _P, _P, c_int64, c_int64, c_int, _P, c_size_t, _P, _P]),
     "mignn_gcn_layer_ring": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
@@ -181,8 +175,6 @@ DIAG_SIGNATURES = {
                                      _P, c_int, _P, c_int64, _P]),
     "mignn_diag_gcn_layer_f16x3": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                            _P, _P, _P, c_int, _P, c_int64, _P]),
-    "mignn_diag_gcn_tile": (c_int, [c_int, c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64,
-                                    c_int, _P, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_diag_ring_trace": (c_int, [_P]),
     "mignn_diag_ring": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                 _P, _P, _P, c_int, _P, c_int64, _P]),

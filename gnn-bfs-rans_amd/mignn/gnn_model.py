@@ -53,12 +53,14 @@ from ._lib import (CSR_ONE_SELF_LOOP, CSR_TRANSPOSE, CSR_VERBATIM, EPI_AFFINE, E
 
 HEADS = 4  # gnn_model.py:67, :79
 # the split-fp16 GCN layer kernel of FlowGNN.gcn_kernel = "auto", per hidden
-# width: the fastest measured on the bench mesh
-# (H = 64: the window kernel in its wave-independent form, 1.31 ms vs the ring
-# kernel's 1.37 per 10M-row layer on the same box; H = 128: the producer /
-# consumer kernel -- the window and ring kernels tie it per layer (3.07, 3.04
-# vs 3.04 ms) but need a 0.46-0.49 ms plan per graph)
-GCN_KERNEL_AUTO = {64: "win", 128: "pc"}
+# width: the fastest measured on the bench mesh: the
+# window kernel at both widths (10M-row layer, same box: H = 64 1.24 ms vs the
+# ring kernel's 1.32; H = 128 2.84 ms vs the producer / consumer kernel's 3.02
+# -- 0.7 ms per 4-layer forward against its 0.46 ms plan per graph).  A
+# block-ordered CSR (a shard's range) takes the ring kernel at H = 64 and the
+# producer / consumer kernel at H = 128 (FlowGNN._gcn_kernel).
+GCN_KERNEL_AUTO = {64: "win", 128: "win"}
+GCN_BLOCK_ORDER = {64: "ring", 128: "pc"}
 
 
 # ---------------------------------------------------------------------------
@@ -180,22 +182,6 @@ class Csr:
                                             _lib.ptr(self.ew), row_begin, row_end, h,
                                             _lib.ptr(info), _lib.ptr(plan), nb, None,
                                             _lib.stream(self.col.device)), "mignn_gcn_win_plan")
-            self.plans[key] = plan
-        return plan
-
-    def gcn_plan(self, h: int, row_begin: int, row_end: int) -> torch.Tensor:
-        """The tile plan of rows [row_begin, row_end) for hidden width h
-        (mignn_gcn_plan), built on first use and kept with the CSR (it copies
-        the ew weights: rebuilt after compute_gcn_weights)."""
-        key = ("tile", h, row_begin, row_end)
-        plan = self.plans.get(key)
-        if plan is None:
-            L = _lib.lib()
-            nb = L.mignn_gcn_plan_bytes(row_begin, row_end)
-            plan = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.col.device)
-            _lib.check(L.mignn_gcn_plan(_lib.ptr(self.row_ptr), _lib.ptr(self.col),
-                                        _lib.ptr(self.ew), row_begin, row_end, h, _lib.ptr(plan),
-                                        nb, _lib.stream(self.col.device)), "mignn_gcn_plan")
             self.plans[key] = plan
         return plan
 
@@ -467,15 +453,15 @@ class FlowGNN(nn.Module):
         # internal locality order of the nodes: "auto" (meshes of >= 2^20
         # nodes with 3-D cell-centre features), "1" always, "0" never
         self.reorder = os.environ.get("MIGNN_REORDER", "auto")
-        # split-fp16 GCN layer kernel at H in {64, 128}: "tile" (the tile-plan
-        # kernel, csrc/gcn_tile.hip), "ring" (the persistent ring kernel,
-        # csrc/gcn_ring.hip), "pc" (the producer / consumer kernel,
-        # csrc/gcn_f16x3.hip) or "auto" (the fastest measured per H,
-        # GCN_KERNEL_AUTO); read once here, not per forward
+        # split-fp16 GCN layer kernel at H in {64, 128}: "win" (the window
+        # kernel over the column order, csrc/gcn_win.hip), "ring" (the
+        # persistent ring kernel, csrc/gcn_ring.hip), "pc" (the producer /
+        # consumer kernel, csrc/gcn_f16x3.hip: any node order, no plan) or
+        # "auto" (GCN_KERNEL_AUTO per H); read once here, not per forward
         self.gcn_kernel = os.environ.get("MIGNN_GCN_KERNEL", "auto")
-        if self.gcn_kernel not in ("tile", "ring", "pc", "win", "auto"):
+        if self.gcn_kernel not in ("ring", "pc", "win", "auto"):
             raise ValueError(
-                f"MIGNN_GCN_KERNEL must be auto, tile, ring or pc, got {self.gcn_kernel!r}")
+                f"MIGNN_GCN_KERNEL must be auto, win, ring or pc, got {self.gcn_kernel!r}")
         # kernel-route switches (A/B studies; the defaults are the measured
         # fastest routes), read once at construction -- plain attributes after
         # that, never environment lookups inside forward:
@@ -962,10 +948,10 @@ class FlowGNN(nn.Module):
     def _gcn_kernel(self, H: int, csr: Optional["Csr"] = None) -> str:
         """The GCN layer kernel at width H; with `csr`: the kernel for that
         graph -- under "auto" the window kernel only on a CSR in the column
-        order (a shard's block-ordered range takes the ring kernel instead)."""
+        order (a shard's block-ordered range takes GCN_BLOCK_ORDER instead)."""
         k = self.gcn_kernel if self.gcn_kernel != "auto" else GCN_KERNEL_AUTO.get(H, "pc")
         if k == "win" and self.gcn_kernel == "auto" and csr is not None and csr.order_info is None:
-            k = "ring"
+            k = GCN_BLOCK_ORDER.get(H, "pc")
         return k
 
     def _column_order(self) -> bool:
@@ -987,8 +973,6 @@ class FlowGNN(nn.Module):
             csr.win_plan(H, row_begin, row_end)
         elif kern == "ring":
             csr.ring_plan(H, row_begin, row_end)
-        elif kern == "tile":
-            csr.gcn_plan(H, row_begin, row_end)
 
     def _use_reorder(self, x) -> bool:
         if self.reorder not in ("auto", "0", "1"):
@@ -1086,13 +1070,6 @@ class FlowGNN(nn.Module):
                     P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
                     P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),
                     "mignn_gcn_layer_ring")
-            elif H in (64, 128) and self.precision == "f16x3" and kern == "tile":
-                # the hot kernel: split-fp16 GCN layer over the CSR's tile plan
-                plan = csr.gcn_plan(H, rb, re)
-                _lib.check(L.mignn_gcn_layer_planned(
-                    P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,
-                    P(w), P(b), P(scale), P(shift), epi, P(out), out.stride(0), st),
-                    "mignn_gcn_layer_planned")
             elif H in (64, 128):
                 fn = L.mignn_gcn_layer_f16x3 if self.precision == "f16x3" else L.mignn_gcn_layer
                 _lib.check(fn(P(csr.row_ptr), P(csr.col), P(csr.ew), P(x), x.stride(0), rb, re, H,

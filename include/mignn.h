@@ -293,33 +293,14 @@ int mignn_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t* col, const floa
                           const float* w, const float* bias, const float* scale,
                           const float* shift, int flags, float* out, int64_t ldo, void* stream);
 
-/* Tile plan of a GCN CSR (the graph-side companion of the layer below; no
- * reference counterpart -- PyG's GCNConv re-reads edge_index every call):
- * for rows [row_begin, row_end) in 64-row tiles, a 64-B record per row with
- * up to 7 CSR entries (in-tile ones as LDS image offsets for hidden width h,
- * out-of-tile ones as columns, each with its ew weight), the counts and a
- * per-16-row summary.  Build once per graph, row range and h (its size:
- * mignn_gcn_plan_bytes); device memory, 16-B aligned. */
-size_t mignn_gcn_plan_bytes(int64_t row_begin, int64_t row_end);
-int mignn_gcn_plan(const int32_t* row_ptr, const int32_t* col, const float* ew,
-                   int64_t row_begin, int64_t row_end, int h, void* plan, size_t plan_bytes,
-                   void* stream);
-/* mignn_gcn_layer_f16x3 over the plan (GCNConv + residual + BN + ReLU,
- * gnn_model.py:63, :166, :184-191): same arguments, flags and arithmetic
- * (split-fp16 transform, fp32 aggregation; a row's out-of-tile entries, then
- * its in-tile entries, each in CSR order), a different kernel structure
- * (independent 4-wave workgroups, csrc/gcn_tile.hip).  row_ptr / col / ew
- * are read only for rows with more than 7 entries.  h in {64, 128}. */
-int mignn_gcn_layer_planned(const void* plan, const int32_t* row_ptr, const int32_t* col,
-                            const float* ew, const float* x, int64_t ldx, int64_t row_begin,
-                            int64_t row_end, int h, const float* w, const float* bias,
-                            const float* scale, const float* shift, int flags, float* out,
-                            int64_t ldo, void* stream);
-/* Ring form of the same layer (csrc/gcn_ring.hip): own rows, plan records and
+/* Ring form of mignn_gcn_layer_f16x3 (csrc/gcn_ring.hip), the route of a
+ * block-ordered H = 64 row range (a shard's): own rows, plan records and
  * out-of-tile rows all arrive by LDS-DMA issued up to 1.5 tiles ahead, one
  * 8-wave workgroup per CU.  Its plan (mignn_gcn_ring_plan, size
  * mignn_gcn_ring_plan_bytes) also fixes the kernel's schedule (the LDS ring
- * slot of every tile): build it on the device that runs the layer.  Sum
+ * slot of every tile): build it on the device that runs the layer; its
+ * header (grid, h, row range) is checked at launch (MIGNN_DEVERR_PLAN on a
+ * mismatch, no rows written).  Sum
  * order: a row's CSR entries in CSR order.  stats (nullable, device uint64[4]):
  * tiles over the out-of-tile capacity, entries gathered synchronously, rows
  * with more than 7 entries, max out-of-tile entries of a tile. */
@@ -366,13 +347,6 @@ int mignn_gcn_layer_win(const void* plan, const int32_t* row_ptr, const int32_t*
 int mignn_gcn_aggregate_win(const void* plan, const int32_t* row_ptr, const int32_t* col,
                             const float* ew, const float* x, int64_t ldx, int64_t row_begin,
                             int64_t row_end, int h, float* out, int64_t ldo, void* stream);
-/* The GCN aggregation alone over the plan: out_i = sum_e ew_e x_{col e}
- * (= mignn_gcn_aggregate's D^-1/2 (A + I) D^-1/2 x with ew from dinv), fp32;
- * the SURVEY 8(d) "aggregate kernel alone" of the north-star target. */
-int mignn_gcn_aggregate_planned(const void* plan, const int32_t* row_ptr, const int32_t* col,
-                                const float* ew, const float* x, int64_t ldx, int64_t row_begin,
-                                int64_t row_end, int h, float* out, int64_t ldo, void* stream);
-
 /* Fused output head (output_proj, gnn_model.py:90-100, :195) in split-fp16
  * MFMA arithmetic, h in {64, 128, 256}, out_dim 1..8:
  *   out = W4 relu(W3 relu(W2 relu(W1 x + b1) + b2) + b3) + b4

@@ -16,7 +16,7 @@ from mignn.synthetic import grid_graph  # noqa: E402
 dev = torch.device("cuda", 0)
 H = int(os.environ.get("KP_H", "128"))
 reps = int(os.environ.get("KP_REPS", "2"))
-kinds = os.environ.get("KP_KINDS", "pc,ring,planned,agg").split(",")
+kinds = os.environ.get("KP_KINDS", "pc,ring,win,winagg").split(",")
 pos, ei = grid_graph(250, 200, 200, device=dev)
 n = pos.shape[0]
 _, inv = locality_order(pos, ei)
@@ -47,10 +47,6 @@ if "ring" in kinds:
     rplan = torch.empty(nbr, dtype=torch.uint8, device=dev)
     _lib.check(L.mignn_gcn_ring_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(rplan), nbr,
                                      None, st), "rp")
-if "planned" in kinds or "agg" in kinds:
-    nb = L.mignn_gcn_plan_bytes(0, n)
-    plan = torch.empty(nb, dtype=torch.uint8, device=dev)
-    _lib.check(L.mignn_gcn_plan(P(csr.row_ptr), P(csr.col), P(csr.ew), 0, n, H, P(plan), nb, st), "p")
 if "gin" in kinds or "tf" in kinds:
     # H = 256 fused layers (KP_H=256): GIN (verbatim CSR) and TransformerConv
     from mignn.gnn_model import f16x3_image, gin_fused_image  # noqa: E402
@@ -98,11 +94,5 @@ for _ in range(reps):
     if "ring" in kinds:
         _lib.check(L.mignn_gcn_layer_ring(P(rplan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
                                           0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "ring")
-    if "planned" in kinds:
-        _lib.check(L.mignn_gcn_layer_planned(P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
-                                             0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "tile")
-    if "agg" in kinds:
-        _lib.check(L.mignn_gcn_aggregate_planned(P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X),
-                                                 H, 0, n, H, P(Y), H, st), "agg")
 torch.cuda.synchronize()
 print("ok")
