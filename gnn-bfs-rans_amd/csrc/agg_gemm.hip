@@ -39,6 +39,7 @@
 #include "common.hpp"
 
 namespace mignn {
+MIGNN_DMA_OOB_WORD
 namespace {
 
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
@@ -73,6 +74,7 @@ __device__ __forceinline__ uint32_t lds_addr_ag(const unsigned char* p) {
 // LDS-DMA of 16 B per lane (inline asm: the compiler does not count it; the
 // kernel's explicit vmcnt(0) before each chunk barrier covers it)
 __device__ __forceinline__ void glds16_ag(const void* src, uint32_t dst) {
+    MIGNN_DMA_BOUND(dst);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -2311,3 +2313,5 @@ extern "C" int mignn_gat_layer0_coords(const int32_t* row_ptr, const int32_t* co
     }
     return launch_status("tf0_kernel<gat>");
 }
+
+MIGNN_DMA_OOB_EXPORT(mignn_diag_dma_oob_agg)

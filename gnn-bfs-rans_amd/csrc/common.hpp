@@ -184,6 +184,40 @@ int head256_prep(const float* w1, const float* b1, const float* w2, const float*
                  void* img, void* stream);
 int head256(const float* x, int64_t ldx, int64_t n, const void* img, int out_dim, float* out,
             int64_t ldo, const int32_t* out_rows, void* stream);
+// LDS-DMA destination bound (diag builds only): a global_load_lds_dwordx4
+// writes 1 KiB from the wave-uniform LDS address `dst`; it must end inside
+// the issuing kernel's static LDS allocation (__builtin_amdgcn_groupstaticsize:
+// the block's own bytes -- past them lie a co-resident block's).  A violation
+// sets the translation unit's word g_dma_oob (mignn_diag_dma_oob_<unit>).
+#ifdef MIGNN_DIAG
+#define MIGNN_DMA_OOB_WORD namespace { __device__ unsigned int g_dma_oob = 0u; }
+#define MIGNN_DMA_BOUND(dst)                                                               \
+    do {                                                                                   \
+        if (static_cast<uint32_t>(dst) + 1024u >                                           \
+                static_cast<uint32_t>(__builtin_amdgcn_groupstaticsize()) &&               \
+            (threadIdx.x & 63u) == 0u)                                                     \
+            __hip_atomic_fetch_or(&g_dma_oob, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    } while (0)
+#define MIGNN_DMA_OOB_EXPORT(name)                                                          \
+    extern "C" int name(unsigned int* out, int clear) {                                     \
+        unsigned int v = 0u;                                                                \
+        MIGNN_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(mignn::g_dma_oob), sizeof(v), 0,       \
+                                      hipMemcpyDeviceToHost));                              \
+        *out = v;                                                                           \
+        if (clear) {                                                                        \
+            const unsigned int zero = 0u;                                                   \
+            MIGNN_HIP(hipMemcpyToSymbol(HIP_SYMBOL(mignn::g_dma_oob), &zero, sizeof(zero), 0, \
+                                        hipMemcpyHostToDevice));                            \
+        }                                                                                   \
+        return MIGNN_OK;                                                                    \
+    }
+#else
+#define MIGNN_DMA_OOB_WORD
+#define MIGNN_DMA_BOUND(dst) \
+    do {                     \
+    } while (0)
+#define MIGNN_DMA_OOB_EXPORT(name)
+#endif
 // the window GCN kernel's device error word, OR-ed into *out (gcn_win.hip)
 int win_device_errors(unsigned int* out, int clear);
 // the ring GCN kernel's device error word, OR-ed into *out (gcn_ring.hip)

@@ -58,6 +58,7 @@
 #include "common.hpp"
 
 namespace mignn {
+MIGNN_DMA_OOB_WORD
 namespace {
 
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
@@ -189,6 +190,7 @@ __device__ __forceinline__ uint32_t lds_addr(const unsigned char* p) {
 // counts it nor inserts conservative vmcnt(0) waits before later LDS reads;
 // the issuing wave waits for it itself (block_barrier with a counted vmcnt).
 __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
+    MIGNN_DMA_BOUND(dst);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -991,3 +993,5 @@ extern "C" int mignn_diag_gcn_layer_f16x3(const int32_t* row_ptr, const int32_t*
     return gcn_f16x3_impl(row_ptr, col, ew, x, ldx, rb, re, h, w, bias, scale, shift, flags, out, ldo, stream);
 }
 #endif
+
+MIGNN_DMA_OOB_EXPORT(mignn_diag_dma_oob_pc)

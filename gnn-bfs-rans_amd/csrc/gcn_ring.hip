@@ -41,6 +41,7 @@
 #include "common.hpp"
 
 namespace mignn {
+MIGNN_DMA_OOB_WORD
 namespace {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_r;
@@ -171,6 +172,7 @@ __device__ __forceinline__ uint32_t rlds(const unsigned char* p) {
 }
 
 __device__ __forceinline__ void rdma(const void* src, uint32_t dst) {
+    MIGNN_DMA_BOUND(dst);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -194,6 +196,7 @@ __device__ __forceinline__ uint64_t runi(const void* p) {
 // the same with an SGPR base address and a per-lane 32-bit offset (no
 // per-piece address arithmetic: the offsets are fixed per lane)
 __device__ __forceinline__ void rdma_s(const void* base, uint32_t voff, uint32_t dst) {
+    MIGNN_DMA_BOUND(dst);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -1115,3 +1118,5 @@ extern "C" int mignn_diag_ring(int mode, const void* plan, const int32_t* row_pt
     return MIGNN_ERR_ARG;
 }
 #endif
+
+MIGNN_DMA_OOB_EXPORT(mignn_diag_dma_oob_ring)

@@ -51,12 +51,18 @@
 #include "common.hpp"
 
 namespace mignn {
+MIGNN_DMA_OOB_WORD
 namespace {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_w;
 using f16x8w = __attribute__((ext_vector_type(8))) _Float16;
 using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 
+// A-fragment prefetch depth of the H = 128 transform, in t-steps of 3 MFMAs
+// (10M-row layer: PD 1 2.87 ms, 2 2.72, 3 2.68, 5 2.67)
+#ifndef MIGNN_WIN_PD
+#define MIGNN_WIN_PD 5
+#endif
 constexpr int kWRec = 48;                 // bytes per plan record: 8 u16 codes + 8 f32 weights
 constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the next-tile entry
 constexpr int kWHdr = 256;                // plan header bytes
@@ -317,6 +323,7 @@ __device__ __forceinline__ uint32_t wlds(const unsigned char* p) {
 }
 
 __device__ __forceinline__ void wdma(const void* src, uint32_t dst) {
+    MIGNN_DMA_BOUND(dst);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -337,6 +344,7 @@ __device__ __forceinline__ uint64_t wuni(const void* p) {
 }
 
 __device__ __forceinline__ void wdma_s(const void* base, uint32_t voff, uint32_t dst) {
+    MIGNN_DMA_BOUND(dst);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -1001,7 +1009,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         bl = *reinterpret_cast<const f16x8w*>(&AL[ao]);
                     };
                     __builtin_amdgcn_sched_barrier(0);
-                    constexpr int PD = 1, NF = PD + 1, NTT = C::KC * IBW;
+                    constexpr int PD = MIGNN_WIN_PD, NF = PD + 1, NTT = C::KC * IBW;
                     f16x8w fh[NF], fl[NF];
 #pragma unroll
                     for (int t = 0; t < PD && t < NTT; ++t) frag(t, fh[t], fl[t]);
@@ -1686,3 +1694,5 @@ extern "C" int mignn_diag_win(int mode, const void* plan, const int32_t* row_ptr
     return MIGNN_ERR_ARG;
 }
 #endif
+
+MIGNN_DMA_OOB_EXPORT(mignn_diag_dma_oob_win)

@@ -36,6 +36,7 @@
 #include "common.hpp"
 
 namespace mignn {
+MIGNN_DMA_OOB_WORD
 namespace {
 
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
@@ -75,6 +76,7 @@ __device__ __forceinline__ uint32_t lds_addr_g(const unsigned char* p) {
 }
 
 __device__ __forceinline__ void glds16_g(const void* src, uint32_t dst) {
+    MIGNN_DMA_BOUND(dst);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -519,3 +521,5 @@ extern "C" int mignn_diag_linear_f16x3(const float* a, int64_t lda, int64_t m, i
     return linear_f16x3_impl(a, lda, m, k1, a2, lda2, k2, img, n, bias, residual, ldr, scale, shift, flags, c, ldc, stream);
 }
 #endif
+
+MIGNN_DMA_OOB_EXPORT(mignn_diag_dma_oob_gemm)

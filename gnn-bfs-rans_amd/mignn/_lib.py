@@ -181,6 +181,11 @@ DIAG_SIGNATURES = {
     "mignn_diag_win_trace": (c_int, [_P]),
     "mignn_diag_win": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P,
                                _P, _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_diag_dma_oob_agg": (c_int, [_P, c_int]),
+    "mignn_diag_dma_oob_ring": (c_int, [_P, c_int]),
+    "mignn_diag_dma_oob_win": (c_int, [_P, c_int]),
+    "mignn_diag_dma_oob_pc": (c_int, [_P, c_int]),
+    "mignn_diag_dma_oob_gemm": (c_int, [_P, c_int]),
     "mignn_diag_set_gat_fused": (c_int, [c_int]),
     "mignn_diag_set_fused_flags": (c_int, [c_int]),
     "mignn_diag_linear": (c_int, [_P, c_int64, c_int64, c_int, _P, c_int64, c_int, _P, c_int, _P,

@@ -6,7 +6,8 @@ window and ring kernels; the window plan build; window ablations
 (mignn_diag_win modes: 1 ext rows from the zero row, 4 no MFMAs, 33
 aggregate with ext from the zero row).  HIP events on the launch stream,
 interleaved rounds, median.  Env: WB_H (comma list, 128,64), WB_GRID,
-WB_REPS, WB_MODES (comma list of diag modes), WB_OLD (0: skip pc / ring).
+WB_REPS, WB_MODES (comma list of diag modes), WB_OLD (0: skip pc / ring),
+WB_LIBS (name=path,...: variant builds timed beside the product).
 Prints one JSON object."""
 import json
 import os
@@ -37,6 +38,12 @@ del ei, pos
 nnz = int(csr_c.row_ptr[-1].item())
 L = _lib.diag_lib()
 P = _lib.ptr
+# WB_LIBS: comma list of variant builds of libmignn.so (name=path); each
+# gets its own "win@name" timing at every H
+VARIANTS = {}
+for item in [v for v in os.environ.get("WB_LIBS", "").split(",") if v]:
+    name, path = item.split("=")
+    VARIANTS[name] = _lib._load(path, _lib.SIGNATURES)
 st = _lib.stream()
 reps = int(os.environ.get("WB_REPS", "7"))
 res = {"grid": [nx, ny, nz], "n": n, "nnz": nnz, "order_info": info.tolist(), "by_h": {}}
@@ -88,6 +95,11 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     res.setdefault("win_plan_stats", {})[H] = wstats.tolist()
     res.setdefault("win_header", {})[H] = hdr[:32].view(torch.int32).tolist() + hdr[32:64].view(torch.int64).tolist()
     cases = {"win_plan": mk_wplan, "win": win, "win_aggregate": win_agg}
+    for vname, VL in VARIANTS.items():
+        def fv(VL=VL):
+            _lib.check(VL.mignn_gcn_layer_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
+                                              H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yd), H, st), "wv")
+        cases[f"win@{vname}"] = fv
     for m in [int(v) for v in os.environ.get("WB_MODES", "").split(",") if v]:
         def fw(m=m):
             _lib.check(L.mignn_diag_win(m, P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
