@@ -60,6 +60,12 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 
 // A-fragment prefetch depth of the H = 128 transform, in t-steps of 3 MFMAs
 // (10M-row layer: PD 1 2.87 ms, 2 2.72, 3 2.68, 5 2.67)
+// H = 128 epilogue stored from the accumulators, 16 rows x 64 B per store
+// (1), or staged over the A image for whole-row stores (0: two more block
+// barriers per step; 10M-row layer 2.92 vs 2.87 ms on one box)
+#ifndef MIGNN_WIN_DIRECT
+#define MIGNN_WIN_DIRECT 1
+#endif
 #ifndef MIGNN_WIN_PD
 #define MIGNN_WIN_PD 5
 #endif
@@ -1028,6 +1034,29 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                     for (int t = NTT; t < NPC; ++t) dma_piece(t);
                 }
                 wtr.stamp(5);
+#if MIGNN_WIN_DIRECT
+                {
+                    // epilogue stored straight from the accumulators: lane (rr, gg) of
+                    // block ib holds row 16 ib + rr, columns n0 + 4 gg .. +3
+                    const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 4 * gg]);
+                    const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + n0 + 4 * gg]);
+                    static_assert(IBW == C::NST, "one store per row block keeps the per-step store count");
+#pragma unroll
+                    for (int ib = 0; ib < IBW; ++ib) {
+                        f32x4 o;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float v = ldexpf(accm[ib][r], -(pr[ib] + qw));
+                            if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
+                            if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
+                            o[r] = v;
+                        }
+                        const int lr = (wm * IBW + ib) * 16 + rr;
+                        if (lr < nlocp)
+                            __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + n0 + 4 * gg));
+                    }
+                }
+#else
                 // (B3) every wave done with the A image: stage there
                 wbar<kWLgkm0>();
                 {
@@ -1067,6 +1096,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                             __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
                     }
                 }
+#endif
                 wtr.stamp(7);
             }
         } else {
