@@ -68,6 +68,16 @@ __device__ __forceinline__ float p2_ag(int p) {
 __device__ __forceinline__ float p2neg_ag(int q) {
     return __uint_as_float(static_cast<uint32_t>(__mul24(q, -8388608) + 0x3f800000));
 }
+// Output-column order of the GIN nn.2 image (mignn_gin_fused_prep): image
+// column m = 16 cb + 4 g + i (the accumulator position of lane (r, g), block
+// cb) holds output feature 32 (cb >> 1) + 8 g + 4 (cb & 1) + i -- the
+// features lane (r, g) reads of its own row in the B-operand layout of chunk
+// cb >> 1 during the aggregation, so the residual x_i stays in its registers
+// (one HBM read of the own rows per layer).  A bijection on [0, 256).
+__host__ __device__ __forceinline__ int gin_operm(int m) {
+    const int cb = m >> 4, g = (m >> 2) & 3, i = m & 3;
+    return 32 * (cb >> 1) + 8 * g + 4 * (cb & 1) + i;
+}
 __device__ __forceinline__ uint32_t lds_addr_ag(const unsigned char* p) {
     return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_ag)(p)));
 }
@@ -141,7 +151,12 @@ __device__ __forceinline__ float rowsum4(float v) {
 // (GIN layer 0 from the coordinates: x = input_proj(pos), TB = [W_in | b_in])
 // LG: also the next GAT layer's logits of each finished row, x_out . WLN^T
 // (WLN [8][N] in LDS) -> lgn[row][8] (the row's 4 lanes summed)
-template <int NCB, bool CRES = false, bool LG = false>
+// OPERM (GIN, NCB = 16): the accumulators are in gin_operm's output order --
+// EV is indexed by image column, each value lands at its feature's staging
+// slot, and the residual comes from RES (the lane's own-row values of the
+// aggregation, RES[kc][h] = x_i[32 kc + 8 g + 4 h ..]) or, with CRES, is
+// computed for the feature.
+template <int NCB, bool CRES = false, bool LG = false, bool OPERM = false>
 __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float* EV,
                                                 const f32x4 (&acc)[NCB], int p, int flags,
                                                 const float* __restrict__ x, int64_t ldx,
@@ -150,13 +165,15 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
                                                 const float* TB = nullptr, float c0 = 0.f,
                                                 float c1 = 0.f, float c2 = 0.f,
                                                 const float* WLN = nullptr,
-                                                float* __restrict__ lgn = nullptr) {
+                                                float* __restrict__ lgn = nullptr,
+                                                const f32x4 (*RES)[2] = nullptr) {
     constexpr int N = NCB * 16, CPR = NCB * 4, ROWB = NCB * 64, RPI = 64 / CPR, NI = 16 / RPI;
+    static_assert(!OPERM || (NCB == 16 && !LG), "gin_operm: H = 256");
     const bool res = (flags & MIGNN_EPI_RESIDUAL) != 0;
     int l = lane;
     asm volatile("" : "+v"(l));
     const int ci = l % CPR, ri = l / CPR;
-    if (res && !CRES) {
+    if (res && !CRES && !OPERM) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             if constexpr (RPI == 1) {          // one row per instruction: scalar row address
@@ -178,16 +195,19 @@ __device__ __forceinline__ void staged_epilogue(unsigned char* STG, const float*
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
         const int n = 16 * cb + 4 * g;
-        f32x4* const slot = reinterpret_cast<f32x4*>(srow + 16 * ((4 * cb + g) ^ (lself & 15)));
+        const int nf = OPERM ? gin_operm(n) : n;          // the feature of accumulator n
+        f32x4* const slot = reinterpret_cast<f32x4*>(srow + 16 * ((nf >> 2) ^ (lself & 15)));
         f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (CRES) {
             if (res) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const f32x4 t = *reinterpret_cast<const f32x4*>(TB + 4 * (n + i));
+                    const f32x4 t = *reinterpret_cast<const f32x4*>(TB + 4 * (nf + i));
                     xv[i] = fmaf(t[2], c2, fmaf(t[1], c1, fmaf(t[0], c0, t[3])));
                 }
             }
+        } else if constexpr (OPERM) {
+            if (res) xv = RES[cb >> 1][cb & 1];
         } else if (res) {
             xv = *slot;
         }
@@ -405,11 +425,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     f32x4 acc[ACB];
 #pragma unroll
     for (int cb = 0; cb < ACB; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // GIN (chained, the nn.2 image in gin_operm order): the own row's values
+    // of every chunk, the epilogue's residual
+    constexpr bool OPERM = MODE == AGG_GIN && CHAIN;
+    f32x4 resx[OPERM ? AKP : 1][2];
     int p = 100;                                   // the row's running exponent
     bool fresh = true;                             // (the row's first chunk not seen yet)
     const unsigned char* const wl0 = lds + lane * 16;
 
     // ---------------------------------------------------------------- transform 1
+    // (not unrolled: the residual's register index is a select chain -- the
+    // unrolled loop measured slower, 15.8 vs 15.0 ms per 12.6M-row layer)
 #pragma unroll 1
     for (int kc = 0; kc < AKP; ++kc) {
         // chunk kc's W, own rows and out-of-tile rows landed (only the own rows
@@ -467,6 +493,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
             for (int i = 0; i < 4; ++i) {
                 a0[i] = fmaf(self_scale, s0[i], a0[i]);
                 a1[i] = fmaf(self_scale, s1[i], a1[i]);
+            }
+            if constexpr (OPERM) {
+                // the residual of the epilogue (gin_operm order): kept, not re-read
+#pragma unroll
+                for (int k = 0; k < AKP; ++k)
+                    if (k == kc) {
+                        resx[k][0] = s0;
+                        resx[k][1] = s1;
+                    }
             }
         }
         // refills: this wave's out-of-tile rows of chunk kc+1 (its reads of
@@ -585,12 +620,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
     if (tid < AH) {
         const int32_t* const qf = reinterpret_cast<const int32_t*>((CHAIN ? img2 : img1) + FB);
         const float* const bf = CHAIN ? b2 : b1;
+        const int nf = OPERM ? gin_operm(tid) : tid;       // (EV by image column)
         EV[tid] = p2neg_ag(qf[tid]);
-        EV[AH + tid] = hb ? bf[tid] : 0.f;
-        EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
-        EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
+        EV[AH + tid] = hb ? bf[nf] : 0.f;
+        EV[2 * AH + tid] = ha ? scale[nf] : 1.f;
+        EV[3 * AH + tid] = ha ? shift[nf] : 0.f;
     }
-    staged_epilogue<ACB>(lds, EV, acc, p, flags, x, ldx, out, ldo, t0, re, wave, lane, lself, g);
+    if constexpr (OPERM)
+        staged_epilogue<ACB, false, false, true>(lds, EV, acc, p, flags, x, ldx, out, ldo, t0, re, wave,
+                                                 lane, lself, g, nullptr, 0.f, 0.f, 0.f, nullptr,
+                                                 nullptr, resx);
+    else
+        staged_epilogue<ACB>(lds, EV, acc, p, flags, x, ldx, out, ldo, t0, re, wave, lane, lself, g);
 }
 
 // GIN layer 0 at H = 256 from the coordinates (input_proj composed into the
@@ -770,13 +811,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void g
     const bool hb = (flags & MIGNN_EPI_BIAS) != 0, ha = (flags & MIGNN_EPI_AFFINE) != 0;
     float* const EV = reinterpret_cast<float*>(lds + OFF_EV);
     if (tid < AH) {
+        const int nf = gin_operm(tid);         // (the nn.2 image's output order)
         EV[tid] = p2neg_ag(reinterpret_cast<const int32_t*>(img2 + FB)[tid]);
-        EV[AH + tid] = hb ? b2[tid] : 0.f;
-        EV[2 * AH + tid] = ha ? scale[tid] : 1.f;
-        EV[3 * AH + tid] = ha ? shift[tid] : 0.f;
+        EV[AH + tid] = hb ? b2[nf] : 0.f;
+        EV[2 * AH + tid] = ha ? scale[nf] : 1.f;
+        EV[3 * AH + tid] = ha ? shift[nf] : 0.f;
     }
-    staged_epilogue<ACB, true>(lds, EV, acc, p, flags, nullptr, 0, out, ldo, t0, re, wave, lane,
-                               lself, g, TB, pi[0], pi[1], pi[2]);
+    staged_epilogue<ACB, true, false, true>(lds, EV, acc, p, flags, nullptr, 0, out, ldo, t0, re, wave,
+                                            lane, lself, g, TB, pi[0], pi[1], pi[2]);
 }
 
 // TransformerConv layer 0 from the coordinates (heads = 4, any H = 64 CPL):
@@ -955,31 +997,33 @@ constexpr int g_fused_diag_flags = 0;   // the product library has no ablation s
 // exponent table as mignn_linear_f16x3_prep's image
 // (n <= 256 output columns; columns past n are zero, exponent 100)
 __global__ __launch_bounds__(256) void perm_exp_kernel(const float* __restrict__ w, int n,
-                                                       int32_t* __restrict__ q) {
+                                                       int32_t* __restrict__ q, bool operm) {
     const int colm = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    const int src = operm ? gin_operm(colm) : colm;   // the W row image column colm holds
     uint32_t m = 0;
     if (colm < n)
-        for (int i = lane; i < AH; i += 64) m = max(m, __float_as_uint(fabsf(w[colm * AH + i])));
+        for (int i = lane; i < AH; i += 64) m = max(m, __float_as_uint(fabsf(w[src * AH + i])));
     for (int o = 32; o > 0; o >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o)));
     if (lane == 0) q[colm] = sexp_ag(m);
 }
 __global__ __launch_bounds__(256) void perm_frag_kernel(const float* __restrict__ w, int n,
                                                         const int32_t* __restrict__ q,
-                                                        unsigned char* __restrict__ img) {
+                                                        unsigned char* __restrict__ img, bool operm) {
     const int t = blockIdx.x * 256 + threadIdx.x;   // (kc, cb, lane)
     if (t >= AKP * ACB * 64) return;
     const int lane = t & 63;
     const int cb = (t >> 6) % ACB;
     const int kc = (t >> 6) / ACB;
     const int colm = 16 * cb + (lane & 15);
+    const int src = operm ? gin_operm(colm) : colm;
     const int gq = lane >> 4;
     const float sc = p2_ag(q[colm]);
     f16x8 h, l;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int kk = 16 * (2 * kc + (j >> 2)) + 4 * gq + (j & 3);
-        const float v = colm < n ? w[colm * AH + kk] * sc : 0.f;
+        const float v = colm < n ? w[src * AH + kk] * sc : 0.f;
         const _Float16 hh = static_cast<_Float16>(v);
         h[j] = hh;
         l[j] = static_cast<_Float16>(v - static_cast<float>(hh));
@@ -991,13 +1035,14 @@ __global__ __launch_bounds__(256) void perm_frag_kernel(const float* __restrict_
 
 // k-permuted image of W [n <= 256, 256] (layout of mignn_linear_f16x3_prep's
 // image, 16 column blocks, exponent table after the fragments)
-int perm_prep(const float* w, int n, unsigned char* img, hipStream_t st) {
+// operm: output columns in gin_operm order (n = 256; the GIN nn.2 image)
+int perm_prep(const float* w, int n, unsigned char* img, hipStream_t st, bool operm = false) {
     int32_t* q = reinterpret_cast<int32_t*>(img + static_cast<size_t>(AKP) * ACB * 2 * AFRAG);
-    hipLaunchKernelGGL(perm_exp_kernel, dim3(AH / 4), dim3(256), 0, st, w, n, q);
+    hipLaunchKernelGGL(perm_exp_kernel, dim3(AH / 4), dim3(256), 0, st, w, n, q, operm);
     int rc = launch_status("perm_exp_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(perm_frag_kernel, dim3((AKP * ACB * 64 + 255) / 256), dim3(256), 0, st, w, n,
-                       q, img);
+                       q, img, operm);
     return launch_status("perm_frag_kernel");
 }
 
@@ -2050,7 +2095,7 @@ extern "C" int mignn_gin_fused_prep(const float* w2, int h, void* img, size_t im
     MIGNN_REQUIRE(w2 && img && h == AH, "gin_fused_prep: h must be 256");
     MIGNN_REQUIRE(img_bytes >= mignn_gin_fused_prep_bytes(h), "gin_fused_prep: image too small");
     MIGNN_REQUIRE(aligned16(img), "gin_fused_prep: image not 16-B aligned");
-    return perm_prep(w2, AH, static_cast<unsigned char*>(img), as_stream(stream));
+    return perm_prep(w2, AH, static_cast<unsigned char*>(img), as_stream(stream), true);
 }
 
 static int check_common(const int32_t* row_ptr, const int32_t* col, const float* x, int64_t ldx,

@@ -2,7 +2,9 @@
 blocks) vs the launches it replaces (sum aggregate + two split-fp16 GEMMs) on
 configs[4]'s per-GPU shard mesh (500 x 400 x 63 periodic hex, 12.6M nodes,
 locality order), HIP events, interleaved rounds; max |fused - unfused|.
-Env: FB_GRID (500,400,63), FB_REPS (5), FB_MODE (gin | gcn)."""
+Env: FB_GRID (500,400,63), FB_REPS (5), FB_MODE (gin | gcn), FB_LIBS
+(name=path,...: variant builds of libmignn.so timed beside it, GIN: each
+with its own nn.2 image from its own mignn_gin_fused_prep)."""
 import json
 import os
 import statistics
@@ -91,6 +93,17 @@ def unfused(Y):
 
 cases = ({"unfused": gat(0), "fused": gat(1)} if mode == "gat" else
          {"unfused": unfused, "fused": fused()})
+for item in [v for v in os.environ.get("FB_LIBS", "").split(",") if v and mode == "gin"]:
+    vname, vpath = item.split("=")
+    VL = _lib._load(vpath, _lib.SIGNATURES)
+    vimg2 = torch.empty(VL.mignn_gin_fused_prep_bytes(H), dtype=torch.uint8, device=dev)
+    _lib.check(VL.mignn_gin_fused_prep(P(W2), H, P(vimg2), vimg2.numel(), st), "vprep")
+
+    def fv(Y, VL=VL, vimg2=vimg2):
+        _lib.check(VL.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
+                                            P(img1), P(b1), P(vimg2), P(b2), P(sc), P(sh), 15,
+                                            P(Y), H, st), "gin_fused_v")
+    cases[f"fused@{vname}"] = fv
 for dflag in [int(v) for v in os.environ.get("FB_ABLATE", "").split(",") if v]:
     cases[f"fused_ablate_{dflag}"] = gat(1, dflag) if mode == "gat" else fused(dflag)
 outs = {k: torch.full_like(X, float("nan")) for k in cases}
