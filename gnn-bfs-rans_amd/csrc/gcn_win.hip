@@ -66,6 +66,14 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 #ifndef MIGNN_WIN_DIRECT
 #define MIGNN_WIN_DIRECT 1
 #endif
+// H = 128 transform: 16-column blocks per wave (1: 8 column blocks x 64
+// rows, every wave reads the whole A image; 2: 4 column pairs x 32 rows, each
+// A fragment feeds 6 MFMAs and half the image is read per wave -- measured
+// 2.79 ms at PD 3 and 3.05 at PD 5 vs 2.78 for 1: the A-image reads are not
+// what bounds the step)
+#ifndef MIGNN_WIN_CPW
+#define MIGNN_WIN_CPW 1
+#endif
 #ifndef MIGNN_WIN_PD
 #define MIGNN_WIN_PD 5
 #endif
@@ -672,36 +680,40 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     // ------------------------------------------------------------ prologue
     for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
     const int rr0 = lane & 15, gg0 = lane >> 4;
-    constexpr int WN = H / 16, WM = C::NW / WN, IBW = (C::BM / 16) / WM;
+    constexpr int CPW = MIGNN_WIN_CPW;            // 16-column blocks per wave
+    constexpr int WN = H / 16 / CPW, WM = C::NW / WN, IBW = (C::BM / 16) / WM;
     static_assert(WN * WM == C::NW && IBW * WM * 16 == C::BM, "window transform grid");
     const int wn = wave % WN, wm = wave / WN;
-    const int n0 = 16 * wn;
-    f16x8w wh[C::KC], wl[C::KC];
-    int qw = 0;
+    const int n0 = 16 * CPW * wn;
+    f16x8w wh[CPW][C::KC], wl[CPW][C::KC];
+    int qw[CPW];
     if constexpr (!AGG) {
-        float wv[C::KC][8];
-        uint32_t m = 0;
 #pragma unroll
-        for (int kc = 0; kc < C::KC; ++kc) {
-            const float* pw = W + static_cast<int64_t>(n0 + rr0) * H + 32 * kc + 8 * gg0;
-            const float4 a = ld4(pw), b = ld4(pw + 4);
-            float* w8 = wv[kc];
-            w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
-            w8[4] = b.x; w8[5] = b.y; w8[6] = b.z; w8[7] = b.w;
+        for (int cp = 0; cp < CPW; ++cp) {
+            float wv[C::KC][8];
+            uint32_t m = 0;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(w8[j])));
-        }
-        qw = wsplit_exp(wwave_max(m));            // one exponent per 16-column block
+            for (int kc = 0; kc < C::KC; ++kc) {
+                const float* pw = W + static_cast<int64_t>(n0 + 16 * cp + rr0) * H + 32 * kc + 8 * gg0;
+                const float4 a = ld4(pw), b = ld4(pw + 4);
+                float* w8 = wv[kc];
+                w8[0] = a.x; w8[1] = a.y; w8[2] = a.z; w8[3] = a.w;
+                w8[4] = b.x; w8[5] = b.y; w8[6] = b.z; w8[7] = b.w;
 #pragma unroll
-        for (int kc = 0; kc < C::KC; ++kc)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float sv = ldexpf(wv[kc][j], qw);
-                const _Float16 hh = static_cast<_Float16>(sv);
-                wh[kc][j] = hh;
-                wl[kc][j] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(w8[j])));
             }
-        if (wm == 0 && lane < 16) {
+            qw[cp] = wsplit_exp(wwave_max(m));    // one exponent per 16-column block
+#pragma unroll
+            for (int kc = 0; kc < C::KC; ++kc)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float sv = ldexpf(wv[kc][j], qw[cp]);
+                    const _Float16 hh = static_cast<_Float16>(sv);
+                    wh[cp][kc][j] = hh;
+                    wl[cp][kc][j] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                }
+        }
+        if (wm == 0 && lane < 16 * CPW) {
             const int n = n0 + lane;
             EPI[n] = (flags & MIGNN_EPI_BIAS) ? bias[n] : 0.f;
             EPI[H + n] = (flags & MIGNN_EPI_AFFINE) ? scale[n] : 1.f;
@@ -896,7 +908,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         wtr.stamp(2);
         // ---- (P1) phase B of tile s - 1, its split and residual seeds
         constexpr int NSEED = AGG ? 1 : IBW;
-        f32x4 seed[NSEED];
+        f32x4 seed[NSEED][CPW];
         if (prv >= 0) {
 #pragma unroll
             for (int qd = 0; qd < C::NQ; ++qd) {
@@ -942,18 +954,21 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         REXP[C::RPW * wave + 4 * qd + (ln >> 4)] = pe;
                     }
                 }
-                // residual + bias of my output block (tile s-1's rows of my
-                // row group, my 16 columns), before slot (s-1) % 3 is refilled
-                const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[n0 + 4 * gg]);
+                // residual + bias of my output blocks (tile s-1's rows of my
+                // row group, my columns), before slot (s-1) % 3 is refilled
 #pragma unroll
-                for (int ib = 0; ib < IBW; ++ib) {
-                    const int lr = (wm * IBW + ib) * 16 + rr;
-                    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (has_res) {
-                        const int ch = (n0 >> 2) + gg;
-                        rv = *reinterpret_cast<const float4*>(XP + lr * C::ROWB + ((ch ^ (lr & 7)) << 4));
+                for (int cp = 0; cp < CPW; ++cp) {
+                    const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[n0 + 16 * cp + 4 * gg]);
+#pragma unroll
+                    for (int ib = 0; ib < IBW; ++ib) {
+                        const int lr = (wm * IBW + ib) * 16 + rr;
+                        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (has_res) {
+                            const int ch = ((n0 + 16 * cp) >> 2) + gg;
+                            rv = *reinterpret_cast<const float4*>(XP + lr * C::ROWB + ((ch ^ (lr & 7)) << 4));
+                        }
+                        seed[ib][cp] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
                     }
-                    seed[ib] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
                 }
             }
         }
@@ -996,14 +1011,16 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                             __builtin_nontemporal_store(accp[qd][j], reinterpret_cast<f32x4*>(out + (tp0 + lrow) * ldo + 4 * (c0 + 16 * j)));
                     }
             } else {
-                // (3) transform: my 16 output columns x my row blocks
+                // (3) transform: my output column blocks x my row blocks
                 int pr[IBW];
-                f32x4 accm[IBW];
+                f32x4 accm[IBW][CPW];
 #pragma unroll
                 for (int ib = 0; ib < IBW; ++ib) {
                     pr[ib] = REXP[(wm * IBW + ib) * 16 + rr];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) accm[ib][r] = ldexpf(seed[ib][r], pr[ib] + qw);
+                    for (int cp = 0; cp < CPW; ++cp)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) accm[ib][cp][r] = ldexpf(seed[ib][cp][r], pr[ib] + qw[cp]);
                 }
                 {
                     const int sw = asw<H>(rr);
@@ -1025,9 +1042,12 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         if (t < NPC) dma_piece(t);
                         if (MODE & 4) continue;
                         if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
-                        accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fh[t % NF], accm[ib], 0, 0, 0);
-                        accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[kc], fl[t % NF], accm[ib], 0, 0, 0);
-                        accm[ib] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[kc], fh[t % NF], accm[ib], 0, 0, 0);
+#pragma unroll
+                        for (int cp = 0; cp < CPW; ++cp) {
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fl[t % NF], accm[ib][cp], 0, 0, 0);
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
+                        }
                         __builtin_amdgcn_sched_barrier(0);
                     }
 #pragma unroll
@@ -1037,26 +1057,31 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
 #if MIGNN_WIN_DIRECT
                 {
                     // epilogue stored straight from the accumulators: lane (rr, gg) of
-                    // block ib holds row 16 ib + rr, columns n0 + 4 gg .. +3
-                    const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 4 * gg]);
-                    const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + n0 + 4 * gg]);
-                    static_assert(IBW == C::NST, "one store per row block keeps the per-step store count");
+                    // block (ib, cp) holds row 16 ib + rr, columns n0 + 16 cp + 4 gg .. +3
+                    static_assert(IBW * CPW == C::NST, "one store per block keeps the per-step store count");
 #pragma unroll
-                    for (int ib = 0; ib < IBW; ++ib) {
-                        f32x4 o;
+                    for (int cp = 0; cp < CPW; ++cp) {
+                        const int nc = n0 + 16 * cp + 4 * gg;
+                        const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + nc]);
+                        const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + nc]);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float v = ldexpf(accm[ib][r], -(pr[ib] + qw));
-                            if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                            if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
-                            o[r] = v;
+                        for (int ib = 0; ib < IBW; ++ib) {
+                            f32x4 o;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                float v = ldexpf(accm[ib][cp][r], -(pr[ib] + qw[cp]));
+                                if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
+                                if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
+                                o[r] = v;
+                            }
+                            const int lr = (wm * IBW + ib) * 16 + rr;
+                            if (lr < nlocp)
+                                __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + nc));
                         }
-                        const int lr = (wm * IBW + ib) * 16 + rr;
-                        if (lr < nlocp)
-                            __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + n0 + 4 * gg));
                     }
                 }
 #else
+                static_assert(CPW == 1, "the staged epilogue: one column block per wave");
                 // (B3) every wave done with the A image: stage there
                 wbar<kWLgkm0>();
                 {
@@ -1067,7 +1092,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         float o[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            float v = ldexpf(accm[ib][r], -(pr[ib] + qw));
+                            float v = ldexpf(accm[ib][0][r], -(pr[ib] + qw[0]));
                             if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
                             if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
                             o[r] = v;

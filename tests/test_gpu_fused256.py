@@ -568,6 +568,44 @@ def test_gat_layer0_coords_matches_two_step(hidden, monkeypatch):
     assert err <= 2e-5 * max(1.0, r64.abs().max().item()), err
 
 
+@pytest.mark.parametrize("hidden", [64, 128, 256])
+def test_gat_layer0_coords_next_logits(hidden):
+    """The shard-only route of GAT layer 0 (FlowGNNShard, mignn.dist): the
+    collapsed layer 0 (mignn_gat_layer0_coords) with logits_next forms layer
+    1's logits in its epilogue.  Direct parity on a row range: the output rows
+    equal the launch without logits_next (bitwise), and the logits match the
+    GEMV out . wlog_next^T (fp64) of those rows; rows outside stay unwritten."""
+    from mignn import FlowGNN
+    from mignn.gnn_model import CSR_ONE_SELF_LOOP
+    from mignn.synthetic import seeded_state_dict
+    n = 3000
+    rb, re = 37, 2950
+    ei = _graph(n, 83)
+    g = torch.Generator(device=DEV).manual_seed(hidden + 9)
+    x = torch.rand(n, 3, device=DEV, generator=g) * 2 - 1
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, hidden_dim=hidden, num_layers=2,
+                layer_type="GAT")
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=hidden + 9))
+    m = m.to(DEV).eval()
+    m.gat_coords = True
+    csr = m._csr.get(ei, n, CSR_ONE_SELF_LOOP, None)
+    pos = m._coords(x, csr)
+    with torch.no_grad():
+        out0 = torch.full((n, hidden), float("nan"), device=DEV)
+        m._gat_layer0(csr, pos, rb, re, out0)
+        out1 = torch.full_like(out0, float("nan"))
+        lg = torch.full((n, 8), float("nan"), device=DEV)
+        m._gat_layer0(csr, pos, rb, re, out1, logits_next=lg)
+        wlog_n, _ = m._gat_weights(m.gnn_layers[1])
+    torch.cuda.synchronize()
+    assert torch.equal(out0[rb:re], out1[rb:re])
+    assert torch.isnan(out1[:rb]).all() and torch.isnan(out1[re:]).all()
+    assert torch.isnan(lg[:rb]).all() and torch.isnan(lg[re:]).all()
+    ref = out1[rb:re].double() @ wlog_n.double().t()
+    err = (lg[rb:re].double() - ref).abs().max().item()
+    assert err <= 2e-6 * max(1.0, ref.abs().max().item()), err
+
+
 @pytest.mark.parametrize("h", [64, 128, 256])
 @pytest.mark.parametrize("fused", [1, 0])
 def test_gat_layer_next_logits(h, fused):
