@@ -290,8 +290,12 @@ def main():
             traffic = None
     roofline = None
     if args.layer_type == "GCN":
-        roofline = gcn_roofline(launches, H, deg_plus_self, model.precision, traffic,
-                                model._gcn_kernel(H))
+        route = model._gcn_kernel(H)
+        if world > 1 and route == "win" and model.gcn_kernel == "auto":
+            # (a shard's rows are block-ordered: FlowGNN._gcn_kernel's fallback)
+            from mignn.gnn_model import GCN_BLOCK_ORDER
+            route = GCN_BLOCK_ORDER.get(H, "pc")
+        roofline = gcn_roofline(launches, H, deg_plus_self, model.precision, traffic, route)
 
     exact = None
     if model.precision != "f32":

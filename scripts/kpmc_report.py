@@ -13,7 +13,8 @@ for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), re
     for row in csv.DictReader(open(f)):
         k = row.get("Kernel_Name", "")
         import re
-        m = re.search(r"(gcn_\w+_kernel|gcn_f16x3_kernel)(<[^>]*>)?", k)
+        m = re.search(r"(gcn_\w+_kernel|agg_gemm_kernel|tf_fused_kernel|gat_fused_kernel|"
+                      r"gemm_f16x3_kernel|gin0_fused_kernel)(<[^>]*>)?", k)
         if not m:
             continue
         short = m.group(1) + (m.group(2) or "")
