@@ -203,15 +203,27 @@ __host__ __device__ inline int64_t win_tile(const WinSched& S, int p, int64_t s)
     const int64_t t = S.t2 + static_cast<int64_t>(p) * S.chunk + j;
     return t < S.ntiles ? t : -1;
 }
-__host__ __device__ inline void win_where(const WinSched& S, int64_t t, int& p, int64_t& s) {
-    if (t < S.t2) {
-        const int64_t i = t / S.L;
-        p = static_cast<int>(i % S.G);
+
+// 32-bit forms for the plan kernel (tiles < 2^25: rows are int32)
+__device__ inline int win_tile32(const WinSched& S, int p, int s) {
+    if (s < 0) return -1;
+    const int s1 = S.R1 * S.L;
+    if (s < s1) return ((s / S.L) * S.G + p) * S.L + s % S.L;
+    const int j = s - s1;
+    if (j >= S.chunk) return -1;
+    const int t = static_cast<int>(S.t2) + p * S.chunk + j;
+    return t < S.ntiles ? t : -1;
+}
+__device__ inline void win_where32(const WinSched& S, int t, int& p, int& s) {
+    const int t2 = static_cast<int>(S.t2);
+    if (t < t2) {
+        const int i = t / S.L;
+        p = i % S.G;
         s = (i / S.G) * S.L + t % S.L;
     } else {
-        const int64_t u = t - S.t2;
-        p = static_cast<int>(u / S.chunk);
-        s = static_cast<int64_t>(S.R1) * S.L + u % S.chunk;
+        const int u = t - t2;
+        p = u / S.chunk;
+        s = S.R1 * S.L + u % S.chunk;
     }
 }
 
@@ -446,10 +458,9 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
     __shared__ uint32_t xl[C::NW * C::XLW];
     const uint32_t zcode = static_cast<uint32_t>(C::OFF_ZERO >> C::CSH);
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        int p;
-        int64_t s;
-        win_where(S, t, p, s);
-        const int64_t tprev = win_tile(S, p, s - 1), tnext = win_tile(S, p, s + 1);
+        int p, s;
+        win_where32(S, static_cast<int>(t), p, s);
+        const int64_t tprev = win_tile32(S, p, s - 1), tnext = win_tile32(S, p, s + 1);
         const int sc = static_cast<int>(s % 3), sp = static_cast<int>((s + 2) % 3),
                   sn = static_cast<int>((s + 1) % 3);
         const int64_t t0 = rb + t * C::BM;
@@ -472,11 +483,26 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
             e0 = row_ptr[r];
             deg = row_ptr[r + 1] - e0;
         }
+        // the row's entries, loaded at once into registers (a loop over deg
+        // serialised one load latency per entry); rows of degree > 8 take
+        // the CSR path -- their entries are not read, their ext slots not
+        // counted
+        const bool small = deg <= 8;
+        int cj[8];
+        uint32_t wj[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const bool v = small && e < deg;
+            cj[e] = v ? col[e0 + e] : -1;
+            wj[e] = v ? __float_as_uint(ew[e0 + e]) : 0u;
+        }
         // pass 1: ext entries of the row
         int next = 0, nA = 0;
         bool haveN = false;
-        for (int e = 0; e < deg; ++e) {
-            const int64_t c = col[e0 + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if (cj[e] < 0) continue;
+            const int64_t c = cj[e];
             int64_t off;
             if (in_tile(c, t, off) || in_tile(c, tprev, off)) {
                 ++nA;
@@ -495,7 +521,7 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
         }
         pre -= next;
         __syncthreads();
-        bool far = deg > 8 || nA > kWA || pre + next > C::KX;
+        bool far = !small || nA > kWA || pre + next > C::KX;
         uint32_t code[8];
         uint32_t wb[8];
 #pragma unroll
@@ -503,12 +529,14 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
             code[q] = zcode;
             wb[q] = 0u;
         }
-        if (lr < nloc && deg > 0 && deg <= 8) {
+        if (lr < nloc && deg > 0 && small) {
             int k = pre, a = 0;
             bool usedN = false;
-            for (int e = 0; e < deg; ++e) {
-                const int64_t c = col[e0 + e];
-                const uint32_t w = __float_as_uint(ew[e0 + e]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (cj[e] < 0) continue;
+                const int64_t c = cj[e];
+                const uint32_t w = wj[e];
                 int64_t off;
                 uint32_t cd;
                 int slot;
