@@ -32,7 +32,7 @@ b = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
 Y = torch.empty_like(X)
-if "win" in kinds or "winagg" in kinds:
+if "win" in kinds or "winagg" in kinds or "windiag" in kinds:
     # the window kernel on the column-order CSR of the same mesh
     _pos, _ei = grid_graph(250, 200, 200, device=dev)
     _, inv_c, info_c = locality_order(_pos, _ei, cols=True)
@@ -94,5 +94,13 @@ for _ in range(reps):
     if "ring" in kinds:
         _lib.check(L.mignn_gcn_layer_ring(P(rplan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
                                           0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "ring")
+    if "windiag" in kinds:
+        # the window kernel's ablations (diag build; kernel names carry the
+        # mode): 1 ext rows from the zero row, 4 no MFMAs, 32 aggregate only,
+        # 33 aggregate only + ext from the zero row -- the per-phase VALU split
+        LD = _lib.diag_lib()
+        for m in (1, 4, 32, 33):
+            _lib.check(LD.mignn_diag_win(m, P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X), H,
+                                         0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "windiag")
 torch.cuda.synchronize()
 print("ok")
