@@ -227,8 +227,9 @@ def main():
     dev_errors = [0]
     launches = []   # (start_event, end_event, n_rows) of the headline loop
     launches32 = []  # the same in the exact-fp32 loop
+    launches01 = []  # layers 0 + 1 in the codes form (GCN H = 128, window route)
     recording = [None]
-    restore = time_layers(model, recording)
+    restore = time_layers(model, recording, launches01)
 
     def timed_loop(cache_graph, rec_into=None):
         # cache_graph False: every forward rebuilds the CSR + GCN norm from
@@ -296,6 +297,17 @@ def main():
             from mignn.gnn_model import GCN_BLOCK_ORDER
             route = GCN_BLOCK_ORDER.get(H, "pc")
         roofline = gcn_roofline(launches, H, deg_plus_self, model.precision, traffic, route)
+        if roofline is not None and launches01:
+            # layers 0 + 1 through the row codes (FlowGNN._gcn_layers01_codes):
+            # the launches above are layers 2 .. L-1
+            ms01 = sum(e0.elapsed_time(e1) for e0, e1, _ in launches01) / len(launches01)
+            roofline["layers01_codes"] = {
+                "kernels": "gcn_layer0_codes_kernel<3> + gcn_win_kernel<128, codes> "
+                           "(mignn_gcn_layer0_codes + mignn_gcn_layer_win_codes)",
+                "avg_ms": round(ms01, 4), "launches": len(launches01),
+                "note": "layer 0 writes 32-B row codes, layer 1 expands the rows it "
+                        "reads from them (DESIGN.md 3.16); the roofline above is "
+                        "over layers 2 .. L-1"}
 
     exact = None
     if model.precision != "f32":
@@ -394,11 +406,23 @@ def main():
         dist.destroy_process_group()
 
 
-def time_layers(model, recording):
+def time_layers(model, recording, recording01=None):
     """Wrap model._layer with HIP events on the current stream (the stream the
     layer kernels are launched on); events go to recording[0] when it is a
-    list.  Returns the restore function."""
+    list -- and those of the codes form of layers 0 + 1
+    (FlowGNN._gcn_layers01_codes) to recording01.  Returns the restore
+    function."""
     orig_layer = model._layer
+    orig01 = model._gcn_layers01_codes
+
+    def timed01(csr, pos, n, out):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        orig01(csr, pos, n, out)
+        e1.record()
+        if recording[0] is not None and recording01 is not None:
+            recording01.append((e0, e1, n))
 
     def timed_layer(i, layer, csr, xin, out, rb, re, **kw):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -410,9 +434,11 @@ def time_layers(model, recording):
             recording[0].append((e0, e1, re - rb))
 
     model._layer = timed_layer
+    model._gcn_layers01_codes = timed01
 
     def restore():
         model._layer = orig_layer
+        model._gcn_layers01_codes = orig01
     return restore
 
 

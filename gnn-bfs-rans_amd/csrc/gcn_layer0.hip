@@ -32,6 +32,50 @@ constexpr int kWaves = 4;
 // the one-role form of round 1.
 constexpr int kSplitRows = kWaves * 64;   // rows per block
 
+// (c_i, C_i = sum_j w_ij c_j, s_i = sum_j w_ij) of row ri, CSR order (the
+// split kernel's gather role and the codes kernel: the same arithmetic)
+template <int D>
+__device__ __forceinline__ void layer0_gather(const int32_t* __restrict__ row_ptr,
+                                              const int32_t* __restrict__ col,
+                                              const float* __restrict__ ew,
+                                              const float* __restrict__ pos, int64_t ldp,
+                                              int64_t ri, float (&c)[D], float (&C)[D],
+                                              float& sum) {
+    sum = 0.f;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { c[a] = pos[ri * ldp + a]; C[a] = 0.f; }
+    const int32_t e0 = row_ptr[ri], e1 = row_ptr[ri + 1];
+    constexpr int kU = 8;
+    int32_t jj[kU];
+    float ww[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+        jj[k] = e0 + k < e1 ? col[e0 + k] : 0;
+        ww[k] = e0 + k < e1 ? ew[e0 + k] : 0.f;
+    }
+    float pv[kU][D];
+#pragma unroll
+    for (int k = 0; k < kU; ++k)
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+            pv[k][a] = e0 + k < e1 ? pos[(int64_t)jj[k] * ldp + a] : 0.f;
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+        if (e0 + k < e1) {
+            sum += ww[k];
+#pragma unroll
+            for (int a = 0; a < D; ++a) C[a] = fmaf(ww[k], pv[k][a], C[a]);
+        }
+    }
+    for (int32_t e = e0 + kU; e < e1; ++e) {
+        const int64_t j = col[e];
+        const float w = ew[e];
+        sum += w;
+#pragma unroll
+        for (int a = 0; a < D; ++a) C[a] = fmaf(w, pos[j * ldp + a], C[a]);
+    }
+}
+
 template <int D>
 __global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -64,40 +108,8 @@ __global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
         if (gather) {
             const int64_t r = bg * kSplitRows + wave * 64 + lane;
             if (bg < nblk && r < nrows) {
-                const int64_t ri = row_begin + r;
-                float c[D], C[D], sum = 0.f;
-#pragma unroll
-                for (int a = 0; a < D; ++a) { c[a] = pos[ri * ldp + a]; C[a] = 0.f; }
-                const int32_t e0 = row_ptr[ri], e1 = row_ptr[ri + 1];
-                constexpr int kU = 8;
-                int32_t jj[kU];
-                float ww[kU];
-#pragma unroll
-                for (int k = 0; k < kU; ++k) {
-                    jj[k] = e0 + k < e1 ? col[e0 + k] : 0;
-                    ww[k] = e0 + k < e1 ? ew[e0 + k] : 0.f;
-                }
-                float pv[kU][D];
-#pragma unroll
-                for (int k = 0; k < kU; ++k)
-#pragma unroll
-                    for (int a = 0; a < D; ++a)
-                        pv[k][a] = e0 + k < e1 ? pos[(int64_t)jj[k] * ldp + a] : 0.f;
-#pragma unroll
-                for (int k = 0; k < kU; ++k) {
-                    if (e0 + k < e1) {
-                        sum += ww[k];
-#pragma unroll
-                        for (int a = 0; a < D; ++a) C[a] = fmaf(ww[k], pv[k][a], C[a]);
-                    }
-                }
-                for (int32_t e = e0 + kU; e < e1; ++e) {
-                    const int64_t j = col[e];
-                    const float w = ew[e];
-                    sum += w;
-#pragma unroll
-                    for (int a = 0; a < D; ++a) C[a] = fmaf(w, pos[j * ldp + a], C[a]);
-                }
+                float c[D], C[D], sum;
+                layer0_gather<D>(row_ptr, col, ew, pos, ldp, row_begin + r, c, C, sum);
                 float* const ag = agg[buf][wave * 64 + lane];
 #pragma unroll
                 for (int a = 0; a < D; ++a) { ag[a] = c[a]; ag[D + a] = C[a]; }
@@ -132,10 +144,53 @@ __global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
     }
 }
 
+// Layer-0 codes (the codes form of the window GCN kernel, gcn_win.hip): per
+// row the 8 floats (c_i, C_i, s_i, 0...) -- the values the split kernel's
+// store role expands -- instead of the [H] row: 32 B written per row.
+template <int D>
+__global__ __launch_bounds__(256) void gcn_layer0_codes_kernel(
+    const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
+    int64_t row_end, float* __restrict__ codes, int64_t ldc) {
+    for (int64_t ri = row_begin + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; ri < row_end;
+         ri += (int64_t)gridDim.x * blockDim.x) {
+        float c[D], C[D], sum;
+        layer0_gather<D>(row_ptr, col, ew, pos, ldp, ri, c, C, sum);
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < D; ++a) { v[a] = c[a]; v[D + a] = C[a]; }
+        v[2 * D] = sum;
+        float* const o = codes + ri * ldc;
+        *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+}
+
 }  // namespace
 }  // namespace mignn
 
 using namespace mignn;
+
+extern "C" int mignn_gcn_layer0_codes(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                                      const float* pos, int64_t ldp, int in_dim,
+                                      int64_t row_begin, int64_t row_end, float* codes,
+                                      int64_t ldc, void* stream) {
+    MIGNN_REQUIRE(row_ptr && col && ew && pos && codes, "gcn_layer0_codes: null pointer");
+    MIGNN_REQUIRE(in_dim >= 1 && in_dim <= 3, "gcn_layer0_codes: in_dim must be 1..3 (got %d)", in_dim);
+    MIGNN_REQUIRE(ldp >= in_dim, "gcn_layer0_codes: ldp < in_dim");
+    MIGNN_REQUIRE(ldc % 4 == 0 && ldc >= 8 && aligned16(codes), "gcn_layer0_codes: codes rows must be 16-B aligned, >= 8 wide");
+    MIGNN_REQUIRE(row_begin >= 0 && row_end >= row_begin, "gcn_layer0_codes: bad row range");
+    if (row_end == row_begin) return MIGNN_OK;
+    hipStream_t st = as_stream(stream);
+    const int64_t blocks = (row_end - row_begin + 255) / 256;
+    const unsigned grid = static_cast<unsigned>(blocks < 8192 ? blocks : 8192);
+    switch (in_dim) {
+    case 1: hipLaunchKernelGGL(gcn_layer0_codes_kernel<1>, dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc); break;
+    case 2: hipLaunchKernelGGL(gcn_layer0_codes_kernel<2>, dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc); break;
+    default: hipLaunchKernelGGL(gcn_layer0_codes_kernel<3>, dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc); break;
+    }
+    return launch_status("gcn_layer0_codes_kernel");
+}
 
 extern "C" int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* col, const float* ew,
                                        const float* pos, int64_t ldp, int in_dim,

@@ -77,6 +77,10 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 #ifndef MIGNN_WIN_PD
 #define MIGNN_WIN_PD 5
 #endif
+// codes form: A-fragment prefetch depth (the expansion's registers beside it)
+#ifndef MIGNN_WIN_PD_X0
+#define MIGNN_WIN_PD_X0 3
+#endif
 constexpr int kWRec = 48;                 // bytes per plan record: 8 u16 codes + 8 f32 weights
 constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the next-tile entry
 constexpr int kWHdr = 256;                // plan header bytes
@@ -118,6 +122,12 @@ struct WCfg {
     static constexpr int OFF_EPI = OFF_REXP + BM * 4;
     static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
     static constexpr int OFF_STG = OFF_AH;             // output staging (fp32 rows) over AH | AL
+    // layer 1 from layer-0 codes (MODE 64): per wave 8 own-row + 4 ext-row
+    // codes (32 B each) DMA'd per step, the [H][8] expansion table
+    static constexpr int CODEB = 32, CODE_W = (RPW + KX / NW) * CODEB;
+    static constexpr int OFF_CODE = LDS_BYTES;
+    static constexpr int OFF_COEF = OFF_CODE + NW * CODE_W;
+    static constexpr int LDS_BYTES_X0 = OFF_COEF + H * 8 * 4;
     static constexpr int WGPC = H == 64 ? 2 : 1;       // workgroups per CU
     static constexpr int NQ = RPW / 4;                 // row quads per wave
     static constexpr int KC = H / 32;
@@ -127,6 +137,8 @@ struct WCfg {
     static constexpr int LPRW = ROWB / 16, RPI = 64 / LPRW;
     static constexpr int NST = RPW / RPI;              // row stores per wave
     static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
+    static_assert(LDS_BYTES_X0 * WGPC <= 160 * 1024, "LDS budget (codes form)");
+    static_assert(RPW == 8 && KX / NW == 4 && CODE_W / 16 <= 64, "codes DMA: 16 own + 8 ext lanes");
     static_assert(2 * A_BYTES >= BM * ROWB, "staging fits the A images");
     static_assert(EPW == NPE * RPP && EPW + 1 <= XLW, "ext rows per wave");
     static_assert((CODE_END >> CSH) <= 65536, "u16 codes");
@@ -598,8 +610,10 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
 
 // ---------------------------------------------------------------- layer
 // MODE: 32 aggregate only (mignn_gcn_aggregate_win: the fp32 sums are the
-// output); timing ablations (mignn_diag_win only): 1 ext rows from the zero
-// row, 4 no MFMAs.  EPIF: the epilogue flags at compile time (15, 11; -1: from
+// output); 64 layer 1 from layer-0 codes (mignn_gcn_layer_win_codes: x =
+// codes [rows, 8], xcoef = the [H][8] expansion, see "codes form" below);
+// timing ablations (mignn_diag_win only): 1 ext rows from the zero
+// row, 2 own rows from the zero row, 4 no MFMAs.  EPIF: the epilogue flags at compile time (15, 11; -1: from
 // `flags`).
 template <int H, int MODE = 0, int EPIF = -1>
 __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void gcn_win_kernel(
@@ -607,11 +621,14 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     const int32_t* __restrict__ col, const float* __restrict__ ew, const float* __restrict__ x,
     int64_t ldx, int64_t rb, int64_t re, const float* __restrict__ W,
     const float* __restrict__ bias, const float* __restrict__ scale,
-    const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo) {
+    const float* __restrict__ shift, int flags, float* __restrict__ out, int64_t ldo,
+    const float* __restrict__ xcoef) {
     using C = WCfg<H>;
     constexpr bool AGG = (MODE & 32) != 0;
+    constexpr bool X0 = (MODE & 64) != 0;
+    static_assert(!X0 || !AGG, "codes form: the full layer only");
     if constexpr (EPIF >= 0) flags = EPIF;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[X0 ? C::LDS_BYTES_X0 : C::LDS_BYTES];
     _Float16* const AH = reinterpret_cast<_Float16*>(lds + C::OFF_AH);
     _Float16* const AL = reinterpret_cast<_Float16*>(lds + C::OFF_AL);
     int* const REXP = reinterpret_cast<int*>(lds + C::OFF_REXP);
@@ -676,7 +693,9 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         const int64_t t0 = rb + tt * C::BM;
         const int pc = pp * C::NW + wave;
         unsigned char* const X = lds + C::OFF_X + q * C::X_BYTES;
-        if (t0 + C::BM <= re) {
+        if constexpr ((MODE & 2) != 0) {
+            wdma(g_win_zero_row + 4 * (lane & 31), wlds(X + pc * 1024));
+        } else if (t0 + C::BM <= re) {
             wdma_s(x + t0 * ldx, xoff[pp], wlds(X + pc * 1024));
         } else {
             int l = lane;
@@ -705,8 +724,87 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         wdma(src, wlds(lds + C::OFF_EXT + (wave * C::EPW + i * C::RPP) * C::ROWB));
     };
 
+    // ---- codes form (X0): layer 1 straight from layer 0's row codes.  Layer
+    // 0 of the GCN stack is relu(coef . (c_i, C_i, s_i, 1)) per feature
+    // (gcn_layer0.hip); mignn_gcn_layer0_codes writes the 32-B code (c, C, s,
+    // 0) of a row instead of its 512-B row, and this kernel expands the rows
+    // it needs into its LDS slots with the same fma chain (bitwise the rows
+    // layer 0 would have written).  Per step a wave DMAs the codes of its 8
+    // own rows of tile s + 2 (lanes 0..15) and of its 4 ext rows of step s + 1
+    // (lanes 16..23, from the records in TAB slot q) into its CODE area and,
+    // after the MFMAs, expands them into slot (s + 2) % 3 and the ext area.
+    auto code_dma = [&](int64_t t, int q, bool ext) {
+        if (lane < (ext ? 24 : 16)) {
+            int l = lane;
+            asm volatile("" : "+v"(l));
+            int64_t row;
+            if (l < 16) {
+                const int64_t tt = t >= 0 ? t : 0;
+                row = rb + tt * C::BM + C::RPW * wave + (l >> 1);
+                if (row >= re) row = re - 1;
+            } else {
+                const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::RPW * kWRec;
+                row = *reinterpret_cast<const uint32_t*>(tab + 4 * ((l - 16) >> 1));
+            }
+            wdma(x + row * ldx + 4 * (l & 1), wlds(lds + C::OFF_CODE + wave * C::CODE_W));
+        }
+    };
+    // (COEF: the table k-major per 16-B feature chunk -- chunk c, input k
+    // (7: the constant) -> features 4c .. 4c + 3 in one f32x4: per feature
+    // the fma sequence of gcn_layer0.hip, which the compiler packs in pairs)
+    auto expand4 = [&](const f32x4 (&cf)[8], const float (&v)[7]) -> f32x4 {
+        f32x4 t = cf[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[q] = fmaf(cf[k][q], v[k], t[q]);
+        return f32x4{relu_nan(t[0]), relu_nan(t[1]), relu_nan(t[2]), relu_nan(t[3])};
+    };
+    // one row of a wave's codes (r: 0..7 own, 8..11 ext) -> the lane's 4
+    // features (16-B chunk lane & 31) of LDS row `dst` (chunk swizzle sw)
+    auto expand_row = [&](const f32x4 (&cf)[8], int r, unsigned char* dst, int sw) {
+        const unsigned char* const cp = lds + C::OFF_CODE + wave * C::CODE_W + r * C::CODEB;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(cp);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(cp + 16);
+        const float v[7] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2]};
+        const int ch = lane & 31;
+        *reinterpret_cast<f32x4*>(dst + ((ch ^ sw) << 4)) = expand4(cf, v);
+    };
+    auto coef_load = [&](f32x4 (&cf)[8]) {
+        const int ch = lane & 31;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            cf[k] = *reinterpret_cast<const f32x4*>(lds + C::OFF_COEF + (ch * 8 + k) * 16);
+    };
+    // the lane's i-th row of the wave's expansion: i < 4 own row 2 i + (lane
+    // >> 5) of the wave into X slot `slot`, else ext row 2 (i - 4) + (lane >> 5)
+    constexpr int NXR = C::RPW / 2 + C::EPW / 2;
+    auto expand_i = [&](const f32x4 (&cf)[8], int slot, int i) {
+        const int hh = lane >> 5;
+        if (i < C::RPW / 2) {
+            const int r = 2 * i + hh, o = C::RPW * wave + r;
+            expand_row(cf, r, lds + C::OFF_X + slot * C::X_BYTES + o * C::ROWB, o & 7);
+        } else {
+            const int r = 2 * (i - C::RPW / 2) + hh, k = C::EPW * wave + r;
+            expand_row(cf, C::RPW + r, lds + C::OFF_EXT + k * C::ROWB, k & 7);
+        }
+    };
+    auto expand = [&](int slot, bool ext) {
+        f32x4 cf[8];
+        coef_load(cf);
+#pragma unroll
+        for (int i = 0; i < NXR; ++i)
+            if (ext || i < C::RPW / 2) expand_i(cf, slot, i);
+    };
+
     // ------------------------------------------------------------ prologue
     for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
+    if constexpr (X0)
+        for (int i = tid; i < H * 2; i += C::NT) {   // i = chunk * 8 + k
+            const int c4 = i >> 3, k = i & 7;
+            const float* const src = xcoef + 4 * c4 * 8 + k;
+            *reinterpret_cast<f32x4*>(lds + C::OFF_COEF + 16 * i) = f32x4{src[0], src[8], src[16], src[24]};
+        }
     const int rr0 = lane & 15, gg0 = lane >> 4;
     constexpr int CPW = MIGNN_WIN_CPW;            // 16-column blocks per wave
     constexpr int WN = H / 16 / CPW, WM = C::NW / WN, IBW = (C::BM / 16) / WM;
@@ -751,14 +849,24 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     const bool has_res = (flags & MIGNN_EPI_RESIDUAL) != 0;
 
     // records and rows of steps 0 and 1, then step 0's ext rows
-    dma_tab(tile_of(0), 0);
+    if constexpr (X0) {
+        dma_tab(tile_of(0), 0);
+        dma_tab(tile_of(1), 1);
+        code_dma(tile_of(0), 0, false);
+        wbar<wvm(0) & kWLgkm0>();                 // (all waves), zero row, EPI, COEF
+        expand(0, false);
+        wwait<kWLgkm0>();                         // CODE read before it is refilled
+        code_dma(tile_of(1), 0, true);
+        wwait<wvm(0)>();
+        expand(1, true);
+    } else {
+        dma_tab(tile_of(0), 0);
 #pragma unroll
-    for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(0), 0, pp);
-    dma_tab(tile_of(1), 1);
+        for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(0), 0, pp);
+        dma_tab(tile_of(1), 1);
 #pragma unroll
-    for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(1), 1, pp);
-    wbar<wvm(0) & kWLgkm0>();                     // (all waves), zero row, EPI
-    {
+        for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(1), 1, pp);
+        wbar<wvm(0) & kWLgkm0>();                 // (all waves), zero row, EPI
         const unsigned char* es[C::NPE];
 #pragma unroll
         for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(0, i, true);
@@ -807,7 +915,17 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         //      s + 1, the own rows of tile s + 2, the last step's stores
         wtr.flush(wave, s - 1);
         wtr.stamp(0);
-        if (s == 0) wbar<wvm(0) & kWLgkm0>();
+        // (codes form: every row of the step was expanded by a ds_write of
+        // the last step -- nothing to wait for but LDS)
+        if constexpr (X0) {
+            // (codes form: also the records of step s + 1 -- the ext list of
+            // the codes DMA'd below; younger only the last step's stores)
+            if (s < 2) wbar<wvm(0) & kWLgkm0>();
+            else wbar<wvm(C::NST) & kWLgkm0>();
+            // this step's codes: own rows of tile s + 2, ext rows of step s + 1
+            // (landing under phase A; expanded between the transform's MFMAs)
+            code_dma(nx2, tq ^ 1, true);
+        } else if (s == 0) wbar<wvm(0) & kWLgkm0>();
         else if (s == 1) wbar<wvm(1 + C::NPX) & kWLgkm0>();
         else wbar<wvm(1 + C::NPX + C::NST) & kWLgkm0>();
 
@@ -900,6 +1018,41 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                                 const bool v = e + k < ee;
                                 cj[k] = v ? col[e + k] : -1;
                                 wj[k] = v ? ew[e + k] : 0.f;
+                            }
+                            if constexpr (X0) {
+                                // codes form: one entry at a time (registers), rows
+                                // outside the tile expanded from their codes
+#pragma unroll 1
+                                for (int k = 0; k < 4; ++k) {
+                                    if (cj[k] < 0) continue;
+                                    f32x4 vk[C::CH];
+                                    const int64_t off = static_cast<int64_t>(cj[k]) - t0;
+                                    if (off >= 0 && off < nloc) {
+                                        const uint32_t o = static_cast<uint32_t>(off);
+                                        const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
+#pragma unroll
+                                        for (int j = 0; j < C::CH; ++j)
+                                            vk[j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+                                    } else {
+                                        const float* cp = x + static_cast<int64_t>(cj[k]) * ldx;
+                                        const float4 v0 = ld4(cp), v1 = ld4(cp + 4);
+                                        const float v[7] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z};
+#pragma unroll 1
+                                        for (int j = 0; j < C::CH; ++j) {
+                                            f32x4 cf[8];
+#pragma unroll
+                                            for (int q = 0; q < 8; ++q)
+                                                cf[q] = *reinterpret_cast<const f32x4*>(
+                                                    lds + C::OFF_COEF + ((c0 + 16 * j) * 8 + q) * 16);
+                                            vk[j] = expand4(cf, v);
+                                        }
+                                    }
+#pragma unroll
+                                    for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                                        for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vk[j][r], accn[qd][j][r]);
+                                }
+                                continue;
                             }
                             f32x4 vv[4][C::CH];
 #pragma unroll
@@ -1007,21 +1160,29 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         wtr.stamp(4);
         // the records of step s + 1 landed (younger: the own rows of tile s + 1
         // and the last step's stores)
-        if (s == 0) wwait<wvm(0)>();
+        // (codes form: waited at B0)
+        if constexpr (X0) {
+        } else if (s == 0) wwait<wvm(0)>();
         else if (s == 1) wwait<wvm(C::NPX)>();
         else wwait<wvm(C::NPX + C::NST)>();
         const int64_t tn1 = nx1, tn2 = nx2;
         const unsigned char* es[C::NPE];
+        if constexpr (!X0)
 #pragma unroll
-        for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
+            for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
         // DMA piece q of this step: ext rows of step s + 1, the records of step
-        // s + 2 (into this step's TAB slot), the own rows of tile s + 2
+        // s + 2 (into this step's TAB slot), the own rows of tile s + 2 (codes
+        // form: the codes of those ext and own rows, then the records)
         auto dma_piece = [&](int q) {
-            if (q < C::NPE) ext_dma(q, es[q]);
-            else if (q == C::NPE) dma_tab(tn2, tq);
-            else dma_own(tn2, xn2, q - C::NPE - 1);
+            if constexpr (X0) {
+                dma_tab(tn2, tq);
+            } else {
+                if (q < C::NPE) ext_dma(q, es[q]);
+                else if (q == C::NPE) dma_tab(tn2, tq);
+                else dma_own(tn2, xn2, q - C::NPE - 1);
+            }
         };
-        constexpr int NPC = C::NPE + 1 + C::NPX;
+        constexpr int NPC = X0 ? 1 : C::NPE + 1 + C::NPX;
 
         if (prv >= 0) {
             if constexpr (AGG) {
@@ -1060,14 +1221,27 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         bl = *reinterpret_cast<const f16x8w*>(&AL[ao]);
                     };
                     __builtin_amdgcn_sched_barrier(0);
-                    constexpr int PD = MIGNN_WIN_PD, NF = PD + 1, NTT = C::KC * IBW;
+                    constexpr int PD = X0 ? MIGNN_WIN_PD_X0 : MIGNN_WIN_PD, NF = PD + 1, NTT = C::KC * IBW;
                     f16x8w fh[NF], fl[NF];
 #pragma unroll
                     for (int t = 0; t < PD && t < NTT; ++t) frag(t, fh[t], fl[t]);
+                    // codes form: the expansion rows between the MFMAs, one
+                    // every XS t-steps from t = XT (the codes DMA'd at B0)
+                    constexpr int XT = 2, XS = 2;
+                    static_assert(!X0 || XT + XS * (NXR - 1) < NTT, "expansion inside the transform");
+                    f32x4 xcf[X0 ? 8 : 1];
 #pragma unroll
                     for (int t = 0; t < NTT; ++t) {
                         const int kc = t / IBW, ib = t % IBW;
                         if (t < NPC) dma_piece(t);
+                        if constexpr (X0) {
+                            if (t == XT) {
+                                wwait<wvm(1)>();      // this wave's codes (the records younger)
+                                coef_load(xcf);
+                            }
+                            if (t >= XT && (t - XT) % XS == 0 && (t - XT) / XS < NXR)
+                                expand_i(xcf, xn2, (t - XT) / XS);
+                        }
                         if (MODE & 4) continue;
                         if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
 #pragma unroll
@@ -1155,6 +1329,10 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         } else {
 #pragma unroll
             for (int q = 0; q < NPC; ++q) dma_piece(q);
+            if constexpr (X0) {
+                wwait<wvm(1)>();
+                expand(xn2, true);
+            }
         }
         // carry tile s into phase B
 #pragma unroll
@@ -1194,7 +1372,7 @@ __device__ __forceinline__ uint32_t wrow4_max(uint32_t m) {
 //   over the row's 4 lanes), 24 MFMAs 16x16x32 f16 (W split in registers),
 //   epilogue, the wave's 16 rows staged in its own LDS region, whole-row
 //   stores.
-// MODE: 32 aggregate only; diag 1 ext rows from the zero row, 4 no MFMAs.
+// MODE: 32 aggregate only; diag 1 ext / 2 own rows from the zero row, 4 no MFMAs.
 template <int MODE = 0, int EPIF = -1>
 __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
     const unsigned char* __restrict__ plan, const int32_t* __restrict__ row_ptr,
@@ -1275,7 +1453,9 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         const int64_t t0 = rb + tt * C::BM;
         const int pc = pp * C::NW + wave;
         unsigned char* const X = lds + C::OFF_X + q * C::X_BYTES;
-        if (t0 + C::BM <= re) {
+        if constexpr ((MODE & 2) != 0) {
+            wdma(g_win_zero_row + 4 * (lane & 15), wlds(X + pc * 1024));
+        } else if (t0 + C::BM <= re) {
             wdma_s(x + t0 * ldx, xoff[pp], wlds(X + pc * 1024));
         } else {
             int l = lane;
@@ -1628,7 +1808,7 @@ template <int H, int MODE, int EPIF>
 void launch_win_k(int G, hipStream_t st, const void* plan, const int32_t* row_ptr,
                   const int32_t* col, const float* ew, const float* x, int64_t ldx, int64_t rb,
                   int64_t re, const float* w, const float* bias, const float* scale,
-                  const float* shift, int flags, float* out, int64_t ldo) {
+                  const float* shift, int flags, float* out, int64_t ldo, const float* xcoef) {
     if constexpr (H == 64)
         hipLaunchKernelGGL((gcn_win64_kernel<MODE, EPIF>), dim3(G), dim3(WCfg<64>::NT), 0, st,
                            static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb, re, w,
@@ -1636,36 +1816,37 @@ void launch_win_k(int G, hipStream_t st, const void* plan, const int32_t* row_pt
     else
         hipLaunchKernelGGL((gcn_win_kernel<H, MODE, EPIF>), dim3(G), dim3(WCfg<H>::NT), 0, st,
                            static_cast<const unsigned char*>(plan), row_ptr, col, ew, x, ldx, rb, re, w,
-                           bias, scale, shift, flags, out, ldo);
+                           bias, scale, shift, flags, out, ldo, xcoef);
 }
 
 template <int H, int MODE>
 void launch_win_h(int G, hipStream_t st, const void* plan, const int32_t* row_ptr,
                   const int32_t* col, const float* ew, const float* x, int64_t ldx, int64_t rb,
                   int64_t re, const float* w, const float* bias, const float* scale,
-                  const float* shift, int flags, float* out, int64_t ldo) {
+                  const float* shift, int flags, float* out, int64_t ldo, const float* xcoef) {
     constexpr int kBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_AFFINE | MIGNN_EPI_RELU;
     constexpr int kNoBN = MIGNN_EPI_BIAS | MIGNN_EPI_RESIDUAL | MIGNN_EPI_RELU;
-    if (MODE == 0 && flags == kBN)
-        launch_win_k<H, MODE, kBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
-    else if (MODE == 0 && flags == kNoBN)
-        launch_win_k<H, MODE, kNoBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+    constexpr bool EPIC = MODE == 0 || MODE == 64;   // the product modes: flags at compile time
+    if (EPIC && flags == kBN)
+        launch_win_k<H, MODE, kBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, xcoef);
+    else if (EPIC && flags == kNoBN)
+        launch_win_k<H, MODE, kNoBN>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, xcoef);
     else
-        launch_win_k<H, MODE, -1>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+        launch_win_k<H, MODE, -1>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, xcoef);
 }
 
 template <int MODE = 0>
 int launch_win(int h, const void* plan, const int32_t* row_ptr, const int32_t* col,
                const float* ew, const float* x, int64_t ldx, int64_t rb, int64_t re,
                const float* w, const float* bias, const float* scale, const float* shift,
-               int flags, float* out, int64_t ldo, hipStream_t st) {
+               int flags, float* out, int64_t ldo, hipStream_t st, const float* xcoef = nullptr) {
     const int64_t ntiles = (re - rb + 63) / 64;
     const int G = win_grid(ntiles, h == 128 ? WCfg<128>::WGPC : WCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_win: device query failed");
     if (h == 128)
-        launch_win_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
-    else
-        launch_win_h<64, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
+        launch_win_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, xcoef);
+    else if constexpr ((MODE & 64) == 0)
+        launch_win_h<64, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, xcoef);
     return launch_status("gcn_win_kernel");
 }
 
@@ -1741,6 +1922,29 @@ extern "C" int mignn_gcn_layer_win(const void* plan, const int32_t* row_ptr, con
                       ldo, as_stream(stream));
 }
 
+extern "C" int mignn_gcn_layer_win_codes(const void* plan, const int32_t* row_ptr,
+                                         const int32_t* col, const float* ew, const float* codes,
+                                         int64_t ldc, int64_t rb, int64_t re, int h,
+                                         const float* xcoef, const float* w, const float* bias,
+                                         const float* scale, const float* shift, int flags,
+                                         float* out, int64_t ldo, void* stream) {
+    MIGNN_REQUIRE(plan && row_ptr && col && ew && codes && xcoef && w && out,
+                  "gcn_layer_win_codes: null pointer");
+    MIGNN_REQUIRE(h == 128, "gcn_layer_win_codes: h must be 128 (got %d)", h);
+    MIGNN_REQUIRE(aligned16(codes) && aligned16(out) && aligned16(plan) && aligned16(w) &&
+                      aligned16(xcoef),
+                  "gcn_layer_win_codes: unaligned");
+    MIGNN_REQUIRE(ldc % 4 == 0 && ldc >= 8 && ldo % 4 == 0 && ldo >= h,
+                  "gcn_layer_win_codes: bad strides");
+    MIGNN_REQUIRE(rb >= 0 && re >= rb, "gcn_layer_win_codes: bad row range");
+    MIGNN_REQUIRE((flags & ~MIGNN_EPI_MASK) == 0, "gcn_layer_win_codes: unknown flags 0x%x", flags);
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_BIAS) || bias, "gcn_layer_win_codes: bias");
+    MIGNN_REQUIRE(!(flags & MIGNN_EPI_AFFINE) || (scale && shift), "gcn_layer_win_codes: affine");
+    if (re == rb) return MIGNN_OK;
+    return launch_win<64>(h, plan, row_ptr, col, ew, codes, ldc, rb, re, w, bias, scale, shift,
+                          flags, out, ldo, as_stream(stream), xcoef);
+}
+
 extern "C" int mignn_gcn_aggregate_win(const void* plan, const int32_t* row_ptr, const int32_t* col,
                                        const float* ew, const float* x, int64_t ldx, int64_t rb,
                                        int64_t re, int h, float* out, int64_t ldo, void* stream) {
@@ -1768,6 +1972,8 @@ extern "C" int mignn_diag_win(int mode, const void* plan, const int32_t* row_ptr
     switch (mode) {
         case 0: return launch_win<0>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
         case 1: return launch_win<1>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        case 2: return launch_win<2>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
+        case 3: return launch_win<3>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
         case 4: return launch_win<4>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
         case 32: return launch_win<32>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);
         case 33: return launch_win<33>(h, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, st);

@@ -14,7 +14,8 @@
 //   K2 csr_scatter  : kept edge e -> slot row_ptr0[key] + (atomic fill index),
 //                     (edge index, value) stored there; a run of equal keys in
 //                     a wave takes consecutive slots with one atomic -- slot
-//                     order within a row is otherwise arbitrary here...
+//                     order within a row is otherwise arbitrary here; the
+//                     gcn_norm weight of each entry (ew) is written with it...
 //   K3 csr_finalize : ...and restored per row by sorting on the edge index
 //                     (already sorted: skipped; <= 16 entries: a register
 //                     network; longer: in memory): in-row order == edge order,
@@ -34,6 +35,11 @@
 #include <cstring>
 
 #include "common.hpp"
+
+// gcn_norm weights written by csr_scatter (1) or per row by csr_finalize (0)
+#ifndef MIGNN_CSR_EW_SCATTER
+#define MIGNN_CSR_EW_SCATTER 0
+#endif
 
 namespace mignn {
 
@@ -141,18 +147,24 @@ __global__ void csr_count_kernel(const int64_t* __restrict__ ei, int64_t E, int6
 // + key in ONE_SELF_LOOP mode: every earlier row gains its self-loop); a run
 // of equal keys takes consecutive slots in edge order with one atomic, so a
 // row filled by ONE run is in edge order already -- rows filled by several
-// runs are flagged for csr_finalize's sort
+// runs are flagged for csr_finalize's sort, and only their entries record
+// the edge index (slot_eid) the sort keys on.  ew (optional): the entry's
+// gcn_norm weight (deg_j + 1)^-1/2 (deg_i + 1)^-1/2 from the kept-edge
+// counts, in csr_finalize's former per-row form (bitwise the same); a
+// flagged row's weights are rewritten after its sort.
 __global__ void csr_scatter_kernel(const uint32_t* __restrict__ keys,
                                    const int32_t* __restrict__ vals, int64_t E, int64_t N,
                                    int one_loop, const int32_t* __restrict__ row_ptr0,
+                                   const int32_t* __restrict__ deg,
                                    int32_t* __restrict__ fill, int32_t* __restrict__ slot_eid,
-                                   int32_t* __restrict__ col, uint8_t* __restrict__ unsorted) {
+                                   int32_t* __restrict__ col, float* __restrict__ ew,
+                                   uint8_t* __restrict__ unsorted) {
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     constexpr int kU = 4;   // edges per lane per trip, loads issued together (as csr_count)
     for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < E; base += kU * stride) {
         uint32_t kk[kU];
-        int32_t vv[kU], b0[kU], b1[kU];
+        int32_t vv[kU], b0[kU], b1[kU], dj[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int64_t e = base + u * stride + threadIdx.x;
@@ -165,6 +177,7 @@ __global__ void csr_scatter_kernel(const uint32_t* __restrict__ keys,
             const bool keep = kk[u] < static_cast<uint32_t>(N);
             b0[u] = keep ? row_ptr0[kk[u]] : 0;
             b1[u] = keep ? row_ptr0[kk[u] + 1] : 0;
+            dj[u] = (MIGNN_CSR_EW_SCATTER && keep && ew != nullptr) ? deg[vv[u]] : 0;
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -180,14 +193,19 @@ __global__ void csr_scatter_kernel(const uint32_t* __restrict__ keys,
             pos0 = __shfl(pos0, hl);
             if (keep) {
                 const int32_t pos = pos0 + (lane - hl);
-                slot_eid[pos] = static_cast<int32_t>(e);
-                col[pos + (one_loop ? static_cast<int32_t>(k) : 0)] = vv[u];
+                const int32_t off = one_loop ? static_cast<int32_t>(k) : 0;
+                if (rl != b1[u] - b0[u]) slot_eid[pos] = static_cast<int32_t>(e);
+                col[pos + off] = vv[u];
+                if (MIGNN_CSR_EW_SCATTER && ew != nullptr)
+                    ew[pos + off] = 1.0f / sqrtf(static_cast<float>(dj[u] + 1)) *
+                                    (1.0f / sqrtf(static_cast<float>(b1[u] - b0[u] + 1)));
             }
         }
     }
 }
 
-// in-place sort of (eid, val)[b, e) by eid (distinct).  Short rows (the mesh
+// in-place sort of (eid, val)[b, e) by eid (distinct) -- or, when the ids are
+// one contiguous range, val placed by id (eid left as is).  Short rows (the mesh
 // case) in registers by an odd-even transposition network over 16 slots;
 // longer rows by insertion sort (<= 64) or heap sort in memory.
 __device__ void sort_row(int32_t* __restrict__ ke, int32_t* __restrict__ kv, int b, int e) {
@@ -196,10 +214,21 @@ __device__ void sort_row(int32_t* __restrict__ ke, int32_t* __restrict__ kv, int
     if (n <= 1) return;
     if (n <= 16) {
         int32_t K[16], V[16];
+        int32_t mn = 0x7fffffff, mx = -1;
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             K[t] = t < n ? ke[b + t] : 0x7fffffff;
             V[t] = t < n ? kv[b + t] : 0;
+            if (t < n) { mn = min(mn, K[t]); mx = max(mx, K[t]); }
+        }
+        // the row's edges one contiguous range of the edge list (a mesh row
+        // split over two waves' runs): entry t belongs at K[t] - mn -- placed
+        // directly (its slot_eid is not read again)
+        if (mx - mn + 1 == n) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                if (t < n) kv[b + K[t] - mn] = V[t];
+            return;
         }
 #pragma unroll
         for (int round = 0; round < 16; ++round) {
@@ -289,10 +318,11 @@ __global__ void csr_finalize_kernel(const int32_t* __restrict__ row_ptr0,
             const float di = 1.0f / sqrtf(static_cast<float>(e - b + 1));
             if (dinv) dinv[i] = di;
             if (ew) {
-                for (int32_t t = b + off; t < e + off; ++t) {
-                    const int32_t j = col[t];
-                    ew[t] = 1.0f / sqrtf(static_cast<float>(row_ptr0[j + 1] - row_ptr0[j] + 1)) * di;
-                }
+                if (unsorted[i] || !MIGNN_CSR_EW_SCATTER)   // (csr_scatter's: in the sorted order)
+                    for (int32_t t = b + off; t < e + off; ++t) {
+                        const int32_t j = col[t];
+                        ew[t] = 1.0f / sqrtf(static_cast<float>(row_ptr0[j + 1] - row_ptr0[j] + 1)) * di;
+                    }
                 ew[e + off] = di * di;
             }
         }
@@ -500,7 +530,7 @@ extern "C" int mignn_csr_build_gcn(const int64_t* edge_index, int64_t E, int64_t
     if (E > 0) {
         hipLaunchKernelGGL(csr_scatter_kernel, dim3(grid_for(E, kBlock, 8192)), dim3(kBlock), 0,
                            st, keys, vals, E, N, mode == MIGNN_CSR_ONE_SELF_LOOP ? 1 : 0, row_ptr0,
-                           fill, slot_eid, col, unsorted);
+                           deg, fill, slot_eid, col, ew, unsorted);
         if ((rc = launch_status("csr_scatter_kernel"))) return rc;
     }
     hipLaunchKernelGGL(csr_finalize_kernel, dim3(grid_for(N + 1, kBlock, 65536)), dim3(kBlock), 0,

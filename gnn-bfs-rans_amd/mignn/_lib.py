@@ -16,7 +16,10 @@ from ctypes import c_float, c_int, c_int64, c_size_t, c_void_p
 import torch  # noqa: F401  (must precede loading libmignn.so)
 
 LIB_NAME = "libmignn.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# (MIGNN_LIB_VARIANT: a variant build of the same library for A/B timing
+# studies -- scripts only; the product loads the in-tree build)
+LIB_PATH = os.environ.get("MIGNN_LIB_VARIANT") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 EPI_BIAS, EPI_RESIDUAL, EPI_AFFINE, EPI_RELU = 1, 2, 4, 8
 CSR_VERBATIM, CSR_ONE_SELF_LOOP, CSR_TRANSPOSE = 0, 1, 4
@@ -75,6 +78,8 @@ SIGNATURES = {
     "mignn_gcn_win_plan": (c_int, [_P, _P, _P, c_int64, c_int64, c_int, _P, _P, c_size_t, _P, _P]),
     "mignn_gcn_layer_win": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P,
                                     _P, _P, c_int, _P, c_int64, _P]),
+    "mignn_gcn_layer_win_codes": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int,
+                                          _P, _P, _P, _P, _P, c_int, _P, c_int64, _P]),
     "mignn_gcn_aggregate_win": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int,
                                         _P, c_int64, _P]),
     "mignn_mlp_head_prep_bytes": (c_size_t, [c_int]),
@@ -92,6 +97,8 @@ SIGNATURES = {
                                           c_size_t, _P]),
     "mignn_gcn_layer0_coords": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,
                                         c_int, _P, c_int64, _P]),
+    "mignn_gcn_layer0_codes": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,
+                                       c_int64, _P]),
     "mignn_mesh_graph_scratch_bytes": (c_size_t, [c_int64, c_int64]),
     "mignn_mesh_graph_count": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, _P, c_int64, c_int,
                                        _P, _P, c_size_t, _P]),

@@ -472,6 +472,9 @@ class FlowGNN(nn.Module):
         #   fused256        H = 256 fused layer / head kernels: "1", "0",
         #                   "layer" or "head" (MIGNN_FUSED256)
         self.fuse_layer0 = os.environ.get("MIGNN_FUSE_LAYER0", "1") == "1"
+        #   gcn_codes       GCN H = 128 on the window kernel: layer 0 writes 32-B
+        #                   row codes and layer 1 expands them (MIGNN_GCN_CODES)
+        self.gcn_codes = os.environ.get("MIGNN_GCN_CODES", "1") == "1"
         # after every eval forward, read the device's sticky in-kernel error word
         # and raise if a bounded wait ran out (costs a device sync; off by
         # default -- bench.py and the tests check it themselves)
@@ -521,7 +524,15 @@ class FlowGNN(nn.Module):
         cur, nxt = buf_a, buf_b
         first = 0
         kind = self._layer0_kind(edge_attr)
-        if kind is not None:
+        if kind == "gcn" and self._use_gcn_codes(csr):
+            # layers 0 and 1 through the row codes: layer 0's [N, H] rows are
+            # never written (mignn_gcn_layer0_codes + mignn_gcn_layer_win_codes)
+            try:
+                self._gcn_layers01_codes(csr, self._coords(xin, csr), num_nodes, cur)
+            except RuntimeError as e:
+                raise self._layer_error(0, e, num_nodes, edge_index, xin, edge_attr) from e
+            first = 2
+        elif kind is not None:
             # input_proj composed into layer 0, from the coordinates
             try:
                 self._layer0(kind, csr, self._coords(xin, csr), 0, num_nodes, cur)
@@ -944,6 +955,34 @@ class FlowGNN(nn.Module):
             _lib.ptr(csr.row_ptr), _lib.ptr(csr.col), _lib.ptr(csr.ew), _lib.ptr(pos),
             pos.stride(0), self.input_dim, rb, re, _lib.ptr(self._layer0_coef()), self.hidden_dim,
             _lib.ptr(out), out.stride(0), _stream(pos)), "mignn_gcn_layer0_coords")
+
+    def _use_gcn_codes(self, csr: Csr) -> bool:
+        """Layers 0 and 1 of a GCN stack through layer 0's row codes: the
+        window kernel at H = 128 on this CSR, 3-D coordinates, >= 2 layers."""
+        return (self.gcn_codes and self.layer_type == "GCN" and self.hidden_dim == 128
+                and self.input_dim == 3 and self.num_layers >= 2 and self.precision == "f16x3"
+                and self._gcn_kernel(128, csr) == "win")
+
+    def _gcn_layers01_codes(self, csr: Csr, pos, n: int, out):
+        """Layer 0 as row codes (c_i, C_i, s_i) [n, 8], then layer 1 by the
+        window kernel expanding every row it reads from them with layer 0's
+        coefficients -- the same rows, bitwise, without layer 0's [n, H]
+        write and layer 1's re-read of it."""
+        L = _lib.lib()
+        P = _lib.ptr
+        st = _stream(pos)
+        codes = torch.empty((n, 8), dtype=torch.float32, device=pos.device)
+        _lib.check(L.mignn_gcn_layer0_codes(P(csr.row_ptr), P(csr.col), P(csr.ew), P(pos),
+                                            pos.stride(0), self.input_dim, 0, n, P(codes), 8, st),
+                   "mignn_gcn_layer0_codes")
+        layer = self.gnn_layers[1]
+        scale, shift = self._bn(1)
+        epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
+        plan = csr.win_plan(128, 0, n)
+        _lib.check(L.mignn_gcn_layer_win_codes(
+            P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(codes), 8, 0, n, 128,
+            P(self._layer0_coef()), P(layer.lin.weight), P(layer.bias), P(scale), P(shift), epi,
+            P(out), out.stride(0), st), "mignn_gcn_layer_win_codes")
 
     def _gcn_kernel(self, H: int, csr: Optional["Csr"] = None) -> str:
         """The GCN layer kernel at width H; with `csr`: the kernel for that

@@ -342,6 +342,18 @@ int mignn_gcn_layer_win(const void* plan, const int32_t* row_ptr, const int32_t*
                         int64_t row_end, int h, const float* w, const float* bias,
                         const float* scale, const float* shift, int flags, float* out,
                         int64_t ldo, void* stream);
+/* Layer 1 of the GCN stack straight from layer 0's row codes (the codes
+ * form, h = 128): codes [rows, ldc >= 8] from mignn_gcn_layer0_codes (D = 3),
+ * xcoef = the [h][8] table mignn_gcn_layer0_coords takes for D = 3; the
+ * kernel expands every row it reads, x_j = relu(xcoef . (code_j, 1)) with
+ * layer 0's fma chain, so out equals mignn_gcn_layer_win over the rows
+ * mignn_gcn_layer0_coords would have written, bitwise.  Same plan. */
+int mignn_gcn_layer_win_codes(const void* plan, const int32_t* row_ptr, const int32_t* col,
+                              const float* ew, const float* codes, int64_t ldc,
+                              int64_t row_begin, int64_t row_end, int h, const float* xcoef,
+                              const float* w, const float* bias, const float* scale,
+                              const float* shift, int flags, float* out, int64_t ldo,
+                              void* stream);
 /* The GCN aggregation alone by the window kernel (same plan): out_i =
  * sum_e ew_e x_{col e}, fp32 (the SURVEY 8(d) "aggregate kernel alone"). */
 int mignn_gcn_aggregate_win(const void* plan, const int32_t* row_ptr, const int32_t* col,
@@ -380,6 +392,12 @@ int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* col, const fl
                             const float* pos, int64_t ldp, int in_dim, int64_t row_begin,
                             int64_t row_end, const float* coef, int h, float* out, int64_t ldo,
                             void* stream);
+/* Layer 0's row codes instead of its rows: codes_i = (c_i, C_i, s_i, 0...)
+ * (8 floats, in_dim 1..3; the values mignn_gcn_layer0_coords expands with
+ * its coefficients), rows row_begin..row_end at codes + i * ldc. */
+int mignn_gcn_layer0_codes(const int32_t* row_ptr, const int32_t* col, const float* ew,
+                           const float* pos, int64_t ldp, int in_dim, int64_t row_begin,
+                           int64_t row_end, float* codes, int64_t ldc, void* stream);
 
 /* Fused GIN layer (gnn_model.py:70-75, :166, :184-191), h in {64, 128}:
  *   tmp_i = relu(nn.0( sum_{j in row i} x_j + (1 + eps) x_i ))      (rows rb..re -> tmp[0..])

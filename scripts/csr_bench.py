@@ -1,7 +1,7 @@
 """Graph-setup timing on the bench mesh (250x200x200, 10M nodes): the column
 order and the CSR build (mignn_csr_build_gcn, relabelled) and the window
 plan, HIP events, median of 5; bitwise check of the CSR against a second
-build.  Prints one JSON object."""
+build.  CB_LIB: time a variant build instead.  Prints one JSON object."""
 import json
 import os
 import statistics
@@ -15,6 +15,11 @@ from mignn import _lib  # noqa: E402
 from mignn.gnn_model import build_csr, locality_order  # noqa: E402
 from mignn.synthetic import grid_graph  # noqa: E402
 
+if os.environ.get("CB_LIB"):   # a variant build of libmignn.so in place of the product
+    import ctypes
+    _h = ctypes.CDLL(os.environ["CB_LIB"])   # (an older build: the symbols it has)
+    _lib._lib = _lib._load(os.environ["CB_LIB"],
+                           {k: v for k, v in _lib.SIGNATURES.items() if hasattr(_h, k)})
 dev = torch.device("cuda", 0)
 pos, ei = grid_graph(250, 200, 200, device=dev)
 n = pos.shape[0]

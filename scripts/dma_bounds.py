@@ -4,7 +4,8 @@ destination ends inside the issuing kernel's static LDS allocation
 (MIGNN_DMA_BOUND, csrc/common.hpp; __builtin_amdgcn_groupstaticsize) and
 records a violation in its translation unit's word (mignn_diag_dma_oob_*).
 This runs the model forwards that reach every LDS-DMA kernel -- the window
-GCN kernels (H = 64: two workgroups per CU; 128), the ring kernel (H = 64: two
+GCN kernels (H = 64: two workgroups per CU; 128, with and without the
+row codes of layers 0 / 1), the ring kernel (H = 64: two
 per CU), the producer / consumer kernel, the fused GAT kernel (two 4-wave
 blocks per CU), the fused GIN and TransformerConv kernels and the split GEMM
 -- through the diag build, reads the five words, and compares every output
@@ -27,6 +28,7 @@ dev = torch.device("cuda", 0)
 UNITS = ("agg", "ring", "win", "pc", "gemm")
 CASES = [  # (layer type, hidden, GCN kernel, mesh)
     ("GCN", 64, "win", (64, 48, 40)), ("GCN", 128, "win", (64, 48, 40)),
+    ("GCN", 128, "win-rows", (64, 48, 40)),
     ("GCN", 64, "ring", (64, 48, 40)), ("GCN", 128, "pc", (64, 48, 40)),
     ("GAT", 128, "auto", (64, 48, 40)), ("GAT", 64, "auto", (64, 48, 40)),
     ("GIN", 256, "auto", (48, 40, 32)), ("Transformer", 256, "auto", (48, 40, 32)),
@@ -48,7 +50,8 @@ def forward(lt, H, kern, dims, use_diag):
     m.load_state_dict(seeded_state_dict(m.state_dict(), seed=11))
     m = m.to(dev).eval()
     m.reorder = "1"
-    m.gcn_kernel = kern
+    m.gcn_kernel = kern.split("-")[0]
+    m.gcn_codes = kern != "win-rows"     # win: layers 0 / 1 through the row codes
     x, ei = grid_graph(*dims, device=dev)
     with torch.no_grad():
         y = m(x, ei)

@@ -3,7 +3,7 @@ column order) against the producer / consumer kernel (mignn_gcn_layer_f16x3)
 and the ring kernel (mignn_gcn_layer_ring), both in the block order, on the
 bench mesh (250x200x200 periodic hex, 10M nodes); the aggregate alone of the
 window and ring kernels; the window plan build; window ablations
-(mignn_diag_win modes: 1 ext rows from the zero row, 4 no MFMAs, 33
+(mignn_diag_win modes: 1 ext rows from the zero row, 2 own rows from it, 3 both, 4 no MFMAs, 33
 aggregate with ext from the zero row).  HIP events on the launch stream,
 interleaved rounds, median.  Env: WB_H (comma list, 128,64), WB_GRID,
 WB_REPS, WB_MODES (comma list of diag modes), WB_OLD (0: skip pc / ring),

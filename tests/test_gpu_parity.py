@@ -93,6 +93,21 @@ def test_csr_build_bit_exact(mode):
         if mode == _lib.CSR_ONE_SELF_LOOP:
             deg = np.diff(rp)
             np.testing.assert_allclose(csr.dinv.cpu().numpy()[:n], 1 / np.sqrt(deg), rtol=2e-7)
+            _check_gcn_weights(csr, name)
+
+
+def _check_gcn_weights(csr, name):
+    """the build's ew (written by csr_scatter, rewritten after a split row's
+    sort) equals mignn_gcn_norm's dinv[col] * dinv[row] bitwise"""
+    nnz = int(csr.row_ptr[-1].item())
+    ew = csr.ew[:nnz].clone()
+    csr.compute_gcn_weights()
+    assert torch.equal(ew, csr.ew[:nnz]), name
+    rp = csr.row_ptr.cpu().numpy()
+    rows = np.repeat(np.arange(csr.num_nodes), np.diff(rp))
+    dinv = csr.dinv.cpu().numpy()[: csr.num_nodes].astype(np.float64)
+    want = dinv[csr.col[:nnz].cpu().numpy()] * dinv[rows]
+    np.testing.assert_allclose(ew.cpu().numpy(), want, rtol=1e-6, err_msg=name)
 
 
 @pytest.mark.parametrize("mode", [_lib.CSR_VERBATIM, _lib.CSR_ONE_SELF_LOOP])
@@ -114,6 +129,8 @@ def test_csr_build_relabeled_and_transposed(mode):
     rp, col = csr_np(ei.flip(0).numpy(), n, mode == _lib.CSR_ONE_SELF_LOOP)
     assert np.array_equal(csr_t.row_ptr.cpu().numpy(), rp)
     assert np.array_equal(csr_t.col[: rp[-1]].cpu().numpy(), col)
+    if mode == _lib.CSR_ONE_SELF_LOOP:
+        _check_gcn_weights(csr, "relabeled")
 
 
 # ------------------------------------------------------------------ dense transforms

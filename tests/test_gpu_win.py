@@ -294,3 +294,73 @@ def test_model_gcn_win_1m(H):
     ref = orc.flowgnn_forward(sd, cfg, x[nodes].cpu(), sub.cpu(), None, dtype=torch.float64)
     err = (ys["win"][seeds.to(DEV)].cpu().double() - ref[:24]).abs().max().item()
     assert err <= 1e-5 * scale, err
+
+
+def _layer0_rows_and_codes(csr, n, H, seed):
+    """Layer 0 both ways: its [n, H] rows (mignn_gcn_layer0_coords) and its
+    row codes (mignn_gcn_layer0_codes), from random 3-D positions and a
+    random [H][8] coefficient table."""
+    g = torch.Generator().manual_seed(seed)
+    pos = (torch.rand(n, 3, generator=g) * 4 - 1).to(DEV)
+    coef = (torch.randn(H, 8, generator=g) * 0.5).to(DEV)
+    L = _lib.lib()
+    rows = torch.full((n, H), float("nan"), device=DEV)
+    _lib.check(L.mignn_gcn_layer0_coords(P(csr.row_ptr), P(csr.col), P(csr.ew), P(pos), 3, 3, 0, n,
+                                         P(coef), H, P(rows), H, _lib.stream()), "layer0_coords")
+    codes = torch.full((n, 8), float("nan"), device=DEV)
+    _lib.check(L.mignn_gcn_layer0_codes(P(csr.row_ptr), P(csr.col), P(csr.ew), P(pos), 3, 3, 0, n,
+                                        P(codes), 8, _lib.stream()), "layer0_codes")
+    return rows, codes, coef
+
+
+@pytest.mark.parametrize("case,dims", [("cols", (64, 48, 40)), ("hub_cols", (64, 48, 40)),
+                                       ("shuffled", (40, 30, 20)), ("natural", (13, 11, 3)),
+                                       ("cols", (100, 100, 100))])
+def test_gcn_layer_win_codes(case, dims):
+    """The codes form (mignn_gcn_layer0_codes + mignn_gcn_layer_win_codes)
+    equals layer 0's rows through mignn_gcn_layer_win bitwise: in-window,
+    ext, next-tile and CSR-path entries (the hub / shuffled graphs) expanded
+    from codes, row ranges off tile boundaries, compile-time and run-time
+    epilogue flags, 1M rows (many steps per workgroup)."""
+    H = 128
+    csr, n, info = _graph(case, dims)
+    X, codes, coef = _layer0_rows_and_codes(csr, n, H, 11)
+    assert not torch.isnan(codes).any()
+    assert torch.equal(codes[:, 7], torch.zeros(n, device=DEV))
+    _, W, b, sc, sh = _weights(H, 23)
+    L = _lib.lib()
+    for rb, re in ((0, n), (37, n - 5)):
+        plan, stats = _plan(csr, rb, re, H, info if rb == 0 else None)
+        for flags in (15, 11, 3):
+            ref = torch.full((n, H), float("nan"), device=DEV)
+            _layer(csr, plan, X, H, rb, re, H, W, b, sc, sh, ref, flags=flags)
+            got = torch.full((n, H), float("nan"), device=DEV)
+            _lib.check(L.mignn_gcn_layer_win_codes(
+                P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(codes), 8, rb, re, H, P(coef),
+                P(W), P(b), P(sc), P(sh), flags, P(got), H, _lib.stream()), "win_codes")
+            assert torch.equal(got[rb:re], ref[rb:re]), (rb, re, flags,
+                                                         (got[rb:re] - ref[rb:re]).abs().max().item())
+            assert torch.isnan(got[:rb]).all() and torch.isnan(got[re:]).all()
+        if case in ("hub_cols", "shuffled") and rb == 0:
+            assert stats.tolist()[1] > 0          # CSR-path rows exercised
+
+
+def test_model_gcn_codes_bitwise():
+    """FlowGNN GCN H = 128 (window route): layers 0 and 1 through the row
+    codes give the same output, bitwise, as layer 0's rows written and read."""
+    from mignn import FlowGNN
+    from mignn.synthetic import seeded_state_dict
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, hidden_dim=128, num_layers=4,
+                layer_type="GCN")
+    m.load_state_dict(seeded_state_dict(m.state_dict(), seed=9))
+    m = m.to(DEV).eval()
+    m.reorder = "1"
+    x, ei = grid_graph(64, 48, 40, device=DEV)
+    ys = {}
+    for codes in (True, False):
+        m.gcn_codes = codes
+        with torch.no_grad():
+            ys[codes] = m(x, ei)
+        csr = next(iter(m._csr.entries.values()))
+        assert m._use_gcn_codes(csr) == codes
+    assert torch.equal(ys[True], ys[False])
