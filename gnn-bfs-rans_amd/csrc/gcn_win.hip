@@ -77,9 +77,14 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 #ifndef MIGNN_WIN_PD
 #define MIGNN_WIN_PD 5
 #endif
+// codes form: the row expansion as f32 MFMAs, every wave 16 features of
+// every row (1), or as fma chains on the VALU, every wave its own rows (0)
+#ifndef MIGNN_WIN_XMFMA
+#define MIGNN_WIN_XMFMA 1
+#endif
 // codes form: A-fragment prefetch depth (the expansion's registers beside it)
 #ifndef MIGNN_WIN_PD_X0
-#define MIGNN_WIN_PD_X0 3
+#define MIGNN_WIN_PD_X0 (MIGNN_WIN_XMFMA ? 5 : 3)
 #endif
 constexpr int kWRec = 48;                 // bytes per plan record: 8 u16 codes + 8 f32 weights
 constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the next-tile entry
@@ -770,7 +775,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         const int ch = lane & 31;
         *reinterpret_cast<f32x4*>(dst + ((ch ^ sw) << 4)) = expand4(cf, v);
     };
-    auto coef_load = [&](f32x4 (&cf)[8]) {
+    [[maybe_unused]] auto coef_load = [&](f32x4 (&cf)[8]) {
         const int ch = lane & 31;
 #pragma unroll
         for (int k = 0; k < 8; ++k)
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     // the lane's i-th row of the wave's expansion: i < 4 own row 2 i + (lane
     // >> 5) of the wave into X slot `slot`, else ext row 2 (i - 4) + (lane >> 5)
     constexpr int NXR = C::RPW / 2 + C::EPW / 2;
-    auto expand_i = [&](const f32x4 (&cf)[8], int slot, int i) {
+    [[maybe_unused]] auto expand_i = [&](const f32x4 (&cf)[8], int slot, int i) {
         const int hh = lane >> 5;
         if (i < C::RPW / 2) {
             const int r = 2 * i + hh, o = C::RPW * wave + r;
@@ -789,12 +794,60 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             expand_row(cf, C::RPW + r, lds + C::OFF_EXT + k * C::ROWB, k & 7);
         }
     };
-    auto expand = [&](int slot, bool ext) {
+    [[maybe_unused]] auto expand = [&](int slot, bool ext) {
         f32x4 cf[8];
         coef_load(cf);
 #pragma unroll
         for (int i = 0; i < NXR; ++i)
             if (ext || i < C::RPW / 2) expand_i(cf, slot, i);
+    };
+    // ---- the expansion as f32 MFMAs (MIGNN_WIN_XMFMA): wave w computes
+    // features 16 w .. 16 w + 15 of every expanded row, a 16-row block per
+    // v_mfma_f32_16x16x4_f32 pair (inputs 0..3, then 4..6 and a zero; the
+    // accumulator starts at the constant e) -- on gfx950 an exact fma chain
+    // in k order, i.e. layer 0's chain -- off the VALU.  Lane l: A = the
+    // coefficient of feature 16 w + (l & 15), input 4 kg + (l >> 4); B =
+    // input 4 kg + (l >> 4) of row l & 15's code; D = features 16 w + 4 (l
+    // >> 4) .. + 3 of row l & 15 (one 16-B chunk).  Row blocks 0..3: the
+    // tile's own rows (CODE of wave j >> 3, row j & 7), 4, 5: its ext rows
+    // (wave k >> 2, row RPW + (k & 3)) -- every wave reads every wave's codes.
+    [[maybe_unused]] constexpr int NXB = (C::BM + C::KX) / 16;
+    float xa0 = 0.f, xa1 = 0.f;
+    f32x4 xe = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (X0 && MIGNN_WIN_XMFMA) {
+        const int f = 16 * wave + (lane & 15), kq = lane >> 4;
+        xa0 = xcoef[f * 8 + kq];
+        xa1 = kq < 3 ? xcoef[f * 8 + 4 + kq] : 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) xe[v] = xcoef[(16 * wave + 4 * kq + v) * 8 + 7];
+    }
+    [[maybe_unused]] auto xblock_mfma = [&](int rbk) -> f32x4 {
+        const int l16 = lane & 15, kq = lane >> 4;
+        uint32_t off;
+        if (rbk < C::BM / 16) {
+            const int j = 16 * rbk + l16;
+            off = (j >> 3) * C::CODE_W + (j & 7) * C::CODEB;
+        } else {
+            const int k = 16 * (rbk - C::BM / 16) + l16;
+            off = (k >> 2) * C::CODE_W + (C::RPW + (k & 3)) * C::CODEB;
+        }
+        const float* const cp = reinterpret_cast<const float*>(lds + C::OFF_CODE + off);
+        const float b0 = cp[kq], b1 = cp[4 + kq];
+        const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(xa0, b0, xe, 0, 0, 0);
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(xa1, b1, d, 0, 0, 0);
+    };
+    [[maybe_unused]] auto xblock_store = [&](int slot, int rbk, const f32x4& d) {
+        const int l16 = lane & 15, ch = 4 * wave + (lane >> 4);
+        const f32x4 o = f32x4{relu_nan(d[0]), relu_nan(d[1]), relu_nan(d[2]), relu_nan(d[3])};
+        unsigned char* dst;
+        if (rbk < C::BM / 16) {
+            const int r = 16 * rbk + l16;
+            dst = lds + C::OFF_X + slot * C::X_BYTES + r * C::ROWB + ((ch ^ (r & 7)) << 4);
+        } else {
+            const int k = 16 * (rbk - C::BM / 16) + l16;
+            dst = lds + C::OFF_EXT + k * C::ROWB + ((ch ^ (k & 7)) << 4);
+        }
+        *reinterpret_cast<f32x4*>(dst) = o;
     };
 
     // ------------------------------------------------------------ prologue
@@ -854,11 +907,21 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         dma_tab(tile_of(1), 1);
         code_dma(tile_of(0), 0, false);
         wbar<wvm(0) & kWLgkm0>();                 // (all waves), zero row, EPI, COEF
+#if MIGNN_WIN_XMFMA
+#pragma unroll
+        for (int rbk = 0; rbk < C::BM / 16; ++rbk) xblock_store(0, rbk, xblock_mfma(rbk));
+        wbar<kWLgkm0>();                          // every wave's CODE reads before the refill
+        code_dma(tile_of(1), 0, true);
+        wbar<wvm(0) & kWLgkm0>();
+#pragma unroll
+        for (int rbk = 0; rbk < NXB; ++rbk) xblock_store(1, rbk, xblock_mfma(rbk));
+#else
         expand(0, false);
         wwait<kWLgkm0>();                         // CODE read before it is refilled
         code_dma(tile_of(1), 0, true);
         wwait<wvm(0)>();
         expand(1, true);
+#endif
     } else {
         dma_tab(tile_of(0), 0);
 #pragma unroll
@@ -1156,7 +1219,8 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         // (B2) A image complete; every read of slot (s-1) % 3, the ext area
         // and this step's records done
         wtr.stamp(3);
-        wbar<kWLgkm0>();
+        if constexpr (X0 && MIGNN_WIN_XMFMA) wbar<wvm(0) & kWLgkm0>();   // (+ every wave's codes)
+        else wbar<kWLgkm0>();
         wtr.stamp(4);
         // the records of step s + 1 landed (younger: the own rows of tile s + 1
         // and the last step's stores)
@@ -1229,11 +1293,23 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                     // every XS t-steps from t = XT (the codes DMA'd at B0)
                     constexpr int XT = 2, XS = 2;
                     static_assert(!X0 || XT + XS * (NXR - 1) < NTT, "expansion inside the transform");
-                    f32x4 xcf[X0 ? 8 : 1];
+                    [[maybe_unused]] f32x4 xcf[X0 && !MIGNN_WIN_XMFMA ? 8 : 1];
+                    [[maybe_unused]] f32x4 xd[2];
 #pragma unroll
                     for (int t = 0; t < NTT; ++t) {
                         const int kc = t / IBW, ib = t % IBW;
                         if (t < NPC) dma_piece(t);
+#if MIGNN_WIN_XMFMA
+                        if constexpr (X0) {
+                            // block i's MFMAs, block i - 1's store (its result landed)
+                            static_assert(!X0 || XT + XS * (NXB - 1) < NTT, "expansion inside the transform");
+                            const int i = (t - XT) / XS;
+                            if (t >= XT && (t - XT) % XS == 0 && i < NXB) {
+                                xd[i & 1] = xblock_mfma(i);
+                                if (i > 0) xblock_store(xn2, i - 1, xd[(i - 1) & 1]);
+                            }
+                        }
+#else
                         if constexpr (X0) {
                             if (t == XT) {
                                 wwait<wvm(1)>();      // this wave's codes (the records younger)
@@ -1242,6 +1318,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                             if (t >= XT && (t - XT) % XS == 0 && (t - XT) / XS < NXR)
                                 expand_i(xcf, xn2, (t - XT) / XS);
                         }
+#endif
                         if (MODE & 4) continue;
                         if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
 #pragma unroll
@@ -1254,6 +1331,9 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                     }
 #pragma unroll
                     for (int t = NTT; t < NPC; ++t) dma_piece(t);
+#if MIGNN_WIN_XMFMA
+                    if constexpr (X0) xblock_store(xn2, NXB - 1, xd[(NXB - 1) & 1]);
+#endif
                 }
                 wtr.stamp(5);
 #if MIGNN_WIN_DIRECT
@@ -1330,8 +1410,13 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
 #pragma unroll
             for (int q = 0; q < NPC; ++q) dma_piece(q);
             if constexpr (X0) {
+#if MIGNN_WIN_XMFMA
+#pragma unroll
+                for (int rbk = 0; rbk < NXB; ++rbk) xblock_store(xn2, rbk, xblock_mfma(rbk));
+#else
                 wwait<wvm(1)>();
                 expand(xn2, true);
+#endif
             }
         }
         // carry tile s into phase B
