@@ -32,9 +32,26 @@ constexpr int kWaves = 4;
 // the one-role form of round 1.
 constexpr int kSplitRows = kWaves * 64;   // rows per block
 
+// a row's D coordinates: V4 (D <= 4, rows padded to 16 B, ldp 4): one 16-B
+// load instead of D 4-B loads (the gathers are TA-bound: a quarter of the
+// instructions for the same bytes)
+template <int D, bool V4>
+__device__ __forceinline__ void layer0_pos(const float* __restrict__ pos, int64_t ldp, int64_t r,
+                                           float (&p)[D]) {
+    if constexpr (V4) {
+        const float4 v = ld4(pos + r * 4);
+        const float q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int a = 0; a < D; ++a) p[a] = q[a];
+    } else {
+#pragma unroll
+        for (int a = 0; a < D; ++a) p[a] = pos[r * ldp + a];
+    }
+}
+
 // (c_i, C_i = sum_j w_ij c_j, s_i = sum_j w_ij) of row ri, CSR order (the
 // split kernel's gather role and the codes kernel: the same arithmetic)
-template <int D>
+template <int D, bool V4>
 __device__ __forceinline__ void layer0_gather(const int32_t* __restrict__ row_ptr,
                                               const int32_t* __restrict__ col,
                                               const float* __restrict__ ew,
@@ -42,8 +59,9 @@ __device__ __forceinline__ void layer0_gather(const int32_t* __restrict__ row_pt
                                               int64_t ri, float (&c)[D], float (&C)[D],
                                               float& sum) {
     sum = 0.f;
+    layer0_pos<D, V4>(pos, ldp, ri, c);
 #pragma unroll
-    for (int a = 0; a < D; ++a) { c[a] = pos[ri * ldp + a]; C[a] = 0.f; }
+    for (int a = 0; a < D; ++a) C[a] = 0.f;
     const int32_t e0 = row_ptr[ri], e1 = row_ptr[ri + 1];
     constexpr int kU = 8;
     int32_t jj[kU];
@@ -55,10 +73,14 @@ __device__ __forceinline__ void layer0_gather(const int32_t* __restrict__ row_pt
     }
     float pv[kU][D];
 #pragma unroll
-    for (int k = 0; k < kU; ++k)
+    for (int k = 0; k < kU; ++k) {
+        if (e0 + k < e1) {
+            layer0_pos<D, V4>(pos, ldp, jj[k], pv[k]);
+        } else {
 #pragma unroll
-        for (int a = 0; a < D; ++a)
-            pv[k][a] = e0 + k < e1 ? pos[(int64_t)jj[k] * ldp + a] : 0.f;
+            for (int a = 0; a < D; ++a) pv[k][a] = 0.f;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < kU; ++k) {
         if (e0 + k < e1) {
@@ -71,12 +93,14 @@ __device__ __forceinline__ void layer0_gather(const int32_t* __restrict__ row_pt
         const int64_t j = col[e];
         const float w = ew[e];
         sum += w;
+        float pj[D];
+        layer0_pos<D, V4>(pos, ldp, j, pj);
 #pragma unroll
-        for (int a = 0; a < D; ++a) C[a] = fmaf(w, pos[j * ldp + a], C[a]);
+        for (int a = 0; a < D; ++a) C[a] = fmaf(w, pj[a], C[a]);
     }
 }
 
-template <int D>
+template <int D, bool V4 = false>
 __global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
@@ -109,7 +133,7 @@ __global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
             const int64_t r = bg * kSplitRows + wave * 64 + lane;
             if (bg < nblk && r < nrows) {
                 float c[D], C[D], sum;
-                layer0_gather<D>(row_ptr, col, ew, pos, ldp, row_begin + r, c, C, sum);
+                layer0_gather<D, V4>(row_ptr, col, ew, pos, ldp, row_begin + r, c, C, sum);
                 float* const ag = agg[buf][wave * 64 + lane];
 #pragma unroll
                 for (int a = 0; a < D; ++a) { ag[a] = c[a]; ag[D + a] = C[a]; }
@@ -147,7 +171,7 @@ __global__ __launch_bounds__(2 * kWaves * 64) void gcn_layer0_split_kernel(
 // Layer-0 codes (the codes form of the window GCN kernel, gcn_win.hip): per
 // row the 8 floats (c_i, C_i, s_i, 0...) -- the values the split kernel's
 // store role expands -- instead of the [H] row: 32 B written per row.
-template <int D>
+template <int D, bool V4 = false>
 __global__ __launch_bounds__(256) void gcn_layer0_codes_kernel(
     const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ ew, const float* __restrict__ pos, int64_t ldp, int64_t row_begin,
@@ -155,7 +179,7 @@ __global__ __launch_bounds__(256) void gcn_layer0_codes_kernel(
     for (int64_t ri = row_begin + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; ri < row_end;
          ri += (int64_t)gridDim.x * blockDim.x) {
         float c[D], C[D], sum;
-        layer0_gather<D>(row_ptr, col, ew, pos, ldp, ri, c, C, sum);
+        layer0_gather<D, V4>(row_ptr, col, ew, pos, ldp, ri, c, C, sum);
         float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int a = 0; a < D; ++a) { v[a] = c[a]; v[D + a] = C[a]; }
@@ -187,7 +211,12 @@ extern "C" int mignn_gcn_layer0_codes(const int32_t* row_ptr, const int32_t* col
     switch (in_dim) {
     case 1: hipLaunchKernelGGL(gcn_layer0_codes_kernel<1>, dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc); break;
     case 2: hipLaunchKernelGGL(gcn_layer0_codes_kernel<2>, dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc); break;
-    default: hipLaunchKernelGGL(gcn_layer0_codes_kernel<3>, dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc); break;
+    default:
+        if (ldp == 4 && aligned16(pos))
+            hipLaunchKernelGGL((gcn_layer0_codes_kernel<3, true>), dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc);
+        else
+            hipLaunchKernelGGL(gcn_layer0_codes_kernel<3>, dim3(grid), dim3(256), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, codes, ldc);
+        break;
     }
     return launch_status("gcn_layer0_codes_kernel");
 }
@@ -211,7 +240,12 @@ extern "C" int mignn_gcn_layer0_coords(const int32_t* row_ptr, const int32_t* co
     switch (in_dim) {
     case 1: hipLaunchKernelGGL(gcn_layer0_split_kernel<1>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
     case 2: hipLaunchKernelGGL(gcn_layer0_split_kernel<2>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
-    case 3: hipLaunchKernelGGL(gcn_layer0_split_kernel<3>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
+    case 3:
+        if (ldp == 4 && aligned16(pos))
+            hipLaunchKernelGGL((gcn_layer0_split_kernel<3, true>), dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo);
+        else
+            hipLaunchKernelGGL(gcn_layer0_split_kernel<3>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo);
+        break;
     default: hipLaunchKernelGGL(gcn_layer0_split_kernel<4>, dim3(grid), dim3(2 * kWaves * 64), 0, st, row_ptr, col, ew, pos, ldp, row_begin, row_end, coef, h, out, ldo); break;
     }
     return launch_status("gcn_layer0_split_kernel");

@@ -944,11 +944,14 @@ class FlowGNN(nn.Module):
         if csr.perm is None:
             return x
         D = self.input_dim
-        pos = torch.empty((x.shape[0], D), dtype=torch.float32, device=x.device)
+        # (3-D coordinates into 16-B rows: the layer-0 kernels gather a
+        # neighbour's coordinates with one 16-B load; the 4th column unread)
+        ld = 4 if D == 3 else D
+        pos = torch.empty((x.shape[0], ld), dtype=torch.float32, device=x.device)
         _lib.check(_lib.lib().mignn_rows_gather(
-            _lib.ptr(x), x.stride(0), _lib.ptr(csr.perm), x.shape[0], D, _lib.ptr(pos), D,
+            _lib.ptr(x), x.stride(0), _lib.ptr(csr.perm), x.shape[0], D, _lib.ptr(pos), ld,
             _stream(x)), "mignn_rows_gather")
-        return pos
+        return pos[:, :D]
 
     def _gcn_layer0(self, csr: Csr, pos, rb, re, out):
         _lib.check(_lib.lib().mignn_gcn_layer0_coords(
