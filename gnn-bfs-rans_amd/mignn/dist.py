@@ -91,11 +91,15 @@ class RangeLayout:
         b = torch.tensor(self.bounds, dtype=torch.int64, device=dev)
         ends = torch.where(b > 0, csum[(b - 1).clamp(min=0)], torch.zeros_like(b))
         counts = ends[1:] - ends[:-1]                        # ghosts per owner rank
-        # boundary rows: owned destinations with a ghost source
-        boundary = torch.zeros(self.n_own, dtype=torch.int32, device=dev)
+        # boundary rows: owned destinations with a ghost source (a flag fill
+        # through a dummy slot for the own-source edges: no atomics -- an
+        # index_add over every edge serialised on a mesh's runs of equal
+        # destinations, 2 ms per 60M edges)
+        bmark = torch.zeros(self.n_own + 1, dtype=torch.int8, device=dev)
         if E:
-            boundary.index_add_(0, (dst - lo).clamp(0, max(self.n_own - 1, 0)), (~own_src).int())
-        boundary = boundary > 0
+            bmark.index_fill_(0, torch.where(own_src, torch.full_like(dst, self.n_own),
+                                             (dst - lo).clamp(0, max(self.n_own, 0))), 1)
+        boundary = bmark[:self.n_own] > 0
         # every host-side size in ONE device->host transfer
         bad_dst = ((dst < lo) | (dst >= hi)).any() if E else torch.zeros((), dtype=torch.bool, device=dev)
         bad_src = ((src < 0) | (src >= N)).any() if E else torch.zeros((), dtype=torch.bool, device=dev)
@@ -117,20 +121,27 @@ class RangeLayout:
         self.ghost_gid = ghost
         # local order of the owned rows: interior first, boundary last
         if order_fn is not None and pos is not None and self.n_own > 0:
-            # the locality order sees the edges among owned rows (own sources
-            # first by a stable sort: no host sync for the count)
-            sel = torch.sort((~own_src).to(torch.int8), stable=True).indices[:n_own_edges]
+            # the locality order sees the edges among owned rows (their count
+            # came with the sizes above: a compaction, no second sync)
+            sel = _nonzero_known(own_src, n_own_edges)
             base = order_fn(pos, torch.stack([src[sel] - lo, dst[sel] - lo])).long()
         else:
             base = torch.arange(self.n_own, device=dev)
-        key = boundary[base].to(torch.int64)
-        perm = base[torch.sort(key, stable=True).indices]       # local position -> owned offset
+        # interior first, boundary last, each in the base order: a stable
+        # partition by prefix sums (a stable sort of the 0/1 keys cost 0.7 ms)
+        bnd = boundary[base]
+        ci = torch.cumsum((~bnd).to(torch.int32), 0)
+        cb = torch.cumsum(bnd.to(torch.int32), 0)
+        dest = torch.where(bnd, self.n_int + cb - 1, ci - 1).long()
+        perm = torch.empty_like(base)
+        perm[dest] = base                                          # local position -> owned offset
         self.perm = perm
         self.inv = torch.empty_like(perm)
         self.inv[perm] = torch.arange(self.n_own, device=dev)
-        # local edge list: owned -> local position, ghost -> n_own + ghost index
+        # local edge list: owned -> local position, ghost -> n_own + ghost
+        # index (the ghost's rank among the marked ids: the prefix sum above)
         lsrc = torch.where(own_src, self.inv[(src - lo).clamp(0, max(self.n_own - 1, 0))],
-                           self.n_own + torch.searchsorted(ghost, src))
+                           self.n_own - 1 + csum[src.clamp(0, N)])
         self.edge_index = torch.stack([lsrc, self.inv[dst - lo]])
         # send lists: every peer's ghost requests, answered with my local rows
         req = {q: ghost[self.ghost_ptr[q]:self.ghost_ptr[q + 1]]
