@@ -427,6 +427,23 @@ __global__ void gcn_norm_kernel(const int32_t* __restrict__ row_ptr,
     }
 }
 
+// a node-range shard's local edge list (mignn.dist.RangeLayout): source ids
+// in [lo, hi) -> the owned row's local position inv[id - lo], others (ghosts)
+// -> n_own + the ghost's rank among the ghost ids (ghost_rank[id] - 1: the
+// inclusive prefix sum of the ghost marks); destination ids (owned) ->
+// inv[id - lo].  out = [2, E] (row 0 sources, row 1 destinations).
+__global__ void range_relabel_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t lo,
+                                     int64_t hi, const int64_t* __restrict__ inv,
+                                     const int64_t* __restrict__ ghost_rank, int64_t n_own,
+                                     int64_t* __restrict__ out) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = ei[e], d = ei[E + e];
+        out[e] = (s >= lo && s < hi) ? inv[s - lo] : n_own - 1 + ghost_rank[s];
+        out[E + e] = inv[d - lo];
+    }
+}
+
 __global__ void rows_gather_kernel(const float* __restrict__ src, int64_t lds,
                                    const int32_t* __restrict__ idx, int64_t n, int h4,
                                    float* __restrict__ dst, int64_t ldd) {
@@ -543,6 +560,17 @@ extern "C" int mignn_csr_build_gcn(const int64_t* edge_index, int64_t E, int64_t
         if ((rc = launch_status("csr_info_kernel"))) return rc;
     }
     return MIGNN_OK;
+}
+
+extern "C" int mignn_range_relabel(const int64_t* edge_index, int64_t E, int64_t lo, int64_t hi,
+                                   const int64_t* inv, const int64_t* ghost_rank, int64_t n_own,
+                                   int64_t* out, void* stream) {
+    MIGNN_REQUIRE(E >= 0 && lo >= 0 && hi >= lo && n_own == hi - lo, "range_relabel: bad sizes");
+    if (E == 0) return MIGNN_OK;
+    MIGNN_REQUIRE(edge_index && inv && ghost_rank && out, "range_relabel: null pointer");
+    hipLaunchKernelGGL(range_relabel_kernel, dim3(grid_for(E, kBlock, 8192)), dim3(kBlock), 0,
+                       as_stream(stream), edge_index, E, lo, hi, inv, ghost_rank, n_own, out);
+    return launch_status("range_relabel_kernel");
 }
 
 extern "C" int mignn_grid_graph(int nx, int ny, int nz, int z_begin, int z_count,

@@ -101,16 +101,20 @@ class RangeLayout:
                                              (dst - lo).clamp(0, max(self.n_own, 0))), 1)
         boundary = bmark[:self.n_own] > 0
         # every host-side size in ONE device->host transfer
-        bad_dst = ((dst < lo) | (dst >= hi)).any() if E else torch.zeros((), dtype=torch.bool, device=dev)
-        bad_src = ((src < 0) | (src >= N)).any() if E else torch.zeros((), dtype=torch.bool, device=dev)
-        host = torch.cat([torch.stack([bad_dst.long(), bad_src.long(), (~boundary).sum(),
-                                       own_src.sum()]), counts]).cpu().tolist()
+        if E:
+            dmin, dmax = torch.aminmax(dst)
+            smin, smax = torch.aminmax(src)
+            bad_dst, bad_src = (dmin < lo) | (dmax >= hi), (smin < 0) | (smax >= N)
+        else:
+            bad_dst = bad_src = torch.zeros((), dtype=torch.bool, device=dev)
+        host = torch.cat([torch.stack([bad_dst.long(), bad_src.long(), (~boundary).sum()]),
+                          counts]).cpu().tolist()
         if host[0]:
             raise ValueError("edge_index holds an edge whose destination this rank does not own")
         if host[1]:
             raise ValueError("edge_index holds a source outside [0, N)")
-        self.n_int, n_own_edges = int(host[2]), int(host[3])
-        counts = [int(c) for c in host[4:]]
+        self.n_int = int(host[2])
+        counts = [int(c) for c in host[3:]]
         self.ghost_ptr = [0]
         for c in counts:
             self.ghost_ptr.append(self.ghost_ptr[-1] + c)
@@ -121,10 +125,14 @@ class RangeLayout:
         self.ghost_gid = ghost
         # local order of the owned rows: interior first, boundary last
         if order_fn is not None and pos is not None and self.n_own > 0:
-            # the locality order sees the edges among owned rows (their count
-            # came with the sizes above: a compaction, no second sync)
-            sel = _nonzero_known(own_src, n_own_edges)
-            base = order_fn(pos, torch.stack([src[sel] - lo, dst[sel] - lo])).long()
+            # the locality order reads edges only for its spacing estimate, a
+            # strided sample of <= 2^18 of them (mignn_locality_order): that
+            # sample of this rank's edges in local ids, the ghost-source ones
+            # marked invalid (-1, skipped by the estimate)
+            ns = min(E, 1 << 18)
+            idx = (torch.arange(ns, device=dev) * E) // max(ns, 1)
+            s_loc = torch.where(own_src[idx], src[idx] - lo, torch.full_like(idx, -1))
+            base = order_fn(pos, torch.stack([s_loc, dst[idx] - lo])).long()
         else:
             base = torch.arange(self.n_own, device=dev)
         # interior first, boundary last, each in the base order: a stable
@@ -140,9 +148,18 @@ class RangeLayout:
         self.inv[perm] = torch.arange(self.n_own, device=dev)
         # local edge list: owned -> local position, ghost -> n_own + ghost
         # index (the ghost's rank among the marked ids: the prefix sum above)
-        lsrc = torch.where(own_src, self.inv[(src - lo).clamp(0, max(self.n_own - 1, 0))],
-                           self.n_own - 1 + csum[src.clamp(0, N)])
-        self.edge_index = torch.stack([lsrc, self.inv[dst - lo]])
+        if dev.type == "cuda" and E > 0:
+            from . import _lib
+            ei64 = edge_index if (edge_index.dtype == torch.int64 and edge_index.is_contiguous()) \
+                else torch.stack([src, dst])
+            self.edge_index = torch.empty((2, E), dtype=torch.int64, device=dev)
+            _lib.check(_lib.lib().mignn_range_relabel(
+                _lib.ptr(ei64), E, lo, hi, _lib.ptr(self.inv), _lib.ptr(csum), self.n_own,
+                _lib.ptr(self.edge_index), _lib.stream(dev)), "mignn_range_relabel")
+        else:
+            lsrc = torch.where(own_src, self.inv[(src - lo).clamp(0, max(self.n_own - 1, 0))],
+                               self.n_own - 1 + csum[src.clamp(0, N)])
+            self.edge_index = torch.stack([lsrc, self.inv[dst - lo]])
         # send lists: every peer's ghost requests, answered with my local rows
         req = {q: ghost[self.ghost_ptr[q]:self.ghost_ptr[q + 1]]
                for q in range(self.world) if q != rank and counts[q] > 0}

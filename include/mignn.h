@@ -654,6 +654,14 @@ int mignn_gat_train_backward(const int32_t* row_ptr, const int32_t* col, const i
 /* dst[r, :] = src[idx[r], :] for r < n (halo pack / unpack by index list) */
 int mignn_rows_gather(const float* src, int64_t lds, const int32_t* idx, int64_t n, int h,
                       float* dst, int64_t ldd, void* stream);
+/* A node-range shard's local edge list (mignn.dist.RangeLayout; the caller
+ * has validated the ids): edge_index [2, E] global ids, destinations in
+ * [lo, hi).  out [2, E]: a source in [lo, hi) -> inv[src - lo], any other
+ * (a ghost) -> n_own + ghost_rank[src] - 1 (ghost_rank: inclusive prefix sum
+ * of the ghost marks over the global ids); a destination -> inv[dst - lo]. */
+int mignn_range_relabel(const int64_t* edge_index, int64_t E, int64_t lo, int64_t hi,
+                        const int64_t* inv, const int64_t* ghost_rank, int64_t n_own,
+                        int64_t* out, void* stream);
 /* Periodic nx*ny*nz hex grid, k-slab [z_begin, z_begin+z_count): writes
  * edge_index [2, 6*n] (src = neighbour, dst = node; global ids) and
  * x [n, 3] = cell centres in [0,1]^3.  n = nx*ny*z_count. */

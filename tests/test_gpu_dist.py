@@ -165,3 +165,27 @@ def test_config4_gin_h256_l8_partitioned(P):
           f"on {seeds.numel()} rows ({nodes.numel()}-node field), fp32 oracle {ref:.2e}")
     assert err <= 2e-6 * scale
     assert e64 <= max(1e-5, 2.0 * ref)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_range_layout_device_matches_host(P):
+    """RangeLayout on the device (the local edge list by mignn_range_relabel)
+    equals the same layout built from host tensors by the torch path: local
+    edges, order, ghosts, boundary split and send lists, on a graph with
+    duplicate edges, self-loops and ranks without ghosts from some peers."""
+    g = torch.Generator().manual_seed(P)
+    n = 3000
+    ei = torch.randint(0, n, (2, 40000), generator=g)
+    ei = torch.cat([ei, torch.stack([torch.arange(n), torch.arange(n)])], 1)
+    b = range_bounds(n, P)
+    edges = [ei[:, (ei[1] >= b[r]) & (ei[1] < b[r + 1])] for r in range(P)]
+    host = build_local_layouts(edges, b)
+    dev = build_local_layouts([e.to(DEV) for e in edges], b)
+    for lh, ld in zip(host, dev):
+        assert (lh.n_int, lh.n_ghost, lh.ghost_ptr) == (ld.n_int, ld.n_ghost, ld.ghost_ptr)
+        assert torch.equal(lh.edge_index, ld.edge_index.cpu())
+        assert torch.equal(lh.perm, ld.perm.cpu())
+        assert torch.equal(lh.ghost_gid, ld.ghost_gid.cpu())
+        assert sorted(lh.send_idx) == sorted(ld.send_idx)
+        for q in lh.send_idx:
+            assert torch.equal(lh.send_idx[q], ld.send_idx[q].cpu())
