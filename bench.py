@@ -202,6 +202,11 @@ def main():
         N_local = x.shape[0]
         bounds = [r * N_local for r in range(world + 1)]
         exch = DistExchange()
+        # the block order: a shard's interior / boundary row ranges have no
+        # column schedule for the window kernel (its chunk schedule ran the
+        # 10M-row interior range in 6.4-6.9 ms vs the producer / consumer
+        # kernel's ~3 -- DESIGN.md 4; the column-order shard route stays
+        # available, FlowGNNShard + an order_fn returning (perm, info))
         order = (lambda p, e: locality_order(p, e)[0]) if model._use_reorder(x) else None
         shard_box = [None]
 
@@ -350,7 +355,7 @@ def main():
                                      "locality: 4x4x4-cell blocks in panels of 4x4 block columns "
                                      "(mignn_locality_order)") + "; part of the per-step graph setup"
                                     if world == 1 else
-                                    "locality order inside each rank's range, interior rows "
+                                    "block order inside each rank's range, interior rows "
                                     "first; the partition layout (ghost / send lists, the "
                                     "order) and the rank-local CSR are rebuilt inside every "
                                     "timed step, as the N = 1 step rebuilds its CSR and order")

@@ -64,7 +64,9 @@ class RangeLayout:
     destination this rank owns (int64, any device); `pos` [n_own, >=3]
     optional cell centres of the owned nodes (caller order = global id
     order), used only to pick the locality order via `order_fn(pos, ei)`
-    -> perm (local position -> owned offset)."""
+    -> perm (local position -> owned offset), or (perm, info) for the
+    column order (mignn_locality_order_cols' info, kept as `order_info`: the
+    window GCN kernel's route on the rank-local CSR)."""
 
     def __init__(self, edge_index: torch.Tensor, bounds: Sequence[int], rank: int,
                  requests: "RequestExchange", pos: Optional[torch.Tensor] = None,
@@ -123,6 +125,7 @@ class RangeLayout:
         # ghosts: sorted global ids == grouped by owner rank (contiguous ranges)
         ghost = _nonzero_known(mark[:N], self.n_ghost)
         self.ghost_gid = ghost
+        self.order_info = None
         # local order of the owned rows: interior first, boundary last
         if order_fn is not None and pos is not None and self.n_own > 0:
             # the locality order reads edges only for its spacing estimate, a
@@ -132,7 +135,10 @@ class RangeLayout:
             ns = min(E, 1 << 18)
             idx = (torch.arange(ns, device=dev) * E) // max(ns, 1)
             s_loc = torch.where(own_src[idx], src[idx] - lo, torch.full_like(idx, -1))
-            base = order_fn(pos, torch.stack([s_loc, dst[idx] - lo])).long()
+            got = order_fn(pos, torch.stack([s_loc, dst[idx] - lo]))
+            if isinstance(got, tuple):
+                got, self.order_info = got
+            base = got.long()
         else:
             base = torch.arange(self.n_own, device=dev)
         # interior first, boundary last, each in the base order: a stable
@@ -463,6 +469,10 @@ class FlowGNNShard(Shard):
         mode = CSR_ONE_SELF_LOOP if m.layer_type in ("GCN", "GAT") else CSR_VERBATIM
         for sh in shards:
             sh.csr = build_csr(sh.layout.edge_index, sh.layout.n_total, mode)
+            # (the column order: the window kernel's route; its plans cover
+            # row ranges -- interior, boundary -- so they take the contiguous
+            # chunk schedule, the info only marks the order)
+            sh.csr.order_info = sh.layout.order_info
         if shards[0].csr.dinv is not None:
             # ghost rows' true deg^-1/2 comes from their owners
             exchange_static(shards, exchange, [sh.csr.dinv[:sh.layout.n_total].view(-1, 1)

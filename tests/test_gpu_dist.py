@@ -31,12 +31,14 @@ def _gpu():
     _lib.lib()
 
 
-def _sharded(model, x, ei, P, ordered=True):
+def _sharded(model, x, ei, P, ordered=True, cols=False):
     n = x.shape[0]
     b = range_bounds(n, P)
     edges = [ei[:, (ei[1] >= b[r]) & (ei[1] < b[r + 1])] for r in range(P)]
     pos = [x[b[r]:b[r + 1]] for r in range(P)]
     order = (lambda p, e: locality_order(p, e)[0]) if ordered else None
+    if ordered and cols:     # the column order: the window kernel on the shards
+        order = lambda p, e: (lambda r: (r[0], r[2]))(locality_order(p, e, cols=True))  # noqa: E731
     lays = build_local_layouts(edges, b, pos=pos, order_fn=order)
     shards = [FlowGNNShard(model, lay, p) for lay, p in zip(lays, pos)]
     ex = LocalExchange()
@@ -189,3 +191,28 @@ def test_range_layout_device_matches_host(P):
         assert sorted(lh.send_idx) == sorted(ld.send_idx)
         for q in lh.send_idx:
             assert torch.equal(lh.send_idx[q], ld.send_idx[q].cpu())
+
+
+@pytest.mark.parametrize("shuffle", [None, 2])
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("H", [64, 128])
+def test_sharded_column_order_window_route(H, P, shuffle):
+    """Shards in the column order take the window kernel (their CSRs carry
+    the order info; plans over the interior / boundary row ranges in the
+    chunk schedule): equal to the unsharded forward up to fp32 summation
+    order and to fp64 within the usual bound."""
+    cfg = dict(hidden_dim=H, num_layers=3, layer_type="GCN")
+    m = FlowGNN(input_dim=3, output_dim=7, dropout=0.0, **cfg)
+    sd = seeded_state_dict(m.state_dict(), seed=6)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    x, ei = grid_graph(40, 32, 24, device=DEV, permute_seed=shuffle)
+    with torch.no_grad():
+        y = m(x, ei)
+    ys, lays = _sharded(m, x, ei, P, cols=True)
+    assert all(l.order_info is not None for l in lays)
+    assert m._gcn_kernel(H) == "win"
+    scale = max(1.0, y.abs().max().item())
+    assert (ys - y).abs().max().item() <= 2e-6 * scale
+    ref = orc.flowgnn_forward(sd, cfg, x.cpu(), ei.cpu(), None, dtype=torch.float64)
+    assert (ys.cpu().double() - ref).abs().max().item() <= 1e-5 * scale
