@@ -202,12 +202,15 @@ def main():
         N_local = x.shape[0]
         bounds = [r * N_local for r in range(world + 1)]
         exch = DistExchange()
-        # the block order: a shard's interior / boundary row ranges have no
-        # column schedule for the window kernel (its chunk schedule ran the
-        # 10M-row interior range in 6.4-6.9 ms vs the producer / consumer
-        # kernel's ~3 -- DESIGN.md 4; the column-order shard route stays
-        # available, FlowGNNShard + an order_fn returning (perm, info))
-        order = (lambda p, e: locality_order(p, e)[0]) if model._use_reorder(x) else None
+        if not model._use_reorder(x):
+            order = None
+        elif model._column_order():
+            # the column order, as on one GPU: its info marks the rank-local
+            # CSR for the window kernel (the interior range's plan takes the
+            # column schedule with the planes per column from the CSR)
+            order = lambda p, e: (lambda r: (r[0], r[2]))(locality_order(p, e, cols=True))  # noqa: E731
+        else:
+            order = lambda p, e: locality_order(p, e)[0]  # noqa: E731
         shard_box = [None]
 
         def build_shard():
@@ -297,8 +300,9 @@ def main():
     roofline = None
     if args.layer_type == "GCN":
         route = model._gcn_kernel(H)
-        if world > 1 and route == "win" and model.gcn_kernel == "auto":
-            # (a shard's rows are block-ordered: FlowGNN._gcn_kernel's fallback)
+        if (world > 1 and route == "win" and model.gcn_kernel == "auto"
+                and not (model._use_reorder(x) and model._column_order())):
+            # (a shard's rows without the column order: FlowGNN._gcn_kernel's fallback)
             from mignn.gnn_model import GCN_BLOCK_ORDER
             route = GCN_BLOCK_ORDER.get(H, "pc")
         roofline = gcn_roofline(launches, H, deg_plus_self, model.precision, traffic, route)
@@ -355,7 +359,9 @@ def main():
                                      "locality: 4x4x4-cell blocks in panels of 4x4 block columns "
                                      "(mignn_locality_order)") + "; part of the per-step graph setup"
                                     if world == 1 else
-                                    "block order inside each rank's range, interior rows "
+                                    ("column order (window GCN kernel)" if model._column_order()
+                                     else "block order") +
+                                    " inside each rank's range, interior rows "
                                     "first; the partition layout (ghost / send lists, the "
                                     "order) and the rank-local CSR are rebuilt inside every "
                                     "timed step, as the N = 1 step rebuilds its CSR and order")

@@ -204,7 +204,9 @@ struct WinHdr {
     int32_t G, h, L;
     int32_t R1, chunk, nsteps, Z;
     int64_t ntiles, t2, rb, re;
+    int32_t zrun;   // (plan build) tiles from tile 0 that chain as z-planes of one column
 };
+static_assert(sizeof(WinHdr) <= kWHdr, "plan header");
 
 struct WinSched {
     int64_t ntiles, t2;
@@ -244,14 +246,36 @@ __device__ inline void win_where32(const WinSched& S, int t, int& p, int& s) {
     }
 }
 
+// the column run of the plan's rows: tile t + 1 continues tile t as the next
+// z-plane of its column when tile t's first row has tile t + 1's first row
+// among its entries; zrun = the first t + 1 where that breaks (a column's
+// plane count from the CSR itself -- a shard's interior range has the column
+// order with its boundary planes moved out, fewer planes than the order's Z)
+__global__ void win_zrun_init_kernel(WinHdr* hdr, int64_t ntiles) {
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        hdr->zrun = static_cast<int32_t>(ntiles < (1ll << 30) ? ntiles : (1ll << 30));
+}
+__global__ void win_zrun_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+                                int64_t rb, int64_t re, int64_t ntiles, WinHdr* hdr) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t + 1 < ntiles;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r0 = rb + t * 64, r1 = r0 + 64;
+        bool cont = false;
+        if (r1 < re)
+            for (int32_t e = row_ptr[r0]; e < row_ptr[r0 + 1]; ++e) cont |= col[e] == r1;
+        if (!cont) atomicMin(&hdr->zrun, static_cast<int32_t>(t + 1));
+    }
+}
+
 // the header: schedule parameters from the order's column info (nullable:
-// {1, Z tiles per full column, full columns, ...}, mignn_locality_order_cols)
+// {1, Z tiles per full column, full columns, ...}, mignn_locality_order_cols),
+// Z capped by the CSR's own column run (win_zrun_kernel)
 __global__ void win_hdr_kernel(WinHdr* hdr, const int32_t* __restrict__ info, int64_t ntiles, int G,
                                int h, int64_t rb, int64_t re) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int64_t Z = 0, C = 0;
     if (info != nullptr && info[0] == 1) {
-        Z = info[1];
+        Z = info[1] < hdr->zrun ? info[1] : hdr->zrun;
         C = info[2];
     }
     // contiguous chunks (no column structure)
@@ -1975,6 +1999,14 @@ extern "C" int mignn_gcn_win_plan(const int32_t* row_ptr, const int32_t* col, co
     MIGNN_REQUIRE(G > 0, "gcn_win_plan: device query failed");
     hipStream_t st = as_stream(stream);
     WinHdr* hdr = static_cast<WinHdr*>(plan);
+    if (order_info != nullptr) {
+        hipLaunchKernelGGL(win_zrun_init_kernel, dim3(1), dim3(64), 0, st, hdr, ntiles);
+        int rc0 = launch_status("win_zrun_init_kernel");
+        if (rc0) return rc0;
+        hipLaunchKernelGGL(win_zrun_kernel, dim3(grid_for(ntiles, 256, 4096)), dim3(256), 0, st,
+                           row_ptr, col, rb, re, ntiles, hdr);
+        if ((rc0 = launch_status("win_zrun_kernel"))) return rc0;
+    }
     hipLaunchKernelGGL(win_hdr_kernel, dim3(1), dim3(64), 0, st, hdr, order_info, ntiles, G, h, rb, re);
     int rc = launch_status("win_hdr_kernel");
     if (rc) return rc;

@@ -169,15 +169,17 @@ class Csr:
         """The window kernel's plan of rows [row_begin, row_end) for hidden
         width h (mignn_gcn_win_plan: header with this device's grid and the
         schedule -- the column schedule when the CSR is in the column order
-        and the plan covers every row -- and a 48-B record per row), built on
-        first use and kept with the CSR (it copies the ew weights)."""
+        and the plan's rows start at row 0 (a shard's interior range: the
+        plane count per column taken from the CSR, mignn_gcn_win_plan) --
+        and a 48-B record per row), built on first use and kept with the CSR
+        (it copies the ew weights)."""
         key = ("win", h, row_begin, row_end)
         plan = self.plans.get(key)
         if plan is None:
             L = _lib.lib()
             nb = L.mignn_gcn_win_plan_bytes(row_begin, row_end, h)
             plan = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.col.device)
-            info = self.order_info if (row_begin == 0 and row_end == self.num_nodes) else None
+            info = self.order_info if row_begin == 0 else None
             _lib.check(L.mignn_gcn_win_plan(_lib.ptr(self.row_ptr), _lib.ptr(self.col),
                                             _lib.ptr(self.ew), row_begin, row_end, h,
                                             _lib.ptr(info), _lib.ptr(plan), nb, None,

@@ -327,8 +327,11 @@ int mignn_gcn_aggregate_ring(const void* plan, const int32_t* row_ptr, const int
  * mignn_gcn_win_plan_bytes; device memory, 16-B aligned) carries a header
  * with the launch grid and schedule, checked by the layer kernel
  * (MIGNN_DEVERR_PLAN on a mismatch), and a 48-B record per row.
- * order_info (nullable: the int32[4] info of mignn_locality_order_cols for
- * the whole graph, row_begin = 0) selects the column schedule.  Build the plan
+ * order_info (nullable: the int32[4] info of mignn_locality_order_cols,
+ * rows from row_begin = 0 in that order -- the whole graph, or a shard's
+ * interior range with its boundary planes moved out) selects the column
+ * schedule, with the planes per column taken as the smaller of the info's
+ * and the CSR's own run of tiles chaining as z-planes.  Build the plan
  * on the device that runs the layer.  Sum order: a row's entries in CSR order
  * except its one next-tile entry, added last.  stats (nullable, device
  * uint64[4]): tiles over the out-of-tile capacity, rows on the CSR path, rows

@@ -5,7 +5,7 @@ k-slab ranges), all P shards driven by sharded_forward over LocalExchange
 Times per step: the partition layout (RangeLayout, every rank), the shard
 setup (rank-local CSR, ghost degrees, gcn_norm weights, ghost coordinates)
 and the forward; per rank = total / P.  SB_P (2), SB_REPS (5), SB_ORDER
-(blocks: the bench's N > 1 route; cols: the column order, window kernel).  Prints one
+(cols: the column order, window kernel, the bench's N > 1 route; blocks).  Prints one
 JSON object."""
 import json
 import os
@@ -37,7 +37,7 @@ for r in range(P):
     eis.append(ei)
 n = xs[0].shape[0]
 bounds = [r * n for r in range(P + 1)]
-if os.environ.get("SB_ORDER", "blocks") == "cols":   # the window kernel's order
+if os.environ.get("SB_ORDER", "cols") == "cols":   # the window kernel's order (bench N > 1)
     order = lambda p, e: (lambda r: (r[0], r[2]))(locality_order(p, e, cols=True))  # noqa: E731
 else:
     order = lambda p, e: locality_order(p, e)[0]  # noqa: E731
