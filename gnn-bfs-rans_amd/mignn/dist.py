@@ -368,6 +368,10 @@ class Shard:
 
     def layer(self, i: int, x: torch.Tensor, out: torch.Tensor, rb: int, re: int) -> None: ...
 
+    def halo_rows(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        """The rows layer i reads from the ghosts (default: its input x)."""
+        return x
+
     def halo_extra(self, i: int) -> Optional[torch.Tensor]:
         """A second per-row tensor whose ghost rows travel with layer i's
         feature halo (sharded GAT: the logits the previous layer's epilogue
@@ -405,7 +409,7 @@ def sharded_forward(shards: List[Shard], exchange, xs_own: List[torch.Tensor]) -
     assert all(s == first for s in starts)
     cur, nxt = bufs_a, bufs_b
     for i in range(first, shards[0].num_layers):
-        h = exchange.start(shards, cur)
+        h = exchange.start(shards, [sh.halo_rows(i, x) for sh, x in zip(shards, cur)])
         extra = [sh.halo_extra(i) for sh in shards]
         if any(e is not None for e in extra) and not all(e is not None for e in extra):
             raise RuntimeError(f"layer {i}: halo_extra differs between shards")
@@ -450,6 +454,7 @@ class FlowGNNShard(Shard):
         self.lg = None          # [n_total, 2 heads] logits of the layer about to run
         self.lg_ready = False   # its owned rows written by the previous layer
         self.lg_next = None
+        self.codes = None       # layer 0's row codes [n_total, 8] when layer 1 reads them
 
     def setup(self, exchange, shards: List["FlowGNNShard"]):
         """Per-graph setup of every shard in `shards` (collective over them):
@@ -502,6 +507,13 @@ class FlowGNNShard(Shard):
     def first_layer(self, x_own, buf):
         m, lay = self.model, self.layout
         self.lg, self.lg_ready, self.lg_next = None, False, None
+        self.codes = None
+        if self.kind0 == "gcn" and m._use_gcn_codes(self.csr):
+            # layer 0 as row codes (the 1-GPU route, FlowGNN._gcn_layers01_codes):
+            # layer 1's halo moves the ghosts' 32-B codes instead of their rows
+            self.codes = torch.zeros((lay.n_total, 8), dtype=torch.float32, device=buf.device)
+            m._gcn_layer0_codes(self.csr, self.pos, 0, lay.n_own, self.codes)
+            return 1
         if self.kind0 is not None:
             lg = None
             if self.kind0 == "gat" and self.chain and self.num_layers > 1:
@@ -512,6 +524,9 @@ class FlowGNNShard(Shard):
         xo = x_own.contiguous().float()
         m._input_proj(xo, buf[:lay.n_own], rows=lay.perm.to(torch.int32))
         return 0
+
+    def halo_rows(self, i, x):
+        return self.codes if (i == 1 and self.codes is not None) else x
 
     def halo_extra(self, i):
         return self.lg if self.lg_ready else None
@@ -537,6 +552,9 @@ class FlowGNNShard(Shard):
             linear(x[self.layout.n_own:], self._wlog(i), out=self.lg[self.layout.n_own:])
 
     def layer(self, i, x, out, rb, re):
+        if i == 1 and self.codes is not None:
+            self.model._gcn_layer1_codes(self.csr, self.codes, rb, re, out)
+            return
         lg_next = None
         if self.chain and i + 1 < self.num_layers:
             if self.lg_next is None:
@@ -546,6 +564,8 @@ class FlowGNNShard(Shard):
                           logits=self.lg, logits_next=lg_next)
 
     def end_layer(self, i):
+        if i == 1:
+            self.codes = None
         if self.chain and i + 1 < self.num_layers:
             self.lg, self.lg_next = self.lg_next, self.lg
             self.lg_ready = True

@@ -973,21 +973,30 @@ class FlowGNN(nn.Module):
         window kernel expanding every row it reads from them with layer 0's
         coefficients -- the same rows, bitwise, without layer 0's [n, H]
         write and layer 1's re-read of it."""
-        L = _lib.lib()
-        P = _lib.ptr
-        st = _stream(pos)
         codes = torch.empty((n, 8), dtype=torch.float32, device=pos.device)
-        _lib.check(L.mignn_gcn_layer0_codes(P(csr.row_ptr), P(csr.col), P(csr.ew), P(pos),
-                                            pos.stride(0), self.input_dim, 0, n, P(codes), 8, st),
-                   "mignn_gcn_layer0_codes")
+        self._gcn_layer0_codes(csr, pos, 0, n, codes)
+        self._gcn_layer1_codes(csr, codes, 0, n, out)
+
+    def _gcn_layer0_codes(self, csr: Csr, pos, rb: int, re: int, codes):
+        """Layer 0's row codes (c_i, C_i, s_i) of rows [rb, re) into codes [*, 8]."""
+        _lib.check(_lib.lib().mignn_gcn_layer0_codes(
+            _lib.ptr(csr.row_ptr), _lib.ptr(csr.col), _lib.ptr(csr.ew), _lib.ptr(pos),
+            pos.stride(0), self.input_dim, rb, re, _lib.ptr(codes), codes.stride(0),
+            _stream(pos)), "mignn_gcn_layer0_codes")
+
+    def _gcn_layer1_codes(self, csr: Csr, codes, rb: int, re: int, out):
+        """Layer 1 of rows [rb, re) by the window kernel's codes form: every
+        row it reads expanded from `codes` (the rows of every referenced node
+        present, a shard's ghosts included)."""
+        P = _lib.ptr
         layer = self.gnn_layers[1]
         scale, shift = self._bn(1)
         epi = EPI_BIAS | EPI_RESIDUAL | (EPI_AFFINE if scale is not None else 0) | EPI_RELU
-        plan = csr.win_plan(128, 0, n)
-        _lib.check(L.mignn_gcn_layer_win_codes(
-            P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(codes), 8, 0, n, 128,
+        plan = csr.win_plan(128, rb, re)
+        _lib.check(_lib.lib().mignn_gcn_layer_win_codes(
+            P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(codes), codes.stride(0), rb, re, 128,
             P(self._layer0_coef()), P(layer.lin.weight), P(layer.bias), P(scale), P(shift), epi,
-            P(out), out.stride(0), st), "mignn_gcn_layer_win_codes")
+            P(out), out.stride(0), _stream(codes)), "mignn_gcn_layer_win_codes")
 
     def _gcn_kernel(self, H: int, csr: Optional["Csr"] = None) -> str:
         """The GCN layer kernel at width H; with `csr`: the kernel for that
