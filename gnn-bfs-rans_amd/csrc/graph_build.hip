@@ -427,6 +427,27 @@ __global__ void gcn_norm_kernel(const int32_t* __restrict__ row_ptr,
     }
 }
 
+// a node-range shard's marks in one pass over its in-edges (mignn.dist.
+// RangeLayout): ghost_mark[src] = 1 for a source outside [lo, hi) (the ghost
+// ids), boundary_mark[dst - lo] = 1 for an owned destination with such a
+// source, bad[0] / bad[1] = 1 for a destination outside [lo, hi) / a source
+// outside [0, N) (those edges mark nothing).  Same-value plain stores.
+__global__ void range_mark_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t lo,
+                                  int64_t hi, int64_t N, int32_t* __restrict__ ghost_mark,
+                                  int8_t* __restrict__ boundary_mark, int32_t* __restrict__ bad) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = ei[e], d = ei[E + e];
+        const bool dok = d >= lo && d < hi, sok = s >= 0 && s < N;
+        if (!dok) bad[0] = 1;
+        if (!sok) bad[1] = 1;
+        if (dok && sok && (s < lo || s >= hi)) {
+            ghost_mark[s] = 1;
+            boundary_mark[d - lo] = 1;
+        }
+    }
+}
+
 // a node-range shard's local edge list (mignn.dist.RangeLayout): source ids
 // in [lo, hi) -> the owned row's local position inv[id - lo], others (ghosts)
 // -> n_own + the ghost's rank among the ghost ids (ghost_rank[id] - 1: the
@@ -560,6 +581,17 @@ extern "C" int mignn_csr_build_gcn(const int64_t* edge_index, int64_t E, int64_t
         if ((rc = launch_status("csr_info_kernel"))) return rc;
     }
     return MIGNN_OK;
+}
+
+extern "C" int mignn_range_mark(const int64_t* edge_index, int64_t E, int64_t lo, int64_t hi,
+                                int64_t N, int32_t* ghost_mark, int8_t* boundary_mark,
+                                int32_t* bad, void* stream) {
+    MIGNN_REQUIRE(E >= 0 && lo >= 0 && hi >= lo && N >= hi, "range_mark: bad sizes");
+    if (E == 0) return MIGNN_OK;
+    MIGNN_REQUIRE(edge_index && ghost_mark && boundary_mark && bad, "range_mark: null pointer");
+    hipLaunchKernelGGL(range_mark_kernel, dim3(grid_for(E, kBlock, 8192)), dim3(kBlock), 0,
+                       as_stream(stream), edge_index, E, lo, hi, N, ghost_mark, boundary_mark, bad);
+    return launch_status("range_mark_kernel");
 }
 
 extern "C" int mignn_range_relabel(const int64_t* edge_index, int64_t E, int64_t lo, int64_t hi,

@@ -97,6 +97,7 @@ SIGNATURES = {
                                           c_size_t, _P]),
     "mignn_gcn_layer0_coords": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,
                                         c_int, _P, c_int64, _P]),
+    "mignn_range_mark": (c_int, [_P, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P]),
     "mignn_range_relabel": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, c_int64, _P, _P]),
     "mignn_gcn_layer0_codes": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,
                                        c_int64, _P]),

@@ -83,32 +83,41 @@ class RangeLayout:
             # (checked before any device indexing: a rank that owns no rows
             # cannot own a destination either)
             raise ValueError("edge_index holds an edge whose destination this rank does not own")
-        own_src = (src >= lo) & (src < hi)
-        # ghost marks over the global ids (+1 dummy slot for owned sources)
+        # ghost marks over the global ids (+1 dummy slot), boundary marks over
+        # the owned rows, id checks: one native pass on the device
         mark = torch.zeros(N + 1, dtype=torch.int32, device=dev)
-        if E:
-            mark.index_fill_(0, torch.where(own_src, torch.full_like(src, N), src.clamp(0, N)), 1)
+        bmark = torch.zeros(self.n_own + 1, dtype=torch.int8, device=dev)
+        if dev.type == "cuda":
+            from . import _lib
+            bad = torch.zeros(2, dtype=torch.int32, device=dev)
+            if E:
+                ei64 = edge_index if (edge_index.dtype == torch.int64 and edge_index.is_contiguous()) \
+                    else torch.stack([src, dst])
+                _lib.check(_lib.lib().mignn_range_mark(
+                    _lib.ptr(ei64), E, lo, hi, N, _lib.ptr(mark), _lib.ptr(bmark), _lib.ptr(bad),
+                    _lib.stream(dev)), "mignn_range_mark")
+            bad_dst, bad_src = bad[0].bool(), bad[1].bool()
+        else:
+            own_src = (src >= lo) & (src < hi)
+            if E:
+                mark.index_fill_(0, torch.where(own_src, torch.full_like(src, N), src.clamp(0, N)), 1)
+                # (a flag fill through a dummy slot: an index_add over every
+                # edge serialised on a mesh's runs of equal destinations)
+                bmark.index_fill_(0, torch.where(own_src, torch.full_like(dst, self.n_own),
+                                                 (dst - lo).clamp(0, max(self.n_own, 0))), 1)
+                dmin, dmax = torch.aminmax(dst)
+                smin, smax = torch.aminmax(src)
+                bad_dst, bad_src = (dmin < lo) | (dmax >= hi), (smin < 0) | (smax >= N)
+            else:
+                bad_dst = bad_src = torch.zeros((), dtype=torch.bool, device=dev)
         mark[N] = 0
         csum = torch.cumsum(mark, 0)
         b = torch.tensor(self.bounds, dtype=torch.int64, device=dev)
         ends = torch.where(b > 0, csum[(b - 1).clamp(min=0)], torch.zeros_like(b))
         counts = ends[1:] - ends[:-1]                        # ghosts per owner rank
-        # boundary rows: owned destinations with a ghost source (a flag fill
-        # through a dummy slot for the own-source edges: no atomics -- an
-        # index_add over every edge serialised on a mesh's runs of equal
-        # destinations, 2 ms per 60M edges)
-        bmark = torch.zeros(self.n_own + 1, dtype=torch.int8, device=dev)
-        if E:
-            bmark.index_fill_(0, torch.where(own_src, torch.full_like(dst, self.n_own),
-                                             (dst - lo).clamp(0, max(self.n_own, 0))), 1)
+        # boundary rows: owned destinations with a ghost source
         boundary = bmark[:self.n_own] > 0
         # every host-side size in ONE device->host transfer
-        if E:
-            dmin, dmax = torch.aminmax(dst)
-            smin, smax = torch.aminmax(src)
-            bad_dst, bad_src = (dmin < lo) | (dmax >= hi), (smin < 0) | (smax >= N)
-        else:
-            bad_dst = bad_src = torch.zeros((), dtype=torch.bool, device=dev)
         host = torch.cat([torch.stack([bad_dst.long(), bad_src.long(), (~boundary).sum()]),
                           counts]).cpu().tolist()
         if host[0]:
@@ -134,7 +143,8 @@ class RangeLayout:
             # marked invalid (-1, skipped by the estimate)
             ns = min(E, 1 << 18)
             idx = (torch.arange(ns, device=dev) * E) // max(ns, 1)
-            s_loc = torch.where(own_src[idx], src[idx] - lo, torch.full_like(idx, -1))
+            s_i = src[idx]
+            s_loc = torch.where((s_i >= lo) & (s_i < hi), s_i - lo, torch.full_like(idx, -1))
             got = order_fn(pos, torch.stack([s_loc, dst[idx] - lo]))
             if isinstance(got, tuple):
                 got, self.order_info = got
@@ -163,6 +173,7 @@ class RangeLayout:
                 _lib.ptr(ei64), E, lo, hi, _lib.ptr(self.inv), _lib.ptr(csum), self.n_own,
                 _lib.ptr(self.edge_index), _lib.stream(dev)), "mignn_range_relabel")
         else:
+            own_src = (src >= lo) & (src < hi)
             lsrc = torch.where(own_src, self.inv[(src - lo).clamp(0, max(self.n_own - 1, 0))],
                                self.n_own - 1 + csum[src.clamp(0, N)])
             self.edge_index = torch.stack([lsrc, self.inv[dst - lo]])

@@ -657,6 +657,14 @@ int mignn_gat_train_backward(const int32_t* row_ptr, const int32_t* col, const i
 /* dst[r, :] = src[idx[r], :] for r < n (halo pack / unpack by index list) */
 int mignn_rows_gather(const float* src, int64_t lds, const int32_t* idx, int64_t n, int h,
                       float* dst, int64_t ldd, void* stream);
+/* A node-range shard's marks in one pass over its in-edges edge_index [2, E]
+ * (global ids; mignn.dist.RangeLayout): ghost_mark[src] = 1 (int32 [N],
+ * zeroed by the caller) for every source outside [lo, hi), boundary_mark[dst
+ * - lo] = 1 (int8 [hi - lo]) for its destination, bad[0] = 1 if a
+ * destination lies outside [lo, hi), bad[1] = 1 if a source lies outside
+ * [0, N) (int32 [2], zeroed; such edges mark nothing). */
+int mignn_range_mark(const int64_t* edge_index, int64_t E, int64_t lo, int64_t hi, int64_t N,
+                     int32_t* ghost_mark, int8_t* boundary_mark, int32_t* bad, void* stream);
 /* A node-range shard's local edge list (mignn.dist.RangeLayout; the caller
  * has validated the ids): edge_index [2, E] global ids, destinations in
  * [lo, hi).  out [2, E]: a source in [lo, hi) -> inv[src - lo], any other
