@@ -193,10 +193,10 @@ def main():
     else:
         # contiguous node ranges of the 250 x 200 x (200 N) mesh (natural order:
         # k-slabs), this rank's in-edges with global ids, RCCL halo exchange.
-        # The partition layout (ghost lists, interior-first locality order,
-        # send lists) is built once, outside the timed loop; each timed step
-        # rebuilds the rank-local CSR + GCN weights (with the ghost-degree
-        # exchange) as the N = 1 step rebuilds its CSR from edge_index
+        # Each timed step (graph cache off, as at N = 1) rebuilds the partition
+        # layout (ghost lists, interior-first locality order, send lists) and
+        # the rank-local CSR + GCN weights (with the ghost-degree exchange), as
+        # the N = 1 step rebuilds its order and CSR from edge_index
         x, ei = grid_graph(nx, ny, nz * world, device=dev, z_begin=rank * nz, z_count=nz)
         E_local = ei.shape[1]
         N_local = x.shape[0]
