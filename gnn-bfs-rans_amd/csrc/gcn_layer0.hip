@@ -66,17 +66,24 @@ __device__ __forceinline__ void layer0_gather(const int32_t* __restrict__ row_pt
     constexpr int kU = 8;
     int32_t jj[kU];
     float ww[kU];
-#pragma unroll
-    for (int k = 0; k < kU; ++k) {
-        jj[k] = e0 + k < e1 ? col[e0 + k] : 0;
-        ww[k] = e0 + k < e1 ? ew[e0 + k] : 0.f;
-    }
     float pv[kU][D];
+    if (e1 > e0) {
+        // the first kU entries' loads unconditional, past the row's end
+        // clamped to its last entry (valid ids, values unused): no
+        // per-entry branches between them -- one round trip per stage
 #pragma unroll
-    for (int k = 0; k < kU; ++k) {
-        if (e0 + k < e1) {
-            layer0_pos<D, V4>(pos, ldp, jj[k], pv[k]);
-        } else {
+        for (int k = 0; k < kU; ++k) {
+            const int32_t ek = e0 + k < e1 ? e0 + k : e1 - 1;
+            jj[k] = col[ek];
+            ww[k] = ew[ek];
+        }
+#pragma unroll
+        for (int k = 0; k < kU; ++k) layer0_pos<D, V4>(pos, ldp, jj[k], pv[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            jj[k] = 0;
+            ww[k] = 0.f;
 #pragma unroll
             for (int a = 0; a < D; ++a) pv[k][a] = 0.f;
         }
