@@ -531,11 +531,23 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
         const bool small = deg <= 8;
         int cj[8];
         uint32_t wj[8];
+        if (small && deg > 0) {
+            // (loads unconditional, past the row's end clamped to its last
+            // entry: no per-entry branches between them)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const bool v = small && e < deg;
-            cj[e] = v ? col[e0 + e] : -1;
-            wj[e] = v ? __float_as_uint(ew[e0 + e]) : 0u;
+            for (int e = 0; e < 8; ++e) {
+                const int ek = e0 + (e < deg ? e : deg - 1);
+                const int cv = col[ek];
+                const uint32_t wv = __float_as_uint(ew[ek]);
+                cj[e] = e < deg ? cv : -1;
+                wj[e] = e < deg ? wv : 0u;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                cj[e] = -1;
+                wj[e] = 0u;
+            }
         }
         // pass 1: ext entries of the row
         int next = 0, nA = 0;
