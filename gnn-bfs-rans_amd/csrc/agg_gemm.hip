@@ -1395,8 +1395,19 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     const int e0 = row_ptr[rowc];
     const int deg = rv ? row_ptr[rowc + 1] - e0 : 0;
     int cj[AS];
+    // (the slots' loads unconditional -- past the row's end clamped to its
+    // last entry, values unused -- so the chain CSR -> logit -> row has no
+    // per-entry branches between its loads)
+    if (deg > 0) {
 #pragma unroll
-    for (int e = 0; e < AS; ++e) cj[e] = e < deg ? col[e0 + e] : -1;
+        for (int e = 0; e < AS; ++e) {
+            const int cv = col[e0 + (e < deg ? e : deg - 1)];
+            cj[e] = e < deg ? cv : -1;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < AS; ++e) cj[e] = -1;
+    }
     const bool extra = __builtin_amdgcn_ballot_w64(deg > AS) != 0ull;
     auto leaky = [&](float v) { return v > 0.f ? v : v * slope; };
     float* const AL = reinterpret_cast<float*>(lds + C::OFF_AL) + ((wave * 16 + r) * 4) * 8;
@@ -1472,7 +1483,8 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
 #pragma unroll
     for (int e = 0; e < AS; ++e) {
         if constexpr (L0) break;
-        sc[e] = cj[e] >= 0 ? leaky(logits[static_cast<int64_t>(cj[e]) * (2 * HEADS) + g] + ad) : -INFINITY;
+        const float lv = logits[static_cast<int64_t>(cj[e] >= 0 ? cj[e] : rowc) * (2 * HEADS) + g];
+        sc[e] = cj[e] >= 0 ? leaky(lv + ad) : -INFINITY;
         mx = fmaxf(mx, sc[e]);
     }
     if (extra && !L0)
