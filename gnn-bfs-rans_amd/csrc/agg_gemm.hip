@@ -364,12 +364,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
     for (int k = 0; k < ES; ++k) xc[k] = -1;
     int next = 0;
+    // (the slots' loads unconditional, past the row's end clamped to its last
+    // entry -- values unused -- so no per-entry branch separates them)
+    int cl[AS];
+    float wl[AS];
 #pragma unroll
     for (int e = 0; e < AS; ++e) {
-        const int c = e < deg ? col[e0 + e] : -1;
+        const int ek = e0 + (e < deg ? e : (deg > 0 ? deg - 1 : 0));
+        cl[e] = deg > 0 ? col[ek] : -1;
+        wl[e] = (MODE == AGG_GCN && deg > 0) ? ew[ek] : 1.f;
+    }
+#pragma unroll
+    for (int e = 0; e < AS; ++e) {
+        const int c = e < deg ? cl[e] : -1;
         // (GIN: weight 1 -- the sum as FMAs, so an empty slot is a weight-0
         // read of the row's own x_i, finite whenever the output is: no select)
-        wgt[e] = e < deg ? (MODE == AGG_GCN ? ew[e0 + e] : 1.f) : 0.f;
+        wgt[e] = e < deg ? wl[e] : 0.f;
         const uint32_t off = static_cast<uint32_t>(c - static_cast<int>(t0));
         if (c < 0) {
             code[e] = -1;
