@@ -65,14 +65,37 @@ __global__ void order_init_kernel(OrderStats* st) {
 __global__ __launch_bounds__(kB) void bbox_kernel(const float* __restrict__ pos, int64_t ldp,
                                                   int64_t n, OrderStats* st) {
     unsigned int lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
-    for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kB) {
+    auto upd = [&](int a, float v) {
+        if (v == v) {   // NaN-free
+            lo[a] = min(lo[a], f2ord(v));
+            hi[a] = max(hi[a], f2ord(v));
+        }
+    };
+    const int64_t stride = (int64_t)gridDim.x * kB;
+    if (ldp == 3 && (reinterpret_cast<uintptr_t>(pos) & 15u) == 0) {
+        // dense [n, 3]: the 3n floats as 16-B loads (the row-wise form read
+        // each row with three 4-B loads at a 12-B stride), axis = index % 3
+        const int64_t nf = 3 * n, nq = nf / 4;
+        for (int64_t q = blockIdx.x * (int64_t)kB + threadIdx.x; q < nq; q += stride) {
+            const float4 v = ld4(pos + 4 * q);
+            int a = static_cast<int>((4 * q) % 3);
+            const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float v = pos[i * ldp + a];
-            if (v == v) {   // NaN-free
-                lo[a] = min(lo[a], f2ord(v));
-                hi[a] = max(hi[a], f2ord(v));
+            for (int k = 0; k < 4; ++k) {
+                // (a is 0, 1 or 2: unrolled selects keep lo / hi in registers)
+                const float x = e[k];
+                if (a == 0) upd(0, x); else if (a == 1) upd(1, x); else upd(2, x);
+                a = a == 2 ? 0 : a + 1;
             }
+        }
+        for (int64_t f = 4 * nq + blockIdx.x * (int64_t)kB + threadIdx.x; f < nf; f += stride) {
+            const int a = static_cast<int>(f % 3);
+            if (a == 0) upd(0, pos[f]); else if (a == 1) upd(1, pos[f]); else upd(2, pos[f]);
+        }
+    } else {
+        for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < n; i += stride) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) upd(a, pos[i * ldp + a]);
         }
     }
     __shared__ unsigned int s_lo[3], s_hi[3];
