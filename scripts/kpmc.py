@@ -1,6 +1,8 @@
 """Short PMC target (round 4): the hot-kernel candidates on the bench mesh
 (250x200x200, locality order, H = KP_H), each launched KP_REPS times, nothing
-else -- run under `rocprofv3 --pmc ...` (scripts/gpu_kpmc.sh)."""
+else -- run under `rocprofv3 --pmc ...` (scripts/gpu_kpmc.sh).  KP_KINDS:
+pc, ring, win, winagg, wincodes (the codes form, MODE 64), windiag, gin, tf,
+gat."""
 import os
 import sys
 
@@ -32,7 +34,7 @@ b = torch.randn(H, device=dev, generator=g) * 0.05
 sc = torch.rand(H, device=dev, generator=g) + 0.5
 sh = torch.randn(H, device=dev, generator=g) * 0.1
 Y = torch.empty_like(X)
-if "win" in kinds or "winagg" in kinds or "windiag" in kinds:
+if "win" in kinds or "winagg" in kinds or "windiag" in kinds or "wincodes" in kinds:
     # the window kernel on the column-order CSR of the same mesh
     _pos, _ei = grid_graph(250, 200, 200, device=dev)
     _, inv_c, info_c = locality_order(_pos, _ei, cols=True)
@@ -42,6 +44,12 @@ if "win" in kinds or "winagg" in kinds or "windiag" in kinds:
     wplan = torch.empty(nbw, dtype=torch.uint8, device=dev)
     _lib.check(L.mignn_gcn_win_plan(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), 0, n, H, P(info_c),
                                     P(wplan), nbw, None, st), "wp")
+if "wincodes" in kinds:
+    # the codes form of the window kernel (layer 1 from layer-0 row codes):
+    # codes [n, 8] (last column 0) and an expansion table [H][8]
+    CODES = torch.rand(n, 8, device=dev, generator=g)
+    CODES[:, 7] = 0.0
+    XCOEF = torch.randn(H, 8, device=dev, generator=g) * 0.5
 if "ring" in kinds:
     nbr = L.mignn_gcn_ring_plan_bytes(0, n, H)
     rplan = torch.empty(nbr, dtype=torch.uint8, device=dev)
@@ -88,6 +96,10 @@ for _ in range(reps):
     if "win" in kinds:
         _lib.check(L.mignn_gcn_layer_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X), H,
                                          0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Y), H, st), "win")
+    if "wincodes" in kinds:
+        _lib.check(L.mignn_gcn_layer_win_codes(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
+                                               P(CODES), 8, 0, n, H, P(XCOEF), P(W), P(b), P(sc),
+                                               P(sh), 15, P(Y), H, st), "wincodes")
     if "winagg" in kinds:
         _lib.check(L.mignn_gcn_aggregate_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
                                              H, 0, n, H, P(Y), H, st), "winagg")
