@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 
 #include "../../include/mignn.h"
 #include "../../include/mignn_diag.h"
@@ -34,6 +35,53 @@ inline int launch_status(const char* what) {
             return MIGNN_ERR_ARG;                 \
         }                                         \
     } while (0)
+
+// Host-side record of the planned kernels' plans (window / ring): the
+// header fields a launch must match -- grid, width, row range, device --
+// registered when a plan is built, checked before a launch so that a plan
+// used with another range, width or device returns MIGNN_ERR_ARG instead of
+// launching (the kernel's own header check remains, for plans this process
+// did not build: error bit + NaN rows).  A small table keyed by the plan
+// pointer; a pointer that is not in it (evicted, foreign) is not checked.
+struct PlanRecord {
+    const void* plan;
+    int kind, G, h, dev;
+    int64_t rb, re;
+};
+struct PlanRegistry {
+    std::mutex mu;
+    PlanRecord table[512] = {};
+    int slot = 0;
+};
+inline PlanRegistry& plan_registry() {
+    static PlanRegistry r;
+    return r;
+}
+inline void plan_registry_put(const PlanRecord& r) {
+    PlanRegistry& g = plan_registry();
+    std::lock_guard<std::mutex> lk(g.mu);
+    for (PlanRecord& t : g.table)
+        if (t.plan == r.plan && t.kind == r.kind) {
+            t = r;
+            return;
+        }
+    g.table[g.slot] = r;
+    g.slot = (g.slot + 1) % 512;
+}
+// 1: matching, or not registered; 0: registered with other header fields
+inline int plan_registry_check(const void* plan, int kind, int G, int h, int dev, int64_t rb,
+                               int64_t re) {
+    PlanRegistry& g = plan_registry();
+    std::lock_guard<std::mutex> lk(g.mu);
+    for (const PlanRecord& t : g.table)
+        if (t.plan == plan && t.kind == kind)
+            return t.G == G && t.h == h && t.dev == dev && t.rb == rb && t.re == re;
+    return 1;
+}
+inline int current_device() {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
 
 #define MIGNN_HIP(call)                                                        \
     do {                                                                       \
@@ -144,6 +192,18 @@ __device__ __forceinline__ float4 fma4(float s, float4 x, float4 acc) {
 //   v = acc + bias; v = residual + v; v = v*scale + shift; relu.
 // ReLU in one v_maximum3_f32: NaN-propagating, like torch.relu (-0 -> +0)
 __device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.0f); }
+
+// A planned layer launch whose plan header does not match it: besides the
+// device error bit, every output row of the launch's range becomes NaN (the
+// whole grid, grid-stride, vector stores) -- a caller that does not read the
+// error word still cannot take the buffer's old contents for layer output.
+__device__ inline void plan_mismatch_fill(float* out, int64_t ldo, int64_t rb, int64_t re, int h) {
+    const float qnan = __builtin_nanf("");
+    const int64_t n = (re - rb) * static_cast<int64_t>(h);
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        out[(rb + i / h) * ldo + i % h] = qnan;
+}
 
 __device__ __forceinline__ float epilogue(float acc, int flags, float bias, float res, float sc,
                                           float sh) {

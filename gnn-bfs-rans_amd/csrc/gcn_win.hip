@@ -688,6 +688,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             if (tid == 0)
                 __hip_atomic_fetch_or(&g_win_errors, static_cast<unsigned>(MIGNN_DEVERR_PLAN),
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            plan_mismatch_fill(out, ldo, rb, re, H);
             return;
         }
     }
@@ -1521,6 +1522,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
             if (tid == 0)
                 __hip_atomic_fetch_or(&g_win_errors, static_cast<unsigned>(MIGNN_DEVERR_PLAN),
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            plan_mismatch_fill(out, ldo, rb, re, H);
             return;
         }
     }
@@ -1964,6 +1966,10 @@ int launch_win(int h, const void* plan, const int32_t* row_ptr, const int32_t* c
     const int64_t ntiles = (re - rb + 63) / 64;
     const int G = win_grid(ntiles, h == 128 ? WCfg<128>::WGPC : WCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_win: device query failed");
+    MIGNN_REQUIRE(plan_registry_check(plan, 1, G, h, current_device(), rb, re),
+                  "gcn_win: the plan was built for another row range, width or device "
+                  "(launch h=%d rows [%lld, %lld) grid %d)", h, static_cast<long long>(rb),
+                  static_cast<long long>(re), G);
     if (h == 128)
         launch_win_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, xcoef);
     else if constexpr ((MODE & 64) == 0)
@@ -2022,6 +2028,7 @@ extern "C" int mignn_gcn_win_plan(const int32_t* row_ptr, const int32_t* col, co
     hipLaunchKernelGGL(win_hdr_kernel, dim3(1), dim3(64), 0, st, hdr, order_info, ntiles, G, h, rb, re);
     int rc = launch_status("win_hdr_kernel");
     if (rc) return rc;
+    plan_registry_put(PlanRecord{plan, 1, G, h, current_device(), rb, re});
     unsigned char* tabs = static_cast<unsigned char*>(plan) + kWHdr;
     const unsigned grid = static_cast<unsigned>(ntiles < (1 << 20) ? ntiles : (1 << 20));
     if (h == 128)

@@ -16,10 +16,11 @@ from ctypes import c_float, c_int, c_int64, c_size_t, c_void_p
 import torch  # noqa: F401  (must precede loading libmignn.so)
 
 LIB_NAME = "libmignn.so"
-# (MIGNN_LIB_VARIANT: a variant build of the same library for A/B timing
-# studies -- scripts only; the product loads the in-tree build)
-LIB_PATH = os.environ.get("MIGNN_LIB_VARIANT") or os.path.join(
-    os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# A/B timing scripts (scripts/gpu_ab.sh, gpu_legab.sh) point this at a variant
+# build of the same sources; lib() then loads it with a warning on stderr and
+# the same ABI-version check.  The product path never sets it.
+VARIANT_ENV = "MIGNN_LIB_VARIANT"
 
 EPI_BIAS, EPI_RESIDUAL, EPI_AFFINE, EPI_RELU = 1, 2, 4, 8
 CSR_VERBATIM, CSR_ONE_SELF_LOOP, CSR_TRANSPOSE = 0, 1, 4
@@ -232,7 +233,12 @@ def lib():
     .so is missing."""
     global _lib
     if _lib is None:
-        _lib = _load(LIB_PATH, SIGNATURES)
+        path = os.environ.get(VARIANT_ENV) or LIB_PATH
+        if path != LIB_PATH:
+            import sys
+            print(f"mignn: {VARIANT_ENV} set -- loading the variant library {path} "
+                  f"instead of {LIB_PATH} (A/B timing only)", file=sys.stderr)
+        _lib = _load(path, SIGNATURES)
     return _lib
 
 

@@ -66,7 +66,15 @@ class RangeLayout:
     order), used only to pick the locality order via `order_fn(pos, ei)`
     -> perm (local position -> owned offset), or (perm, info) for the
     column order (mignn_locality_order_cols' info, kept as `order_info`: the
-    window GCN kernel's route on the rank-local CSR)."""
+    window GCN kernel's route on the rank-local CSR).
+
+    The `ei` handed to `order_fn` is NOT this rank's adjacency: it is a
+    strided sample of at most 2^18 of its edges ([2, <= 2^18], int64, local
+    owned offsets), and an edge whose source is a ghost has its source set to
+    -1.  The locality orders only estimate the mesh spacing from it
+    (mignn_locality_order skips the -1 entries).  An order_fn that needs the
+    full owned-to-owned adjacency (RCM, a graph partitioner) must not rely on
+    it: build that from `edge_index` before constructing the layout."""
 
     def __init__(self, edge_index: torch.Tensor, bounds: Sequence[int], rank: int,
                  requests: "RequestExchange", pos: Optional[torch.Tensor] = None,
@@ -294,9 +302,11 @@ class DistExchange:
     def __init__(self, group=None):
         self.group = group
         self._staged = None
-        # per-peer pack buffers, allocated once per (peer, width, dtype,
-        # device) and reused by every layer (a layer's sends complete --
-        # wait() -- before the next layer packs)
+        # per-peer pack buffers, one per (peer, width, dtype, device), grown
+        # when a layout needs more rows and handed out as a view of the first
+        # n rows -- reused by every layer (a layer's sends complete -- wait()
+        # -- before the next layer packs), and by rebuilt layouts of other
+        # sizes without a buffer per distinct ghost count
         self._pack: Dict[tuple, torch.Tensor] = {}
 
     def _stage(self, buf) -> bool:
@@ -305,11 +315,11 @@ class DistExchange:
         return self._staged and buf.is_cuda
 
     def _pack_buf(self, q, n, buf):
-        key = (q, n, buf.shape[1], buf.dtype, str(buf.device))
+        key = (q, buf.shape[1], buf.dtype, str(buf.device))
         pk = self._pack.get(key)
-        if pk is None:
+        if pk is None or pk.shape[0] < n:
             pk = self._pack[key] = torch.empty((n, buf.shape[1]), dtype=buf.dtype, device=buf.device)
-        return pk
+        return pk[:n]
 
     def start(self, shards, bufs, tag: int = TAG_HALO):
         (sh,), (buf,) = shards, bufs
