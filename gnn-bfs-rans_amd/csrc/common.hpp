@@ -6,7 +6,6 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
-#include <mutex>
 
 #include "../../include/mignn.h"
 #include "../../include/mignn_diag.h"
@@ -36,52 +35,6 @@ inline int launch_status(const char* what) {
         }                                         \
     } while (0)
 
-// Host-side record of the planned kernels' plans (window / ring): the
-// header fields a launch must match -- grid, width, row range, device --
-// registered when a plan is built, checked before a launch so that a plan
-// used with another range, width or device returns MIGNN_ERR_ARG instead of
-// launching (the kernel's own header check remains, for plans this process
-// did not build: error bit + NaN rows).  A small table keyed by the plan
-// pointer; a pointer that is not in it (evicted, foreign) is not checked.
-struct PlanRecord {
-    const void* plan;
-    int kind, G, h, dev;
-    int64_t rb, re;
-};
-struct PlanRegistry {
-    std::mutex mu;
-    PlanRecord table[512] = {};
-    int slot = 0;
-};
-inline PlanRegistry& plan_registry() {
-    static PlanRegistry r;
-    return r;
-}
-inline void plan_registry_put(const PlanRecord& r) {
-    PlanRegistry& g = plan_registry();
-    std::lock_guard<std::mutex> lk(g.mu);
-    for (PlanRecord& t : g.table)
-        if (t.plan == r.plan && t.kind == r.kind) {
-            t = r;
-            return;
-        }
-    g.table[g.slot] = r;
-    g.slot = (g.slot + 1) % 512;
-}
-// 1: matching, or not registered; 0: registered with other header fields
-inline int plan_registry_check(const void* plan, int kind, int G, int h, int dev, int64_t rb,
-                               int64_t re) {
-    PlanRegistry& g = plan_registry();
-    std::lock_guard<std::mutex> lk(g.mu);
-    for (const PlanRecord& t : g.table)
-        if (t.plan == plan && t.kind == kind)
-            return t.G == G && t.h == h && t.dev == dev && t.rb == rb && t.re == re;
-    return 1;
-}
-inline int current_device() {
-    int d = -1;
-    return hipGetDevice(&d) == hipSuccess ? d : -1;
-}
 
 #define MIGNN_HIP(call)                                                        \
     do {                                                                       \

@@ -288,4 +288,85 @@ extern "C" int mignn_diag_clock(int blocks, int iters, int64_t* out, void* strea
     return launch_status("clock_probe_kernel");
 }
 
+// ---- v_pk_fma_f32 forms of the row-code expansion.
+// out[i][f] = relu(coef[f][7] + sum_{k<7} coef[f][k] v[i][k]) as layer 0's
+// fma chain (gcn_layer0.hip, gcn_win.hip expand4), one lane per (row, feature
+// pair f, f + 1):
+//   form 0  scalar v_fma_f32 chain (the reference the other forms must equal bitwise)
+//   form 1  inline v_pk_fma_f32, the input broadcast to both halves by
+//           op_sel_hi:[1,0,1] (the high result takes src1's LOW half)
+//   form 2  the same instruction without the op_sel_hi modifier (its
+//           default, op_sel_hi:[1,1,1]): the high result takes src1's HIGH
+//           half -- with the inputs loaded as pairs {v[k], v[k+1]} that is
+//           the neighbouring input, so feature f + 1 is wrong in every row
+//   form 3  the packed form the compiler emits itself (__builtin_elementwise_fma
+//           on 2-vectors)
+namespace {
+template <int FORM>
+__global__ __launch_bounds__(256) void pk_fma_kernel(const float* __restrict__ codes, int64_t n,
+                                                     const float* __restrict__ coef, int h,
+                                                     float* __restrict__ out) {
+    const int pairs = h / 2;
+    for (int64_t id = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; id < n * pairs;
+         id += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t i = id / pairs;
+        const int f = 2 * static_cast<int>(id % pairs);
+        const float* v = codes + i * 8;
+        const float* c0 = coef + f * 8;
+        const float* c1 = coef + (f + 1) * 8;
+        float r0, r1;
+        if constexpr (FORM == 0) {
+            float t0 = c0[7], t1 = c1[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                // (explicit v_fma_f32: plain fmaf here is SLP-packed into
+                // v_pk_fma_f32 by the compiler, which is form 3's subject)
+                asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(t0) : "v"(c0[k]), "v"(v[k]));
+                asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(t1) : "v"(c1[k]), "v"(v[k]));
+            }
+            r0 = t0;
+            r1 = t1;
+        } else if constexpr (FORM == 3) {
+            f32x2 t = f32x2{c0[7], c1[7]};
+#pragma unroll
+            for (int k = 0; k < 7; ++k)
+                t = __builtin_elementwise_fma(f32x2{c0[k], c1[k]}, f32x2{v[k], v[k]}, t);
+            r0 = t[0];
+            r1 = t[1];
+        } else {
+            f32x2 t = f32x2{c0[7], c1[7]};
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                const f32x2 cp = f32x2{c0[k], c1[k]};
+                const f32x2 vp = f32x2{v[k], v[k + 1]};   // inputs as loaded: a pair
+                if constexpr (FORM == 1)
+                    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(t) : "v"(cp), "v"(vp));
+                else
+                    asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(t) : "v"(cp), "v"(vp));
+            }
+            r0 = t[0];
+            r1 = t[1];
+        }
+        out[i * h + f] = relu_nan(r0);
+        out[i * h + f + 1] = relu_nan(r1);
+    }
+}
+}  // namespace
+
+extern "C" int mignn_diag_pk_fma(int form, const float* codes, int64_t n, const float* coef, int h,
+                                 float* out, void* stream) {
+    MIGNN_REQUIRE(codes && coef && out && n >= 0 && h > 0 && h % 2 == 0, "diag_pk_fma: bad args");
+    if (n == 0) return MIGNN_OK;
+    const unsigned g = static_cast<unsigned>(grid_for(n * (h / 2), 256, 4096));
+    hipStream_t st = as_stream(stream);
+    switch (form) {
+        case 0: hipLaunchKernelGGL(pk_fma_kernel<0>, dim3(g), dim3(256), 0, st, codes, n, coef, h, out); break;
+        case 1: hipLaunchKernelGGL(pk_fma_kernel<1>, dim3(g), dim3(256), 0, st, codes, n, coef, h, out); break;
+        case 2: hipLaunchKernelGGL(pk_fma_kernel<2>, dim3(g), dim3(256), 0, st, codes, n, coef, h, out); break;
+        case 3: hipLaunchKernelGGL(pk_fma_kernel<3>, dim3(g), dim3(256), 0, st, codes, n, coef, h, out); break;
+        default: set_error("diag_pk_fma: form 0..3"); return MIGNN_ERR_ARG;
+    }
+    return launch_status("pk_fma_kernel");
+}
+
 #endif  // MIGNN_DIAG

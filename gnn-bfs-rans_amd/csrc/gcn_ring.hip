@@ -997,10 +997,6 @@ int launch_ring(int h, const void* plan, const int32_t* row_ptr, const int32_t* 
     const int64_t ntiles = (re - rb + bm - 1) / bm;
     const int G = ring_grid(ntiles, h == 128 ? RCfg<128>::WGPC : RCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_ring: device query failed");
-    MIGNN_REQUIRE(plan_registry_check(plan, 2, G, h, current_device(), rb, re),
-                  "gcn_ring: the plan was built for another row range, width or device "
-                  "(launch h=%d rows [%lld, %lld) grid %d)", h, static_cast<long long>(rb),
-                  static_cast<long long>(re), G);
     if (h == 128)
         launch_ring_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo);
     else
@@ -1049,7 +1045,6 @@ extern "C" int mignn_gcn_ring_plan(const int32_t* row_ptr, const int32_t* col, c
     const int G = ring_grid(ntiles, h == 128 ? RCfg<128>::WGPC : RCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_ring_plan: device query failed");
     const unsigned grid = static_cast<unsigned>(ntiles < (1 << 20) ? ntiles : (1 << 20));
-    plan_registry_put(PlanRecord{plan, 2, G, h, current_device(), rb, re});
     if (h == 128)
         hipLaunchKernelGGL(ring_plan_kernel<128>, dim3(grid), dim3(RCfg<128>::BM), 0, as_stream(stream), row_ptr,
                            col, ew, rb, re, ntiles, G, static_cast<unsigned char*>(plan), stats);

@@ -59,32 +59,16 @@ using f16x8w = __attribute__((ext_vector_type(8))) _Float16;
 using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 
 // A-fragment prefetch depth of the H = 128 transform, in t-steps of 3 MFMAs
-// (10M-row layer: PD 1 2.87 ms, 2 2.72, 3 2.68, 5 2.67)
-// H = 128 epilogue stored from the accumulators, 16 rows x 64 B per store
-// (1), or staged over the A image for whole-row stores (0: two more block
-// barriers per step; 10M-row layer 2.92 vs 2.87 ms on one box)
-#ifndef MIGNN_WIN_DIRECT
-#define MIGNN_WIN_DIRECT 1
-#endif
-// H = 128 transform: 16-column blocks per wave (1: 8 column blocks x 64
-// rows, every wave reads the whole A image; 2: 4 column pairs x 32 rows, each
-// A fragment feeds 6 MFMAs and half the image is read per wave -- measured
-// 2.79 ms at PD 3 and 3.05 at PD 5 vs 2.78 for 1: the A-image reads are not
-// what bounds the step)
-#ifndef MIGNN_WIN_CPW
-#define MIGNN_WIN_CPW 1
-#endif
-#ifndef MIGNN_WIN_PD
-#define MIGNN_WIN_PD 5
-#endif
-// codes form: the row expansion as f32 MFMAs, every wave 16 features of
-// every row (1), or as fma chains on the VALU, every wave its own rows (0)
-#ifndef MIGNN_WIN_XMFMA
-#define MIGNN_WIN_XMFMA 1
-#endif
-// codes form: A-fragment prefetch depth (the expansion's registers beside it)
-#ifndef MIGNN_WIN_PD_X0
-#define MIGNN_WIN_PD_X0 (MIGNN_WIN_XMFMA ? 5 : 3)
+// (10M-row layer: PD 1 2.87 ms, 2 2.72, 3 2.68, 5 2.67).  Measured and
+// removed (round 6 prune): the staged whole-row epilogue at H = 128 (two
+// more block barriers per step, 2.92 vs 2.87 ms), 4 column pairs x 32 rows
+// per wave (2.79-3.05 vs 2.78 ms), the codes expansion as VALU fma chains
+// (3.14-3.27 vs the MFMA expansion's 2.71 ms).
+constexpr int kWinPD = 3;
+// the pipelined step's DMA pieces interleaved with phase B and the split (1)
+// or issued together after B1 (0)
+#ifndef MIGNN_WIN_DMAIL
+#define MIGNN_WIN_DMAIL 1
 #endif
 constexpr int kWRec = 48;                 // bytes per plan record: 8 u16 codes + 8 f32 weights
 constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the next-tile entry
@@ -126,7 +110,6 @@ struct WCfg {
     static constexpr int OFF_REXP = OFF_AL + A_BYTES;
     static constexpr int OFF_EPI = OFF_REXP + BM * 4;
     static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
-    static constexpr int OFF_STG = OFF_AH;             // output staging (fp32 rows) over AH | AL
     // layer 1 from layer-0 codes (MODE 64): per wave 8 own-row + 4 ext-row
     // codes (32 B each) DMA'd per step, the [H][8] expansion table
     static constexpr int CODEB = 32, CODE_W = (RPW + KX / NW) * CODEB;
@@ -144,7 +127,6 @@ struct WCfg {
     static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
     static_assert(LDS_BYTES_X0 * WGPC <= 160 * 1024, "LDS budget (codes form)");
     static_assert(RPW == 8 && KX / NW == 4 && CODE_W / 16 <= 64, "codes DMA: 16 own + 8 ext lanes");
-    static_assert(2 * A_BYTES >= BM * ROWB, "staging fits the A images");
     static_assert(EPW == NPE * RPP && EPW + 1 <= XLW, "ext rows per wave");
     static_assert((CODE_END >> CSH) <= 65536, "u16 codes");
     static_assert(RECW % 16 == 0 && TLANES <= 64 && TAB_BYTES % 16 == 0, "records DMA");
@@ -802,43 +784,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             for (int q = 0; q < 4; ++q) t[q] = fmaf(cf[k][q], v[k], t[q]);
         return f32x4{relu_nan(t[0]), relu_nan(t[1]), relu_nan(t[2]), relu_nan(t[3])};
     };
-    // one row of a wave's codes (r: 0..7 own, 8..11 ext) -> the lane's 4
-    // features (16-B chunk lane & 31) of LDS row `dst` (chunk swizzle sw)
-    auto expand_row = [&](const f32x4 (&cf)[8], int r, unsigned char* dst, int sw) {
-        const unsigned char* const cp = lds + C::OFF_CODE + wave * C::CODE_W + r * C::CODEB;
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(cp);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(cp + 16);
-        const float v[7] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2]};
-        const int ch = lane & 31;
-        *reinterpret_cast<f32x4*>(dst + ((ch ^ sw) << 4)) = expand4(cf, v);
-    };
-    [[maybe_unused]] auto coef_load = [&](f32x4 (&cf)[8]) {
-        const int ch = lane & 31;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            cf[k] = *reinterpret_cast<const f32x4*>(lds + C::OFF_COEF + (ch * 8 + k) * 16);
-    };
-    // the lane's i-th row of the wave's expansion: i < 4 own row 2 i + (lane
-    // >> 5) of the wave into X slot `slot`, else ext row 2 (i - 4) + (lane >> 5)
-    constexpr int NXR = C::RPW / 2 + C::EPW / 2;
-    [[maybe_unused]] auto expand_i = [&](const f32x4 (&cf)[8], int slot, int i) {
-        const int hh = lane >> 5;
-        if (i < C::RPW / 2) {
-            const int r = 2 * i + hh, o = C::RPW * wave + r;
-            expand_row(cf, r, lds + C::OFF_X + slot * C::X_BYTES + o * C::ROWB, o & 7);
-        } else {
-            const int r = 2 * (i - C::RPW / 2) + hh, k = C::EPW * wave + r;
-            expand_row(cf, C::RPW + r, lds + C::OFF_EXT + k * C::ROWB, k & 7);
-        }
-    };
-    [[maybe_unused]] auto expand = [&](int slot, bool ext) {
-        f32x4 cf[8];
-        coef_load(cf);
-#pragma unroll
-        for (int i = 0; i < NXR; ++i)
-            if (ext || i < C::RPW / 2) expand_i(cf, slot, i);
-    };
-    // ---- the expansion as f32 MFMAs (MIGNN_WIN_XMFMA): wave w computes
+    // ---- the row expansion as f32 MFMAs: wave w computes
     // features 16 w .. 16 w + 15 of every expanded row, a 16-row block per
     // v_mfma_f32_16x16x4_f32 pair (inputs 0..3, then 4..6 and a zero; the
     // accumulator starts at the constant e) -- on gfx950 an exact fma chain
@@ -851,7 +797,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     [[maybe_unused]] constexpr int NXB = (C::BM + C::KX) / 16;
     float xa0 = 0.f, xa1 = 0.f;
     f32x4 xe = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (X0 && MIGNN_WIN_XMFMA) {
+    if constexpr (X0) {
         const int f = 16 * wave + (lane & 15), kq = lane >> 4;
         xa0 = xcoef[f * 8 + kq];
         xa1 = kq < 3 ? xcoef[f * 8 + 4 + kq] : 0.f;
@@ -896,7 +842,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             *reinterpret_cast<f32x4*>(lds + C::OFF_COEF + 16 * i) = f32x4{src[0], src[8], src[16], src[24]};
         }
     const int rr0 = lane & 15, gg0 = lane >> 4;
-    constexpr int CPW = MIGNN_WIN_CPW;            // 16-column blocks per wave
+    constexpr int CPW = 1;                        // 16-column blocks per wave
     constexpr int WN = H / 16 / CPW, WM = C::NW / WN, IBW = (C::BM / 16) / WM;
     static_assert(WN * WM == C::NW && IBW * WM * 16 == C::BM, "window transform grid");
     const int wn = wave % WN, wm = wave / WN;
@@ -944,7 +890,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         dma_tab(tile_of(1), 1);
         code_dma(tile_of(0), 0, false);
         wbar<wvm(0) & kWLgkm0>();                 // (all waves), zero row, EPI, COEF
-#if MIGNN_WIN_XMFMA
 #pragma unroll
         for (int rbk = 0; rbk < C::BM / 16; ++rbk) xblock_store(0, rbk, xblock_mfma(rbk));
         wbar<kWLgkm0>();                          // every wave's CODE reads before the refill
@@ -952,13 +897,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         wbar<wvm(0) & kWLgkm0>();
 #pragma unroll
         for (int rbk = 0; rbk < NXB; ++rbk) xblock_store(1, rbk, xblock_mfma(rbk));
-#else
-        expand(0, false);
-        wwait<kWLgkm0>();                         // CODE read before it is refilled
-        code_dma(tile_of(1), 0, true);
-        wwait<wvm(0)>();
-        expand(1, true);
-#endif
     } else {
         dma_tab(tile_of(0), 0);
 #pragma unroll
@@ -974,6 +912,494 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
     }
 
+    // ---- phase A of a tile (its records in TAB slot tq, its rows in X): the
+    // in-window / ext entries from LDS in CSR order, the +z entry held back
+    // for phase B (ncn, nwn), or the CSR path for a wave with a row outside
+    // the plan's form.  mid(G), G = 0..3, runs between the slot batches (after
+    // batch G's loads, before its FMAs) -- the pipelined transform puts a
+    // quarter of the previous tile's MFMAs there; every G runs exactly once
+    // whatever the path.
+    auto phase_a = [&](int tq, int64_t t0, int64_t nloc, const unsigned char* X, bool live,
+                       f32x4 (&accn)[C::NQ][C::CH], uint32_t (&ncn)[C::NQ], float (&nwn)[C::NQ],
+                       auto&& mid) {
+#pragma unroll
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            ncn[qd] = C::OFF_ZERO >> C::CSH;
+            nwn[qd] = 0.f;
+#pragma unroll
+            for (int j = 0; j < C::CH; ++j) accn[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // (the four mid() calls sit in straight-line code, once each: copies
+        // of the MFMA groups in the branches cost ~100 spilled VGPRs)
+        const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
+        const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+            *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
+        const bool far = live && ((summ >> 8) & 1u) != 0u;
+        const int maxa = (live && !far) ? static_cast<int>(summ & 0xffu) : 0;
+        {
+            {
+                // the codes held for the whole phase; each batch's weights read
+                // with its rows (registers: the pipelined transform's
+                // fragments and accumulators are live through phase A)
+                uint4 cds[C::NQ];
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd)
+                    cds[qd] = *reinterpret_cast<const uint4*>(RW + (4 * qd + gq) * kWRec);
+                auto codeof = [&](int qd, int u) -> uint32_t {
+                    const uint32_t d = u < 2 ? cds[qd].x : u < 4 ? cds[qd].y : u < 6 ? cds[qd].z : cds[qd].w;
+                    return (u & 1) ? (d >> 16) : (d & 0xffffu);
+                };
+                auto wld = [&](int qd, int u) -> float {
+                    return *reinterpret_cast<const float*>(RW + (4 * qd + gq) * kWRec + 16 + 4 * u);
+                };
+                float wv[C::NQ][2];
+                // slots in batches of 2: loads of a batch, mid(G), then its FMAs
+                // (batches of 2: the VGPR budget of 2 waves per SIMD beside
+                // the pipelined transform's fragments)
+                f32x4 vv[C::NQ][2][C::CH];
+                auto bload = [&](auto U0, auto NB) {
+                    constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
+#pragma unroll
+                    for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                        for (int uu = 0; uu < nb; ++uu) {
+                            const uint32_t ad = decode(codeof(qd, u0 + uu));
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+                                vv[qd][uu][j] = *reinterpret_cast<const f32x4*>(lds + ad + 256 * j);
+                            wv[qd][uu] = wld(qd, u0 + uu);
+                        }
+                };
+                auto bfma = [&](auto, auto NB) {
+                    constexpr int nb = decltype(NB)::value;
+#pragma unroll
+                    for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                        for (int uu = 0; uu < nb; ++uu) {
+                            const float w = wv[qd][uu];
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(w, vv[qd][uu][j][r], accn[qd][j][r]);
+                        }
+                };
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                using I2 = std::integral_constant<int, 2>;
+                using I3 = std::integral_constant<int, 3>;
+                using I4 = std::integral_constant<int, 4>;
+                using I6 = std::integral_constant<int, 6>;
+                if (maxa > 0) bload(I0{}, I2{});
+                mid(I0{});
+                if (maxa > 0) bfma(I0{}, I2{});
+                if (maxa > 2) bload(I2{}, I2{});
+                mid(I1{});
+                if (maxa > 2) bfma(I2{}, I2{});
+                if (maxa > 4) bload(I4{}, I2{});
+                mid(I2{});
+                if (maxa > 4) bfma(I4{}, I2{});
+                if (maxa > 6) bload(I6{}, I1{});
+                mid(I3{});
+                if (maxa > 6) bfma(I6{}, I1{});
+                if (live && !far) {
+#pragma unroll
+                    for (int qd = 0; qd < C::NQ; ++qd) {
+                        ncn[qd] = codeof(qd, 7);
+                        nwn[qd] = wld(qd, 7);
+                    }
+                }
+            }
+        }
+        return far;
+    };
+    // the CSR path of phase A (a wave with a row outside the plan's form;
+    // phase_a returned true): every entry of the wave's rows in CSR order,
+    // the current tile from LDS, everything else from x (L2); the full sum
+    // (no phase B).  Run by the caller where the fewest registers are live
+    // (the pipelined step: after tile s - 2's stores)
+    auto phase_a_far = [&](int64_t t0, int64_t nloc, const unsigned char* X, f32x4 (&accn)[C::NQ][C::CH]) {
+        // CSR path: every entry of the wave's rows in CSR order, the
+        // current tile from LDS, everything else from x (L2); the full
+        // sum (no phase B)
+#pragma unroll
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            const int lrow = C::RPW * wave + 4 * qd + gq;
+            if (lrow < nloc) {
+                const int64_t row = t0 + lrow;
+                const int eb = row_ptr[row], ee = row_ptr[row + 1];
+                for (int e = eb; e < ee; e += 4) {
+                    int cj[4];
+                    float wj[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const bool v = e + k < ee;
+                        cj[k] = v ? col[e + k] : -1;
+                        wj[k] = v ? ew[e + k] : 0.f;
+                    }
+                    if constexpr (X0) {
+                        // codes form: one entry at a time (registers), rows
+                        // outside the tile expanded from their codes
+#pragma unroll 1
+                        for (int k = 0; k < 4; ++k) {
+                            if (cj[k] < 0) continue;
+                            f32x4 vk[C::CH];
+                            const int64_t off = static_cast<int64_t>(cj[k]) - t0;
+                            if (off >= 0 && off < nloc) {
+                                const uint32_t o = static_cast<uint32_t>(off);
+                                const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
+#pragma unroll
+                                for (int j = 0; j < C::CH; ++j)
+                                    vk[j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+                            } else {
+                                const float* cp = x + static_cast<int64_t>(cj[k]) * ldx;
+                                const float4 v0 = ld4(cp), v1 = ld4(cp + 4);
+                                const float v[7] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z};
+#pragma unroll 1
+                                for (int j = 0; j < C::CH; ++j) {
+                                    // (the table offset opaque per use: hoisted out
+                                    // of the entry loops its 64 VGPRs spill)
+                                    uint32_t co = static_cast<uint32_t>(C::OFF_COEF + (c0 + 16 * j) * 8 * 16);
+                                    asm volatile("" : "+v"(co));
+                                    f32x4 cf[8];
+#pragma unroll
+                                    for (int q = 0; q < 8; ++q)
+                                        cf[q] = *reinterpret_cast<const f32x4*>(lds + co + q * 16);
+                                    vk[j] = expand4(cf, v);
+                                }
+                            }
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vk[j][r], accn[qd][j][r]);
+                        }
+                        continue;
+                    }
+                    f32x4 vv[4][C::CH];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int64_t off = static_cast<int64_t>(cj[k]) - t0;
+                        if (cj[k] < 0) {
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j) vv[k][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        } else if (off >= 0 && off < nloc) {
+                            const uint32_t o = static_cast<uint32_t>(off);
+                            const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+                                vv[k][j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+                        } else {
+                            const float* rp = x + static_cast<int64_t>(cj[k]) * ldx + 4 * c0;
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+                                vv[k][j] = *reinterpret_cast<const f32x4*>(rp + 64 * j);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+#pragma unroll
+                        for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vv[k][j][r], accn[qd][j][r]);
+                }
+            }
+        }
+    };
+        auto no_mid = [](auto) {};
+
+    if constexpr (!AGG) {
+        // ---- the pipelined step (every full-layer mode).  Step s runs phase
+        // A of tile s with the transform of tile s - 2 (its 48 MFMAs in four
+        // groups between phase A's slot batches: the matrix pipe works under
+        // the aggregation's LDS reads and FMAs instead of in a phase of its
+        // own), then phase B and the split of tile s - 1 into the A image:
+        //   B0  ext rows of step s landed (older: this step's records, the own
+        //       rows of tile s, the stores of tile s - 3); younger: the records
+        //       of step s + 1, the own rows of tile s + 1
+        //   phase A(s) || MFMAs(s - 2) (A image and REXP of tile s - 2);
+        //   epilogue and stores of tile s - 2; residual seeds of tile s - 1
+        //   B1  every read of slot (s-1) % 3, the ext area, this step's
+        //       records and the A image done
+        //       -> DMA ext rows of step s + 1, records of step s + 2, own rows
+        //       of tile s + 2 into slot (s-1) % 3
+        //   phase B(s - 1) (its +z term from tile s), split -> A image, REXP
+        //   (codes form: tile s + 2's and step s + 1's rows expanded here)
+        f32x4 accp[C::NQ][C::CH];
+        uint32_t ncode[C::NQ];
+        float nwt[C::NQ];
+#pragma unroll
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            ncode[qd] = C::OFF_ZERO >> C::CSH;
+            nwt[qd] = 0.f;
+#pragma unroll
+            for (int j = 0; j < C::CH; ++j) accp[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // residual + bias of tile s - 1's rows in the transform's layout (lane
+        // (rr, gg) of block (ib, cp): row 16 (wm IBW + ib) + rr, columns n0 +
+        // 16 cp + 4 gg ..), read at step s, used by step s + 1's MFMAs
+        f32x4 seedc[IBW][CPW];
+#pragma unroll
+        for (int ib = 0; ib < IBW; ++ib)
+#pragma unroll
+            for (int cp = 0; cp < CPW; ++cp) seedc[ib][cp] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int64_t prv2 = -1, prv = -1, cur = tile_of(0), nx1 = tile_of(1);
+        WinCursor c2{0, 0, 0};
+        c2.next(S.L);
+        c2.next(S.L);
+        int xs = 0;                               // X slot of step s (s % 3)
+        const int rr = rr0, gg = gg0;
+        constexpr int PD = X0 ? 3 : kWinPD, NF = PD + 1, NTT = C::KC * IBW, TG = NTT / 4;
+        static_assert(NTT % 4 == 0 && PD < NTT, "four MFMA groups");
+        for (int s = 0;; ++s) {
+            if (cur < 0 && prv < 0 && prv2 < 0) break;   // (uniform)
+            const int64_t nx2 = win_tile_c(S, p, c2);
+            // (the REXP row recomputed from an opaque lane)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            const int xp = xs == 0 ? 2 : xs - 1;  // slot of tile s - 1 (and of tile s + 2)
+            const int tq = static_cast<int>(s & 1);
+            const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
+            const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
+            const int64_t t20 = rb + (prv2 >= 0 ? prv2 : 0) * C::BM;
+            const int64_t nloc2 = prv2 >= 0 ? (re - t20 < C::BM ? re - t20 : C::BM) : 0;
+            const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
+            const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
+            wtr.flush(wave, s - 1);
+            wtr.stamp(0);
+            // (B0)
+            if constexpr (X0) {
+                // (codes form: the records of step s + 1 landed -- the ext list of
+                // the codes DMA'd below; nothing younger)
+                wbar<wvm(0) & kWLgkm0>();
+                code_dma(nx2, tq ^ 1, true);
+            } else if (s == 0) wbar<wvm(0) & kWLgkm0>();
+            else wbar<wvm(1 + C::NPX) & kWLgkm0>();
+            wtr.stamp(1);
+
+            // ---- the transform of tile s - 2, as four MFMA groups
+            const bool mf = prv2 >= 0;             // (uniform)
+            int pr2[IBW];
+            f32x4 accm[IBW][CPW];
+            f16x8w fh[NF], fl[NF];
+            const int sw = asw<H>(rr);
+            auto frag = [&](int t, f16x8w& bh, f16x8w& bl) {
+                const int kc = t / IBW, ib = t % IBW;
+                const int R = (wm * IBW + ib) * 16 + rr;
+                const int ao = R * H + 8 * ((4 * kc + gg) ^ sw);
+                bh = *reinterpret_cast<const f16x8w*>(&AH[ao]);
+                bl = *reinterpret_cast<const f16x8w*>(&AL[ao]);
+            };
+            if (mf) {
+#pragma unroll
+                for (int ib = 0; ib < IBW; ++ib) {
+                    pr2[ib] = REXP[(wm * IBW + ib) * 16 + rr];
+#pragma unroll
+                    for (int cp = 0; cp < CPW; ++cp)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) accm[ib][cp][r] = ldexpf(seedc[ib][cp][r], pr2[ib] + qw[cp]);
+                }
+#pragma unroll
+                for (int t = 0; t < PD; ++t) frag(t, fh[t], fl[t]);
+            }
+            auto mid = [&](auto G) {
+                constexpr int g = decltype(G)::value;
+                if (!mf) return;
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = g * TG; t < (g + 1) * TG; ++t) {
+                    const int kc = t / IBW, ib = t % IBW;
+                    if constexpr ((MODE & 4) == 0) {
+                        if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
+#pragma unroll
+                        for (int cp = 0; cp < CPW; ++cp) {
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fl[t % NF], accm[ib][cp], 0, 0, 0);
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
+                        }
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            };
+
+            // ---- phase A of tile s (the MFMA groups between its batches)
+            f32x4 accn[C::NQ][C::CH];
+            uint32_t ncn[C::NQ];
+            float nwn[C::NQ];
+            const bool far = phase_a(tq, t0, nloc, X, cur >= 0, accn, ncn, nwn, mid);
+            wtr.stamp(2);
+            // epilogue of tile s - 2 in registers (gnn_model.py:184-191: conv
+            // + bias, + x, BN, ReLU); lane (rr, gg) of block (ib, cp) holds row
+            // 16 (wm IBW + ib) + rr, columns n0 + 16 cp + 4 gg .. + 3
+            if (mf) {
+#pragma unroll
+                for (int cp = 0; cp < CPW; ++cp) {
+                    const int nc = n0 + 16 * cp + 4 * gg;
+                    const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + nc]);
+                    const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + nc]);
+#pragma unroll
+                    for (int ib = 0; ib < IBW; ++ib)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float v = ldexpf(accm[ib][cp][r], -(pr2[ib] + qw[cp]));
+                            if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
+                            if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
+                            accm[ib][cp][r] = v;
+                        }
+                }
+                // the stores of tile s - 2 (before B1 and this step's DMAs; a
+                // partial tile is the last of its workgroup -- fewer stores
+                // there change no wait that matters: the later steps' records
+                // and rows are dummies)
+                static_assert(IBW * CPW == C::NST, "one store per block keeps the per-step store count");
+#pragma unroll
+                for (int cp = 0; cp < CPW; ++cp) {
+                    const int nc = n0 + 16 * cp + 4 * gg;
+#pragma unroll
+                    for (int ib = 0; ib < IBW; ++ib) {
+                        const int lr = (wm * IBW + ib) * 16 + rr;
+                        if (lr < nloc2)
+                            __builtin_nontemporal_store(accm[ib][cp], reinterpret_cast<f32x4*>(out + (t20 + lr) * ldo + nc));
+                    }
+                }
+            }
+            if (far) phase_a_far(t0, nloc, X, accn);
+            // residual + bias of tile s - 1, before slot (s-1) % 3 is refilled
+            f32x4 seedn[IBW][CPW];
+            if (prv >= 0) {
+#pragma unroll
+                for (int cp = 0; cp < CPW; ++cp) {
+                    const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[n0 + 16 * cp + 4 * gg]);
+#pragma unroll
+                    for (int ib = 0; ib < IBW; ++ib) {
+                        const int lr = (wm * IBW + ib) * 16 + rr;
+                        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (has_res) {
+                            const int ch = ((n0 + 16 * cp) >> 2) + gg;
+                            rv = *reinterpret_cast<const float4*>(XP + lr * C::ROWB + ((ch ^ (lr & 7)) << 4));
+                        }
+                        seedn[ib][cp] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
+                    }
+                }
+            }
+            // (B1)
+            wtr.stamp(3);
+            if constexpr (X0) wbar<wvm(0) & kWLgkm0>();   // (+ every wave's codes)
+            else wbar<kWLgkm0>();
+            const int64_t tn1 = nx1, tn2 = nx2;
+            // DMA pieces of this step: ext rows of step s + 1, the records of
+            // step s + 2, the own rows of tile s + 2 (codes form: the records
+            // only), issued between phase B's and the split's VALU work
+            // (MIGNN_WIN_DMAIL; 0: all at once after B1)
+            const unsigned char* es[C::NPE];
+            if constexpr (!X0) {
+                // this wave's records of step s + 1 landed (its ext list);
+                // younger: the own rows of tile s + 1, the stores of tile s - 2
+                if (s == 0) wwait<wvm(0)>();
+                else if (s == 1) wwait<wvm(C::NPX)>();
+                else wwait<wvm(C::NPX + C::NST)>();
+#pragma unroll
+                for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
+            }
+            constexpr int NPC = X0 ? 1 : C::NPE + 1 + C::NPX;
+            auto dpiece = [&](int q) {
+                if constexpr (X0) {
+                    dma_tab(tn2, tq);
+                } else {
+                    if (q < C::NPE) ext_dma(q, es[q]);
+                    else if (q == C::NPE) dma_tab(tn2, tq);
+                    else dma_own(tn2, xp, q - C::NPE - 1);
+                }
+            };
+            // pieces [q0, q1)
+            auto dpieces = [&](int q0, int q1) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = q0; q < q1 && q < NPC; ++q) dpiece(q);
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            constexpr bool DIL = MIGNN_WIN_DMAIL != 0;
+            if (!DIL || prv < 0) dpieces(0, NPC);
+            wtr.stamp(4);
+            // ---- phase B of tile s - 1 (its +z term, from tile s), split
+            if (prv >= 0) {
+                f32x4 pv[C::NQ][C::CH];
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    const uint32_t ad = decode(ncode[qd]);
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j) pv[qd][j] = *reinterpret_cast<const f32x4*>(lds + ad + 256 * j);
+                }
+                if (DIL) dpieces(0, 3);
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) accp[qd][j][r] = fmaf(nwt[qd], pv[qd][j][r], accp[qd][j][r]);
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    if (DIL && qd == 1) dpieces(3, 5);
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) m = max(m, __float_as_uint(fabsf(accp[qd][j][r])));
+                    m = wrow_max(m);
+                    const int pe = wsplit_exp(m);
+                    const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
+                    const int lrow = C::RPW * wave + 4 * qd + gq;
+                    const int swr = asw<H>(lrow);
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j) {
+                        f16x4w hv, lv;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float sv = accp[qd][j][r] * sc;
+                            const _Float16 hh = static_cast<_Float16>(sv);
+                            hv[r] = hh;
+                            lv[r] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                        }
+                        const int cc = c0 + 16 * j;             // the lane's 16-B fp32 chunk
+                        const int ao = lrow * H + 8 * ((cc >> 1) ^ swr) + 4 * (cc & 1);
+                        *reinterpret_cast<f16x4w*>(&AH[ao]) = hv;
+                        *reinterpret_cast<f16x4w*>(&AL[ao]) = lv;
+                    }
+                    if (iq == 0) REXP[C::RPW * wave + 4 * qd + (ln >> 4)] = pe;
+                }
+                if (DIL) dpieces(5, NPC);
+            }
+            if constexpr (X0) {
+                // codes form: tile s + 2's own rows (slot (s-1) % 3) and step s +
+                // 1's ext rows, block i's MFMAs before block i - 1's store
+                f32x4 xd[2];
+#pragma unroll
+                for (int i = 0; i < NXB; ++i) {
+                    xd[i & 1] = xblock_mfma(i);
+                    if (i > 0) xblock_store(xp, i - 1, xd[(i - 1) & 1]);
+                }
+                xblock_store(xp, NXB - 1, xd[(NXB - 1) & 1]);
+            }
+            wtr.stamp(5);
+            // carry
+#pragma unroll
+            for (int qd = 0; qd < C::NQ; ++qd) {
+                ncode[qd] = ncn[qd];
+                nwt[qd] = nwn[qd];
+#pragma unroll
+                for (int j = 0; j < C::CH; ++j) accp[qd][j] = accn[qd][j];
+            }
+#pragma unroll
+            for (int ib = 0; ib < IBW; ++ib)
+#pragma unroll
+                for (int cp = 0; cp < CPW; ++cp) seedc[ib][cp] = seedn[ib][cp];
+            xs = xs == 2 ? 0 : xs + 1;
+            prv2 = prv;
+            prv = cur;
+            cur = nx1;
+            nx1 = nx2;
+            c2.next(S.L);
+        }
+        wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
+    } else {
     // phase-B carry: tile s-1's partial sums and +z entries
     f32x4 accp[C::NQ][C::CH];
     uint32_t ncode[C::NQ];
@@ -1034,157 +1460,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         f32x4 accn[C::NQ][C::CH];
         uint32_t ncn[C::NQ];
         float nwn[C::NQ];
-#pragma unroll
-        for (int qd = 0; qd < C::NQ; ++qd) {
-            ncn[qd] = C::OFF_ZERO >> C::CSH;
-            nwn[qd] = 0.f;
-#pragma unroll
-            for (int j = 0; j < C::CH; ++j) accn[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        if (cur >= 0) {
-            const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
-            const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-                *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
-            const int maxa = static_cast<int>(summ & 0xffu);
-            const bool far = ((summ >> 8) & 1u) != 0u;
-            if (!far) {
-                uint4 cds[C::NQ], w03[C::NQ], w47[C::NQ];
-#pragma unroll
-                for (int qd = 0; qd < C::NQ; ++qd) {
-                    const unsigned char* rec = RW + (4 * qd + gq) * kWRec;
-                    cds[qd] = *reinterpret_cast<const uint4*>(rec);
-                    w03[qd] = *reinterpret_cast<const uint4*>(rec + 16);
-                    w47[qd] = *reinterpret_cast<const uint4*>(rec + 32);
-                }
-                auto codeof = [&](int qd, int u) -> uint32_t {
-                    const uint32_t d = u < 2 ? cds[qd].x : u < 4 ? cds[qd].y : u < 6 ? cds[qd].z : cds[qd].w;
-                    return (u & 1) ? (d >> 16) : (d & 0xffffu);
-                };
-                auto wof = [&](int qd, int u) -> float {
-                    const uint32_t d = u == 0 ? w03[qd].x : u == 1 ? w03[qd].y : u == 2 ? w03[qd].z
-                                     : u == 3 ? w03[qd].w : u == 4 ? w47[qd].x : u == 5 ? w47[qd].y
-                                     : u == 6 ? w47[qd].z : w47[qd].w;
-                    return __uint_as_float(d);
-                };
-                // slots in batches of 2: loads of a batch first
-                auto batch = [&](auto U0, auto NB) {
-                    constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
-                    f32x4 vv[C::NQ][nb][C::CH];
-#pragma unroll
-                    for (int qd = 0; qd < C::NQ; ++qd)
-#pragma unroll
-                        for (int uu = 0; uu < nb; ++uu) {
-                            const uint32_t a = decode(codeof(qd, u0 + uu));
-#pragma unroll
-                            for (int j = 0; j < C::CH; ++j)
-                                vv[qd][uu][j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
-                        }
-#pragma unroll
-                    for (int qd = 0; qd < C::NQ; ++qd)
-#pragma unroll
-                        for (int uu = 0; uu < nb; ++uu) {
-                            const float w = wof(qd, u0 + uu);
-#pragma unroll
-                            for (int j = 0; j < C::CH; ++j)
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(w, vv[qd][uu][j][r], accn[qd][j][r]);
-                        }
-                };
-                // (batches of 2: the 128-VGPR budget of 4 waves per SIMD)
-                if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
-                if (maxa > 2) batch(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
-                if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
-                if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
-#pragma unroll
-                for (int qd = 0; qd < C::NQ; ++qd) {
-                    ncn[qd] = codeof(qd, 7);
-                    nwn[qd] = wof(qd, 7);
-                }
-            } else {
-                // CSR path: every entry of the wave's rows in CSR order, the
-                // current tile from LDS, everything else from x (L2); the full
-                // sum (no phase B)
-#pragma unroll
-                for (int qd = 0; qd < C::NQ; ++qd) {
-                    const int lrow = C::RPW * wave + 4 * qd + gq;
-                    if (lrow < nloc) {
-                        const int64_t row = t0 + lrow;
-                        const int eb = row_ptr[row], ee = row_ptr[row + 1];
-                        for (int e = eb; e < ee; e += 4) {
-                            int cj[4];
-                            float wj[4];
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                const bool v = e + k < ee;
-                                cj[k] = v ? col[e + k] : -1;
-                                wj[k] = v ? ew[e + k] : 0.f;
-                            }
-                            if constexpr (X0) {
-                                // codes form: one entry at a time (registers), rows
-                                // outside the tile expanded from their codes
-#pragma unroll 1
-                                for (int k = 0; k < 4; ++k) {
-                                    if (cj[k] < 0) continue;
-                                    f32x4 vk[C::CH];
-                                    const int64_t off = static_cast<int64_t>(cj[k]) - t0;
-                                    if (off >= 0 && off < nloc) {
-                                        const uint32_t o = static_cast<uint32_t>(off);
-                                        const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
-#pragma unroll
-                                        for (int j = 0; j < C::CH; ++j)
-                                            vk[j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
-                                    } else {
-                                        const float* cp = x + static_cast<int64_t>(cj[k]) * ldx;
-                                        const float4 v0 = ld4(cp), v1 = ld4(cp + 4);
-                                        const float v[7] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z};
-#pragma unroll 1
-                                        for (int j = 0; j < C::CH; ++j) {
-                                            f32x4 cf[8];
-#pragma unroll
-                                            for (int q = 0; q < 8; ++q)
-                                                cf[q] = *reinterpret_cast<const f32x4*>(
-                                                    lds + C::OFF_COEF + ((c0 + 16 * j) * 8 + q) * 16);
-                                            vk[j] = expand4(cf, v);
-                                        }
-                                    }
-#pragma unroll
-                                    for (int j = 0; j < C::CH; ++j)
-#pragma unroll
-                                        for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vk[j][r], accn[qd][j][r]);
-                                }
-                                continue;
-                            }
-                            f32x4 vv[4][C::CH];
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                const int64_t off = static_cast<int64_t>(cj[k]) - t0;
-                                if (cj[k] < 0) {
-#pragma unroll
-                                    for (int j = 0; j < C::CH; ++j) vv[k][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-                                } else if (off >= 0 && off < nloc) {
-                                    const uint32_t o = static_cast<uint32_t>(off);
-                                    const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
-#pragma unroll
-                                    for (int j = 0; j < C::CH; ++j)
-                                        vv[k][j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
-                                } else {
-                                    const float* rp = x + static_cast<int64_t>(cj[k]) * ldx + 4 * c0;
-#pragma unroll
-                                    for (int j = 0; j < C::CH; ++j)
-                                        vv[k][j] = *reinterpret_cast<const f32x4*>(rp + 64 * j);
-                                }
-                            }
-#pragma unroll
-                            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                                for (int j = 0; j < C::CH; ++j)
-#pragma unroll
-                                    for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vv[k][j][r], accn[qd][j][r]);
-                        }
-                    }
-                }
-            }
-        }
+        if (phase_a(tq, t0, nloc, X, cur >= 0, accn, ncn, nwn, no_mid)) phase_a_far(t0, nloc, X, accn);
 
         wtr.stamp(2);
         // ---- (P1) phase B of tile s - 1, its split and residual seeds
@@ -1256,7 +1532,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         // (B2) A image complete; every read of slot (s-1) % 3, the ext area
         // and this step's records done
         wtr.stamp(3);
-        if constexpr (X0 && MIGNN_WIN_XMFMA) wbar<wvm(0) & kWLgkm0>();   // (+ every wave's codes)
+        if constexpr (X0) wbar<wvm(0) & kWLgkm0>();   // (+ every wave's codes)
         else wbar<kWLgkm0>();
         wtr.stamp(4);
         // the records of step s + 1 landed (younger: the own rows of tile s + 1
@@ -1322,21 +1598,18 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         bl = *reinterpret_cast<const f16x8w*>(&AL[ao]);
                     };
                     __builtin_amdgcn_sched_barrier(0);
-                    constexpr int PD = X0 ? MIGNN_WIN_PD_X0 : MIGNN_WIN_PD, NF = PD + 1, NTT = C::KC * IBW;
+                    constexpr int PD = kWinPD, NF = PD + 1, NTT = C::KC * IBW;
                     f16x8w fh[NF], fl[NF];
 #pragma unroll
                     for (int t = 0; t < PD && t < NTT; ++t) frag(t, fh[t], fl[t]);
                     // codes form: the expansion rows between the MFMAs, one
                     // every XS t-steps from t = XT (the codes DMA'd at B0)
                     constexpr int XT = 2, XS = 2;
-                    static_assert(!X0 || XT + XS * (NXR - 1) < NTT, "expansion inside the transform");
-                    [[maybe_unused]] f32x4 xcf[X0 && !MIGNN_WIN_XMFMA ? 8 : 1];
                     [[maybe_unused]] f32x4 xd[2];
 #pragma unroll
                     for (int t = 0; t < NTT; ++t) {
                         const int kc = t / IBW, ib = t % IBW;
                         if (t < NPC) dma_piece(t);
-#if MIGNN_WIN_XMFMA
                         if constexpr (X0) {
                             // block i's MFMAs, block i - 1's store (its result landed)
                             static_assert(!X0 || XT + XS * (NXB - 1) < NTT, "expansion inside the transform");
@@ -1346,16 +1619,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                                 if (i > 0) xblock_store(xn2, i - 1, xd[(i - 1) & 1]);
                             }
                         }
-#else
-                        if constexpr (X0) {
-                            if (t == XT) {
-                                wwait<wvm(1)>();      // this wave's codes (the records younger)
-                                coef_load(xcf);
-                            }
-                            if (t >= XT && (t - XT) % XS == 0 && (t - XT) / XS < NXR)
-                                expand_i(xcf, xn2, (t - XT) / XS);
-                        }
-#endif
                         if (MODE & 4) continue;
                         if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
 #pragma unroll
@@ -1368,12 +1631,9 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                     }
 #pragma unroll
                     for (int t = NTT; t < NPC; ++t) dma_piece(t);
-#if MIGNN_WIN_XMFMA
                     if constexpr (X0) xblock_store(xn2, NXB - 1, xd[(NXB - 1) & 1]);
-#endif
                 }
                 wtr.stamp(5);
-#if MIGNN_WIN_DIRECT
                 {
                     // epilogue stored straight from the accumulators: lane (rr, gg) of
                     // block (ib, cp) holds row 16 ib + rr, columns n0 + 16 cp + 4 gg .. +3
@@ -1399,61 +1659,14 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         }
                     }
                 }
-#else
-                static_assert(CPW == 1, "the staged epilogue: one column block per wave");
-                // (B3) every wave done with the A image: stage there
-                wbar<kWLgkm0>();
-                {
-                    const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + n0 + 4 * gg]);
-                    const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + n0 + 4 * gg]);
-#pragma unroll
-                    for (int ib = 0; ib < IBW; ++ib) {
-                        float o[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float v = ldexpf(accm[ib][0][r], -(pr[ib] + qw[0]));
-                            if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                            if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
-                            o[r] = v;
-                        }
-                        const int lr = (wm * IBW + ib) * 16 + rr;
-                        const int ch = (n0 >> 2) + gg;
-                        *reinterpret_cast<f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4)) =
-                            f32x4{o[0], o[1], o[2], o[3]};
-                    }
-                }
-                // (B4) staged: my 8 rows out, whole rows
-                wtr.stamp(6);
-                wbar<kWLgkm0>();
-                {
-                    const int ch = lane % C::LPRW;
-                    f32x4 v[C::NST];
-#pragma unroll
-                    for (int i = 0; i < C::NST; ++i) {
-                        const int lr = C::RPW * wave + i * C::RPI + lane / C::LPRW;
-                        v[i] = *reinterpret_cast<const f32x4*>(lds + C::OFF_STG + lr * C::ROWB + ((ch ^ (lr & 15)) << 4));
-                    }
-#pragma unroll
-                    for (int i = 0; i < C::NST; ++i) {
-                        const int lr = C::RPW * wave + i * C::RPI + lane / C::LPRW;
-                        if (lr < nlocp)
-                            __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
-                    }
-                }
-#endif
                 wtr.stamp(7);
             }
         } else {
 #pragma unroll
             for (int q = 0; q < NPC; ++q) dma_piece(q);
             if constexpr (X0) {
-#if MIGNN_WIN_XMFMA
 #pragma unroll
                 for (int rbk = 0; rbk < NXB; ++rbk) xblock_store(xn2, rbk, xblock_mfma(rbk));
-#else
-                wwait<wvm(1)>();
-                expand(xn2, true);
-#endif
             }
         }
         // carry tile s into phase B
@@ -1471,6 +1684,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         c2.next(S.L);
     }
     wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
+    }
 }
 
 // max over the 4 lanes of a row of the B layout (l, l ^ 16, l ^ 32, l ^ 48)
@@ -1966,10 +2180,6 @@ int launch_win(int h, const void* plan, const int32_t* row_ptr, const int32_t* c
     const int64_t ntiles = (re - rb + 63) / 64;
     const int G = win_grid(ntiles, h == 128 ? WCfg<128>::WGPC : WCfg<64>::WGPC);
     MIGNN_REQUIRE(G > 0, "gcn_win: device query failed");
-    MIGNN_REQUIRE(plan_registry_check(plan, 1, G, h, current_device(), rb, re),
-                  "gcn_win: the plan was built for another row range, width or device "
-                  "(launch h=%d rows [%lld, %lld) grid %d)", h, static_cast<long long>(rb),
-                  static_cast<long long>(re), G);
     if (h == 128)
         launch_win_h<128, MODE>(G, st, plan, row_ptr, col, ew, x, ldx, rb, re, w, bias, scale, shift, flags, out, ldo, xcoef);
     else if constexpr ((MODE & 64) == 0)
@@ -2028,7 +2238,6 @@ extern "C" int mignn_gcn_win_plan(const int32_t* row_ptr, const int32_t* col, co
     hipLaunchKernelGGL(win_hdr_kernel, dim3(1), dim3(64), 0, st, hdr, order_info, ntiles, G, h, rb, re);
     int rc = launch_status("win_hdr_kernel");
     if (rc) return rc;
-    plan_registry_put(PlanRecord{plan, 1, G, h, current_device(), rb, re});
     unsigned char* tabs = static_cast<unsigned char*>(plan) + kWHdr;
     const unsigned grid = static_cast<unsigned>(ntiles < (1 << 20) ? ntiles : (1 << 20));
     if (h == 128)

@@ -180,6 +180,7 @@ DIAG_SIGNATURES = {
     "mignn_diag_set_trace": (c_int, [_P]),
     "mignn_diag_set_trace_f16x3": (c_int, [_P]),
     "mignn_diag_clock": (c_int, [c_int, c_int, _P, _P]),
+    "mignn_diag_pk_fma": (c_int, [c_int, _P, c_int64, _P, c_int, _P, _P]),
     "mignn_diag_mlp_head": (c_int, [c_int, _P, c_int64, _P, _P, _P]),
     "mignn_diag_gcn_layer": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int64, c_int, _P, _P, _P,
                                      _P, c_int, _P, c_int64, _P]),

@@ -146,13 +146,15 @@ class Csr:
         self.perm = self.inv = self.pos = None
         self.order_info = None   # int32[4] of the column order (mignn_locality_order_cols)
         self.key_tensor = None   # the caller's edge_index the cache key was made from
-        self.plans: Dict[Tuple[str, int, int, int], torch.Tensor] = {}
+        self.plans: Dict[Tuple[str, int, int, int, int], torch.Tensor] = {}
 
     def ring_plan(self, h: int, row_begin: int, row_end: int) -> torch.Tensor:
         """The ring kernel's plan of rows [row_begin, row_end) for hidden
         width h (mignn_gcn_ring_plan: per-tile records, ext-row lists and the
         schedule of this device), built on first use and kept with the CSR."""
-        key = ("ring", h, row_begin, row_end)
+        # (the plan's schedule is for the device current at build time: its
+        # CU count sets the grid -- a launch from another device must not reuse it)
+        key = ("ring", h, row_begin, row_end, torch.cuda.current_device())
         plan = self.plans.get(key)
         if plan is None:
             L = _lib.lib()
@@ -173,7 +175,7 @@ class Csr:
         plane count per column taken from the CSR, mignn_gcn_win_plan) --
         and a 48-B record per row), built on first use and kept with the CSR
         (it copies the ew weights)."""
-        key = ("win", h, row_begin, row_end)
+        key = ("win", h, row_begin, row_end, torch.cuda.current_device())
         plan = self.plans.get(key)
         if plan is None:
             L = _lib.lib()

@@ -68,6 +68,11 @@ int mignn_diag_set_trace_f16x3(void* buf);
  * loads, bit 2 = no MFMAs (results wrong by design). */
 /* Shader clock probe: `blocks` workgroups of 4*iters dependent FMAs each;
  * out[2b] = s_memtime delta, out[2b+1] = s_memrealtime delta (100 MHz). */
+/* v_pk_fma_f32 forms of the row-code expansion (0 scalar chain, 1 inline
+ * asm with op_sel_hi:[1,0,1], 2 inline asm without it, 3 compiler-packed);
+ * codes [n, 8], coef [h, 8], out [n, h] */
+int mignn_diag_pk_fma(int form, const float* codes, int64_t n, const float* coef, int h,
+                      float* out, void* stream);
 int mignn_diag_clock(int blocks, int iters, int64_t* out, void* stream);
 
 int mignn_diag_mlp_head(int mode, const float* x, int64_t n, const void* img, float* out,

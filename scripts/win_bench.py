@@ -36,6 +36,10 @@ if old:
     csr_b = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv_b)
 del ei, pos
 nnz = int(csr_c.row_ptr[-1].item())
+# the product entry points from the product library (the diag build carries
+# bounds checks and trace branches: slower); the ablation modes from the
+# diag library
+LP = _lib.lib()
 L = _lib.diag_lib()
 P = _lib.ptr
 # WB_LIBS: comma list of variant builds of libmignn.so (name=path); each
@@ -72,21 +76,21 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     b = torch.randn(H, device=dev, generator=g) * 0.05
     sc = torch.rand(H, device=dev, generator=g) + 0.5
     sh = torch.randn(H, device=dev, generator=g) * 0.1
-    nbw = L.mignn_gcn_win_plan_bytes(0, n, H)
+    nbw = LP.mignn_gcn_win_plan_bytes(0, n, H)
     wplan = torch.empty(nbw, dtype=torch.uint8, device=dev)
     wstats = torch.zeros(4, dtype=torch.int64, device=dev)
     Yw, Ywa, Yd = torch.empty_like(X), torch.empty_like(X), torch.empty_like(X)
 
     def mk_wplan(s_=None):
-        _lib.check(L.mignn_gcn_win_plan(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), 0, n, H, P(info),
+        _lib.check(LP.mignn_gcn_win_plan(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), 0, n, H, P(info),
                                         P(wplan), nbw, s_, st), "wplan")
 
     def win():
-        _lib.check(L.mignn_gcn_layer_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
+        _lib.check(LP.mignn_gcn_layer_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
                                          H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yw), H, st), "win")
 
     def win_agg():
-        _lib.check(L.mignn_gcn_aggregate_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
+        _lib.check(LP.mignn_gcn_aggregate_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
                                              P(X), H, 0, n, H, P(Ywa), H, st), "win_agg")
 
     mk_wplan(P(wstats))
@@ -95,11 +99,25 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     res.setdefault("win_plan_stats", {})[H] = wstats.tolist()
     res.setdefault("win_header", {})[H] = hdr[:32].view(torch.int32).tolist() + hdr[32:64].view(torch.int64).tolist()
     cases = {"win_plan": mk_wplan, "win": win, "win_aggregate": win_agg}
+    vout = {}
     for vname, VL in VARIANTS.items():
-        def fv(VL=VL):
-            _lib.check(VL.mignn_gcn_layer_win(P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
-                                              H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yd), H, st), "wv")
+        # each variant builds its own plan (plan formats may differ)
+        vnb = VL.mignn_gcn_win_plan_bytes(0, n, H)
+        vplan = torch.empty(vnb, dtype=torch.uint8, device=dev)
+        _lib.check(VL.mignn_gcn_win_plan(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), 0, n, H, P(info),
+                                         P(vplan), vnb, None, st), "vplan")
+        Yv = torch.empty_like(X)
+        vout[vname] = Yv
+
+        def fv(VL=VL, vplan=vplan, Yv=Yv):
+            _lib.check(VL.mignn_gcn_layer_win(P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
+                                              H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yv), H, st), "wv")
+
+        def fva(VL=VL, vplan=vplan):
+            _lib.check(VL.mignn_gcn_aggregate_win(P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
+                                                  P(X), H, 0, n, H, P(Yd), H, st), "wva")
         cases[f"win@{vname}"] = fv
+        cases[f"win_aggregate@{vname}"] = fva
     for m in [int(v) for v in os.environ.get("WB_MODES", "").split(",") if v]:
         def fw(m=m):
             _lib.check(L.mignn_diag_win(m, P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
@@ -136,6 +154,11 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     torch.cuda.synchronize()
     out["win_deterministic"] = bool(torch.equal(Yw, Yw2))
     del Yw2
+    for vname in vout:
+        cases[f"win@{vname}"]()
+        torch.cuda.synchronize()
+        out[f"win_vs_{vname}_max_diff"] = (Yw - vout[vname]).abs().max().item()
+        out[f"win_vs_{vname}_bitwise"] = bool(torch.equal(Yw, vout[vname]))
     if old:
         pc()
         torch.cuda.synchronize()

@@ -1,8 +1,9 @@
 """Timeline of the window GCN kernel (mignn_diag_win_trace): median cycles per
 phase over workgroups 0..7, steps 8..62, waves 0 and 4 (10M mesh, column
-order).  Points: 0 top, 1 after B0, 2 phase A done, 3 phase B + split +
-seeds done, 4 after B2, 5 MFMAs (+ DMA issue) done, 6 staging written, 7
-stores issued.  Env: WT_H (128), WT_MODE (diag mode, 0)."""
+order).  Points (H = 128, round 6 pipelined step): 0 top, 1 after B0, 2 phase A
+with tile s-2's MFMA groups, 3 epilogue + stores + seeds, 4 B1 + DMA issue,
+5 phase B + split; aggregate mode (32): 0 top, 1 after B0, 2 phase A, 3
+phase B, 4 after B2.  Env: WT_H (128), WT_MODE (diag mode, 0)."""
 import json
 import os
 import statistics
@@ -58,7 +59,10 @@ res = {"H": H, "mode": mode}
 if H == 64:
     pts = [0, 1, 2, 3, 6, 4, 5] if not mode & 32 else [0, 1, 2, 3, 6, 5]
 else:
-    pts = [0, 1, 2, 3, 4, 5, 6, 7] if not mode & 32 else [0, 1, 2, 3, 4]
+    # (round 6 pipelined step: 0 top, 1 after B0, 2 phase A with tile s-2's
+    # MFMA groups, 3 epilogue + stores + seeds (before B1), 4 B1 + DMA issue,
+    # 5 phase B + split (+ codes expansion))
+    pts = [0, 1, 2, 3, 4, 5] if not mode & 32 else [0, 1, 2, 3, 4]
 for wv in ((0,) if H == 64 else (0, 1)):
     d = {}
     for a, b_ in zip(pts, pts[1:] + [0]):

@@ -202,21 +202,22 @@ def test_model_gcn_kernel_routes_agree(H, reorder):
 
 def test_ring_plan_header_mismatch():
     """A ring plan built for another row range (or grid) is refused by the
-    kernel: MIGNN_DEVERR_PLAN in the device error word, no row written."""
+    kernel: MIGNN_DEVERR_PLAN in the device error word, the launch's output
+    rows set to NaN, rows outside its range untouched."""
     csr, n = _graph("locality")
     H = 64
     X = torch.randn(n, H, device=DEV)
     W = torch.randn(H, H, device=DEV) * 0.05
     z = torch.zeros(H, device=DEV)
     plan, _ = _ring_plan(csr, 0, n, H)
-    out = torch.full_like(X, float("nan"))
+    out = torch.zeros_like(X)
     P = _lib.ptr
     _lib.device_errors(clear=True)
     _lib.check(_lib.lib().mignn_gcn_layer_ring(P(plan), P(csr.row_ptr), P(csr.col), P(csr.ew), P(X), H,
                                                 0, n - 1, H, P(W), P(z), P(z), P(z), 11, P(out), H,
                                                 _lib.stream()), "ring")
     assert _lib.device_errors(clear=True) & _lib.DEVERR_PLAN
-    assert torch.isnan(out).all()
+    assert torch.isnan(out[:n - 1]).all() and torch.count_nonzero(out[n - 1:]).item() == 0
 
 
 def test_forward_device_error_check_opt_in():

@@ -248,19 +248,21 @@ def test_bench_mesh_column_schedule():
 
 
 def test_win_plan_header_mismatch_flags_device_error():
-    """A launch whose row range does not match its plan's header writes
-    nothing and sets MIGNN_DEVERR_PLAN."""
+    """A launch whose row range does not match its plan's header: the kernel
+    sets MIGNN_DEVERR_PLAN and writes NaN over the launch's output rows (no
+    stale buffer contents pass for layer output); rows outside the launch's
+    range are untouched."""
     csr, n, _ = _graph("natural", (20, 16, 12))
     H = 64
     g, W, b, sc, sh = _weights(H, 4)
     X = torch.randn(n, H, generator=g).to(DEV)
     plan, _ = _plan(csr, 0, n, H)
-    out = torch.full((n, H), float("nan"), device=DEV)
+    out = torch.zeros((n, H), device=DEV)
     _lib.device_errors(clear=True)
     _layer(csr, plan, X, H, 0, n - 64, H, W, b, sc, sh, out)
     bits = _lib.device_errors(clear=True)
     assert bits & _lib.DEVERR_PLAN
-    assert torch.isnan(out).all()
+    assert torch.isnan(out[:n - 64]).all() and torch.count_nonzero(out[n - 64:]).item() == 0
 
 
 @pytest.mark.parametrize("H", [64, 128])
