@@ -64,9 +64,20 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 // more block barriers per step, 2.92 vs 2.87 ms), 4 column pairs x 32 rows
 // per wave (2.79-3.05 vs 2.78 ms), the codes expansion as VALU fma chains
 // (3.14-3.27 vs the MFMA expansion's 2.71 ms).
-constexpr int kWinPD = 3;
+#ifndef MIGNN_WIN_PD
+#define MIGNN_WIN_PD 3
+#endif
+#ifndef MIGNN_WIN_PDX
+#define MIGNN_WIN_PDX 1
+#endif
+constexpr int kWinPD = MIGNN_WIN_PD, kWinPDX = MIGNN_WIN_PDX;   // (codes form: PDX)
 // the pipelined step's DMA pieces interleaved with phase B and the split (1)
 // or issued together after B1 (0)
+// H = 64: the pipelined step (1: phase B + split first, the MFMAs inside
+// phase A, the epilogue before B1) or the round-5 order (0)
+#ifndef MIGNN_WIN64_PIPE
+#define MIGNN_WIN64_PIPE 1
+#endif
 #ifndef MIGNN_WIN_DMAIL
 #define MIGNN_WIN_DMAIL 1
 #endif
@@ -776,14 +787,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     // (COEF: the table k-major per 16-B feature chunk -- chunk c, input k
     // (7: the constant) -> features 4c .. 4c + 3 in one f32x4: per feature
     // the fma sequence of gcn_layer0.hip, which the compiler packs in pairs)
-    auto expand4 = [&](const f32x4 (&cf)[8], const float (&v)[7]) -> f32x4 {
-        f32x4 t = cf[7];
-#pragma unroll
-        for (int k = 0; k < 7; ++k)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) t[q] = fmaf(cf[k][q], v[k], t[q]);
-        return f32x4{relu_nan(t[0]), relu_nan(t[1]), relu_nan(t[2]), relu_nan(t[3])};
-    };
     // ---- the row expansion as f32 MFMAs: wave w computes
     // features 16 w .. 16 w + 15 of every expanded row, a 16-row block per
     // v_mfma_f32_16x16x4_f32 pair (inputs 0..3, then 4..6 and a zero; the
@@ -1056,15 +1059,23 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                                 const float v[7] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z};
 #pragma unroll 1
                                 for (int j = 0; j < C::CH; ++j) {
-                                    // (the table offset opaque per use: hoisted out
-                                    // of the entry loops its 64 VGPRs spill)
+                                    // layer 0's chain (expand4's order), one
+                                    // coefficient chunk live at a time: the
+                                    // table offset opaque and the steps pinned
+                                    // (hoisted, the 8 chunks are 32 VGPRs the
+                                    // pipelined step does not have)
                                     uint32_t co = static_cast<uint32_t>(C::OFF_COEF + (c0 + 16 * j) * 8 * 16);
                                     asm volatile("" : "+v"(co));
-                                    f32x4 cf[8];
+                                    f32x4 t = *reinterpret_cast<const f32x4*>(lds + co + 7 * 16);
 #pragma unroll
-                                    for (int q = 0; q < 8; ++q)
-                                        cf[q] = *reinterpret_cast<const f32x4*>(lds + co + q * 16);
-                                    vk[j] = expand4(cf, v);
+                                    for (int k = 0; k < 7; ++k) {
+                                        __builtin_amdgcn_sched_barrier(0);
+                                        const f32x4 cfk = *reinterpret_cast<const f32x4*>(lds + co + k * 16);
+#pragma unroll
+                                        for (int q = 0; q < 4; ++q) t[q] = fmaf(cfk[q], v[k], t[q]);
+                                    }
+                                    __builtin_amdgcn_sched_barrier(0);
+                                    vk[j] = f32x4{relu_nan(t[0]), relu_nan(t[1]), relu_nan(t[2]), relu_nan(t[3])};
                                 }
                             }
 #pragma unroll
@@ -1147,7 +1158,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         c2.next(S.L);
         int xs = 0;                               // X slot of step s (s % 3)
         const int rr = rr0, gg = gg0;
-        constexpr int PD = X0 ? 3 : kWinPD, NF = PD + 1, NTT = C::KC * IBW, TG = NTT / 4;
+        constexpr int PD = X0 ? kWinPDX : kWinPD, NF = PD + 1, NTT = C::KC * IBW, TG = NTT / 4;
         static_assert(NTT % 4 == 0 && PD < NTT, "four MFMA groups");
         for (int s = 0;; ++s) {
             if (cur < 0 && prv < 0 && prv2 < 0) break;   // (uniform)
@@ -1400,172 +1411,80 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         }
         wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
     } else {
-    // phase-B carry: tile s-1's partial sums and +z entries
-    f32x4 accp[C::NQ][C::CH];
-    uint32_t ncode[C::NQ];
-    float nwt[C::NQ];
+        // ---- the aggregate alone (mignn_gcn_aggregate_win: the fp32 sums are
+        // the output).  Step s: B0 (ext rows of step s landed; younger: the
+        // records of step s + 1, the own rows of tile s + 2, the last step's
+        // stores), phase A of tile s, phase B of tile s - 1, B2 (every read of
+        // slot (s-1) % 3, the ext area and this step's records done), the DMA
+        // of step s + 1's ext rows, step s + 2's records and tile s + 2's own
+        // rows, tile s - 1's stores
+        f32x4 accp[C::NQ][C::CH];
+        uint32_t ncode[C::NQ];
+        float nwt[C::NQ];
 #pragma unroll
-    for (int qd = 0; qd < C::NQ; ++qd) {
-        ncode[qd] = C::OFF_ZERO >> C::CSH;
-        nwt[qd] = 0.f;
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            ncode[qd] = C::OFF_ZERO >> C::CSH;
+            nwt[qd] = 0.f;
 #pragma unroll
-        for (int j = 0; j < C::CH; ++j) accp[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-
-    // schedule: cur / nx1 = tiles of steps s / s + 1, the cursor at s + 2
-    int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
-    WinCursor c2{0, 0, 0};
-    c2.next(S.L);
-    c2.next(S.L);
-    int xs = 0;                                   // X slot of step s (s % 3)
-    for (int s = 0;; ++s) {
-        if (cur < 0 && prv < 0) break;            // (uniform)
-        const int64_t nx2 = win_tile_c(S, p, c2);
-        const int rr = rr0, gg = gg0;
-        const int iql = iq;
-        // (the REXP row recomputed from an opaque lane: hoisted out of the
-        // step loop it is a register too many at H = 64)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1
-        const int xn2 = xp;                       // slot of tile s + 2 (= (s-1) % 3)
-        const int tq = static_cast<int>(s & 1);   // TAB slot of step s
-        const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
-        const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
-        const int64_t tp0 = rb + (prv >= 0 ? prv : 0) * C::BM;
-        const int64_t nlocp = prv >= 0 ? (re - tp0 < C::BM ? re - tp0 : C::BM) : 0;
-        const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
-        const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
-        // (B0) this step's ext rows landed (and, older, the own rows of tile
-        //      s + 1 and this step's records); younger: the records of step
-        //      s + 1, the own rows of tile s + 2, the last step's stores
-        wtr.flush(wave, s - 1);
-        wtr.stamp(0);
-        // (codes form: every row of the step was expanded by a ds_write of
-        // the last step -- nothing to wait for but LDS)
-        if constexpr (X0) {
-            // (codes form: also the records of step s + 1 -- the ext list of
-            // the codes DMA'd below; younger only the last step's stores)
-            if (s < 2) wbar<wvm(0) & kWLgkm0>();
-            else wbar<wvm(C::NST) & kWLgkm0>();
-            // this step's codes: own rows of tile s + 2, ext rows of step s + 1
-            // (landing under phase A; expanded between the transform's MFMAs)
-            code_dma(nx2, tq ^ 1, true);
-        } else if (s == 0) wbar<wvm(0) & kWLgkm0>();
-        else if (s == 1) wbar<wvm(1 + C::NPX) & kWLgkm0>();
-        else wbar<wvm(1 + C::NPX + C::NST) & kWLgkm0>();
-
-        wtr.stamp(1);
-        // ---- (P1) phase A of tile s
-        f32x4 accn[C::NQ][C::CH];
-        uint32_t ncn[C::NQ];
-        float nwn[C::NQ];
-        if (phase_a(tq, t0, nloc, X, cur >= 0, accn, ncn, nwn, no_mid)) phase_a_far(t0, nloc, X, accn);
-
-        wtr.stamp(2);
-        // ---- (P1) phase B of tile s - 1, its split and residual seeds
-        constexpr int NSEED = AGG ? 1 : IBW;
-        f32x4 seed[NSEED][CPW];
-        if (prv >= 0) {
-#pragma unroll
-            for (int qd = 0; qd < C::NQ; ++qd) {
-                const uint32_t a = decode(ncode[qd]);
-#pragma unroll
-                for (int j = 0; j < C::CH; ++j) {
-                    const f32x4 v = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) accp[qd][j][r] = fmaf(nwt[qd], v[r], accp[qd][j][r]);
-                }
-            }
-            if constexpr (!AGG) {
+            for (int j = 0; j < C::CH; ++j) accp[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
+        WinCursor c2{0, 0, 0};
+        c2.next(S.L);
+        c2.next(S.L);
+        int xs = 0;                               // X slot of step s (s % 3)
+        for (int s = 0;; ++s) {
+            if (cur < 0 && prv < 0) break;        // (uniform)
+            const int64_t nx2 = win_tile_c(S, p, c2);
+            const int xp = xs == 0 ? 2 : xs - 1;  // slot of tile s - 1 (and of tile s + 2)
+            const int tq = static_cast<int>(s & 1);
+            const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
+            const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
+            const int64_t tp0 = rb + (prv >= 0 ? prv : 0) * C::BM;
+            const int64_t nlocp = prv >= 0 ? (re - tp0 < C::BM ? re - tp0 : C::BM) : 0;
+            const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
+            wtr.flush(wave, s - 1);
+            wtr.stamp(0);
+            if (s == 0) wbar<wvm(0) & kWLgkm0>();
+            else if (s == 1) wbar<wvm(1 + C::NPX) & kWLgkm0>();
+            else wbar<wvm(1 + C::NPX + C::NST) & kWLgkm0>();
+            wtr.stamp(1);
+            f32x4 accn[C::NQ][C::CH];
+            uint32_t ncn[C::NQ];
+            float nwn[C::NQ];
+            if (phase_a(tq, t0, nloc, X, cur >= 0, accn, ncn, nwn, no_mid)) phase_a_far(t0, nloc, X, accn);
+            wtr.stamp(2);
+            if (prv >= 0) {
 #pragma unroll
                 for (int qd = 0; qd < C::NQ; ++qd) {
-                    uint32_t m = 0;
-#pragma unroll
-                    for (int j = 0; j < C::CH; ++j)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) m = max(m, __float_as_uint(fabsf(accp[qd][j][r])));
-                    m = wrow_max(m);
-                    const int pe = wsplit_exp(m);
-                    const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
-                    const int lrow = C::RPW * wave + 4 * qd + gq;
-                    const int sw = asw<H>(lrow);
+                    const uint32_t ad = decode(ncode[qd]);
 #pragma unroll
                     for (int j = 0; j < C::CH; ++j) {
-                        f16x4w hv, lv;
+                        const f32x4 v = *reinterpret_cast<const f32x4*>(lds + ad + 256 * j);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float sv = accp[qd][j][r] * sc;
-                            const _Float16 hh = static_cast<_Float16>(sv);
-                            hv[r] = hh;
-                            lv[r] = static_cast<_Float16>(sv - static_cast<float>(hh));
-                        }
-                        const int cc = c0 + 16 * j;             // the lane's 16-B fp32 chunk
-                        const int ao = lrow * H + 8 * ((cc >> 1) ^ sw) + 4 * (cc & 1);
-                        *reinterpret_cast<f16x4w*>(&AH[ao]) = hv;
-                        *reinterpret_cast<f16x4w*>(&AL[ao]) = lv;
-                    }
-                    if (iql == 0) {
-                        // (the row index recomputed from an opaque lane: hoisted
-                        // out of the step loop it is a register too many at H = 64)
-                        REXP[C::RPW * wave + 4 * qd + (ln >> 4)] = pe;
-                    }
-                }
-                // residual + bias of my output blocks (tile s-1's rows of my
-                // row group, my columns), before slot (s-1) % 3 is refilled
-#pragma unroll
-                for (int cp = 0; cp < CPW; ++cp) {
-                    const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[n0 + 16 * cp + 4 * gg]);
-#pragma unroll
-                    for (int ib = 0; ib < IBW; ++ib) {
-                        const int lr = (wm * IBW + ib) * 16 + rr;
-                        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
-                        if (has_res) {
-                            const int ch = ((n0 + 16 * cp) >> 2) + gg;
-                            rv = *reinterpret_cast<const float4*>(XP + lr * C::ROWB + ((ch ^ (lr & 7)) << 4));
-                        }
-                        seed[ib][cp] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
+                        for (int r = 0; r < 4; ++r) accp[qd][j][r] = fmaf(nwt[qd], v[r], accp[qd][j][r]);
                     }
                 }
             }
-        }
-        // (B2) A image complete; every read of slot (s-1) % 3, the ext area
-        // and this step's records done
-        wtr.stamp(3);
-        if constexpr (X0) wbar<wvm(0) & kWLgkm0>();   // (+ every wave's codes)
-        else wbar<kWLgkm0>();
-        wtr.stamp(4);
-        // the records of step s + 1 landed (younger: the own rows of tile s + 1
-        // and the last step's stores)
-        // (codes form: waited at B0)
-        if constexpr (X0) {
-        } else if (s == 0) wwait<wvm(0)>();
-        else if (s == 1) wwait<wvm(C::NPX)>();
-        else wwait<wvm(C::NPX + C::NST)>();
-        const int64_t tn1 = nx1, tn2 = nx2;
-        const unsigned char* es[C::NPE];
-        if constexpr (!X0)
+            wtr.stamp(3);
+            wbar<kWLgkm0>();                      // (B2)
+            wtr.stamp(4);
+            // the records of step s + 1 landed (younger: the own rows of tile
+            // s + 1 and the last step's stores)
+            if (s == 0) wwait<wvm(0)>();
+            else if (s == 1) wwait<wvm(C::NPX)>();
+            else wwait<wvm(C::NPX + C::NST)>();
+            const int64_t tn1 = nx1, tn2 = nx2;
+            const unsigned char* es[C::NPE];
 #pragma unroll
             for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
-        // DMA piece q of this step: ext rows of step s + 1, the records of step
-        // s + 2 (into this step's TAB slot), the own rows of tile s + 2 (codes
-        // form: the codes of those ext and own rows, then the records)
-        auto dma_piece = [&](int q) {
-            if constexpr (X0) {
-                dma_tab(tn2, tq);
-            } else {
-                if (q < C::NPE) ext_dma(q, es[q]);
-                else if (q == C::NPE) dma_tab(tn2, tq);
-                else dma_own(tn2, xn2, q - C::NPE - 1);
-            }
-        };
-        constexpr int NPC = X0 ? 1 : C::NPE + 1 + C::NPX;
-
-        if (prv >= 0) {
-            if constexpr (AGG) {
 #pragma unroll
-                for (int q = 0; q < NPC; ++q) dma_piece(q);
-                static_assert(!AGG || C::NQ * C::CH == C::NST, "aggregate stores keep the per-step store count");
+            for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
+            dma_tab(tn2, tq);
+#pragma unroll
+            for (int pp = 0; pp < C::NPX; ++pp) dma_own(tn2, xp, pp);
+            if (prv >= 0) {
+                static_assert(C::NQ * C::CH == C::NST, "aggregate stores keep the per-step store count");
 #pragma unroll
                 for (int qd = 0; qd < C::NQ; ++qd)
 #pragma unroll
@@ -1576,114 +1495,22 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         if (lrow < nlocp)
                             __builtin_nontemporal_store(accp[qd][j], reinterpret_cast<f32x4*>(out + (tp0 + lrow) * ldo + 4 * (c0 + 16 * j)));
                     }
-            } else {
-                // (3) transform: my output column blocks x my row blocks
-                int pr[IBW];
-                f32x4 accm[IBW][CPW];
-#pragma unroll
-                for (int ib = 0; ib < IBW; ++ib) {
-                    pr[ib] = REXP[(wm * IBW + ib) * 16 + rr];
-#pragma unroll
-                    for (int cp = 0; cp < CPW; ++cp)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) accm[ib][cp][r] = ldexpf(seed[ib][cp][r], pr[ib] + qw[cp]);
-                }
-                {
-                    const int sw = asw<H>(rr);
-                    auto frag = [&](int t, f16x8w& bh, f16x8w& bl) {
-                        const int kc = t / IBW, ib = t % IBW;
-                        const int R = (wm * IBW + ib) * 16 + rr;
-                        const int ao = R * H + 8 * ((4 * kc + gg) ^ sw);
-                        bh = *reinterpret_cast<const f16x8w*>(&AH[ao]);
-                        bl = *reinterpret_cast<const f16x8w*>(&AL[ao]);
-                    };
-                    __builtin_amdgcn_sched_barrier(0);
-                    constexpr int PD = kWinPD, NF = PD + 1, NTT = C::KC * IBW;
-                    f16x8w fh[NF], fl[NF];
-#pragma unroll
-                    for (int t = 0; t < PD && t < NTT; ++t) frag(t, fh[t], fl[t]);
-                    // codes form: the expansion rows between the MFMAs, one
-                    // every XS t-steps from t = XT (the codes DMA'd at B0)
-                    constexpr int XT = 2, XS = 2;
-                    [[maybe_unused]] f32x4 xd[2];
-#pragma unroll
-                    for (int t = 0; t < NTT; ++t) {
-                        const int kc = t / IBW, ib = t % IBW;
-                        if (t < NPC) dma_piece(t);
-                        if constexpr (X0) {
-                            // block i's MFMAs, block i - 1's store (its result landed)
-                            static_assert(!X0 || XT + XS * (NXB - 1) < NTT, "expansion inside the transform");
-                            const int i = (t - XT) / XS;
-                            if (t >= XT && (t - XT) % XS == 0 && i < NXB) {
-                                xd[i & 1] = xblock_mfma(i);
-                                if (i > 0) xblock_store(xn2, i - 1, xd[(i - 1) & 1]);
-                            }
-                        }
-                        if (MODE & 4) continue;
-                        if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
-#pragma unroll
-                        for (int cp = 0; cp < CPW; ++cp) {
-                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
-                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fl[t % NF], accm[ib][cp], 0, 0, 0);
-                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-#pragma unroll
-                    for (int t = NTT; t < NPC; ++t) dma_piece(t);
-                    if constexpr (X0) xblock_store(xn2, NXB - 1, xd[(NXB - 1) & 1]);
-                }
-                wtr.stamp(5);
-                {
-                    // epilogue stored straight from the accumulators: lane (rr, gg) of
-                    // block (ib, cp) holds row 16 ib + rr, columns n0 + 16 cp + 4 gg .. +3
-                    static_assert(IBW * CPW == C::NST, "one store per block keeps the per-step store count");
-#pragma unroll
-                    for (int cp = 0; cp < CPW; ++cp) {
-                        const int nc = n0 + 16 * cp + 4 * gg;
-                        const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + nc]);
-                        const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + nc]);
-#pragma unroll
-                        for (int ib = 0; ib < IBW; ++ib) {
-                            f32x4 o;
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                float v = ldexpf(accm[ib][cp][r], -(pr[ib] + qw[cp]));
-                                if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
-                                if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
-                                o[r] = v;
-                            }
-                            const int lr = (wm * IBW + ib) * 16 + rr;
-                            if (lr < nlocp)
-                                __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + nc));
-                        }
-                    }
-                }
-                wtr.stamp(7);
             }
-        } else {
+            // carry tile s into phase B
 #pragma unroll
-            for (int q = 0; q < NPC; ++q) dma_piece(q);
-            if constexpr (X0) {
+            for (int qd = 0; qd < C::NQ; ++qd) {
+                ncode[qd] = ncn[qd];
+                nwt[qd] = nwn[qd];
 #pragma unroll
-                for (int rbk = 0; rbk < NXB; ++rbk) xblock_store(xn2, rbk, xblock_mfma(rbk));
+                for (int j = 0; j < C::CH; ++j) accp[qd][j] = accn[qd][j];
             }
+            xs = xs == 2 ? 0 : xs + 1;
+            prv = cur;
+            cur = nx1;
+            nx1 = nx2;
+            c2.next(S.L);
         }
-        // carry tile s into phase B
-#pragma unroll
-        for (int qd = 0; qd < C::NQ; ++qd) {
-            ncode[qd] = ncn[qd];
-            nwt[qd] = nwn[qd];
-#pragma unroll
-            for (int j = 0; j < C::CH; ++j) accp[qd][j] = accn[qd][j];
-        }
-        xs = xs == 2 ? 0 : xs + 1;
-        prv = cur;
-        cur = nx1;
-        nx1 = nx2;
-        c2.next(S.L);
-    }
-    wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
+        wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
     }
 }
 
@@ -1882,6 +1709,278 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k) accp[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // schedule: cur / nx1 = tiles of steps s / s + 1, the cursor at s + 2
+    int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
+    WinCursor c2{0, 0, 0};
+    c2.next(S.L);
+    c2.next(S.L);
+    int xs = 0;
+    if constexpr (MIGNN_WIN64_PIPE) {
+    // ---- pipelined step (MIGNN_WIN64_PIPE): phase B and the split of tile
+    // s - 1 first (its +z rows are in tile s, landed at B0), its 24 MFMAs in
+    // four groups between phase A's slot batches of tile s, its epilogue,
+    // staging and stores before B1, then this step's DMA pieces
+    for (int s = 0;; ++s) {
+        if (cur < 0 && prv < 0) break;            // (uniform)
+        const int64_t nx2 = win_tile_c(S, p, c2);
+        const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1 (and of tile s + 2)
+        const int tq = static_cast<int>(s & 1);
+        const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
+        const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
+        const int64_t tp0 = rb + (prv >= 0 ? prv : 0) * C::BM;
+        const int64_t nlocp = prv >= 0 ? (re - tp0 < C::BM ? re - tp0 : C::BM) : 0;
+        const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
+        const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
+        wtr.flush(wave, s - 1);
+        wtr.stamp(0);
+        // (B0) this step's ext rows and the records of step s + 1 landed;
+        // younger: the own rows of tile s + 1 (the last step's stores are
+        // older: issued before its B1)
+        if (s == 0) wbar<wvm(0) & kWLgkm0>();
+        else wbar<wvm(C::NPX) & kWLgkm0>();
+        wtr.stamp(1);
+        // phase B of tile s - 1 and its split (registers only)
+        const bool mf = !AGG && prv >= 0;         // (uniform)
+        f16x8w bh[2], bl[2];
+        f32x4 acc[4];
+        int pe = 0;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (prv >= 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(lds + (ncode ^ coff[k]));
+#pragma unroll
+                for (int t = 0; t < 4; ++t) accp[k][t] = fmaf(nwt, v[t], accp[k][t]);
+            }
+        }
+        if constexpr (AGG) {
+            // the aggregate alone: tile s - 1's sums are its output -- staged
+            // and stored before phase A of tile s (the stores drain under it)
+            if (prv >= 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    *reinterpret_cast<f32x4*>(STG + rw * C::ROWB + (((coff[k] >> 4) ^ rw) << 4)) = accp[k];
+                const int ch = lane & 15;
+                f32x4 v[C::NST];
+#pragma unroll
+                for (int i = 0; i < C::NST; ++i) {
+                    const int sr = i * C::RPP + (lane >> 4);
+                    v[i] = *reinterpret_cast<const f32x4*>(STG + sr * C::ROWB + ((ch ^ sr) << 4));
+                }
+#pragma unroll
+                for (int i = 0; i < C::NST; ++i) {
+                    const int lr = C::RPW * wave + i * C::RPP + (lane >> 4);
+                    if (lr < nlocp)
+                        __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
+                }
+            }
+        }
+        if (mf) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) m = max(m, __float_as_uint(fabsf(accp[k][t])));
+            pe = wsplit_exp(wrow4_max(m));
+            const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float sv = accp[k][t] * sc;
+                    const _Float16 hh = static_cast<_Float16>(sv);
+                    bh[k >> 1][4 * (k & 1) + t] = hh;
+                    bl[k >> 1][4 * (k & 1) + t] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                }
+        }
+        // MFMA group g: column block g, both k-chunks
+        auto mid = [&](auto G) {
+            constexpr int cb = decltype(G)::value;
+            if (!mf) return;
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr ((MODE & 4) == 0) {
+#pragma unroll
+                for (int kc = 0; kc < 2; ++kc) {
+                    acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], bh[kc], acc[cb], 0, 0, 0);
+                    acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], bl[kc], acc[cb], 0, 0, 0);
+                    acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cb][kc], bh[kc], acc[cb], 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        // ---- phase A of tile s (the four MFMA groups between its batches)
+        f32x4 accn[4];
+        uint32_t ncn = C::OFF_ZERO;
+        float nwn = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) accn[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
+        const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+            *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
+        const bool live = cur >= 0;
+        const bool far = live && ((summ >> 8) & 1u) != 0u;
+        const int maxa = (live && !far) ? static_cast<int>(summ & 0xffu) : 0;
+        {
+            const unsigned char* rec = RW + rw * kWRec;
+            const uint4 cds = *reinterpret_cast<const uint4*>(rec);
+            auto codeof = [&](int u) -> uint32_t {
+                const uint32_t d = u < 2 ? cds.x : u < 4 ? cds.y : u < 6 ? cds.z : cds.w;
+                return (u & 1) ? (d >> 16) : (d & 0xffffu);
+            };
+            auto wld = [&](int u) -> float { return *reinterpret_cast<const float*>(rec + 16 + 4 * u); };
+            f32x4 vv[2][4];
+            float wv[2];
+            auto bload = [&](auto U0, auto NB) {
+                constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
+#pragma unroll
+                for (int uu = 0; uu < nb; ++uu) {
+                    const uint32_t cd = codeof(u0 + uu);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) vv[uu][k] = *reinterpret_cast<const f32x4*>(lds + (cd ^ coff[k]));
+                    wv[uu] = wld(u0 + uu);
+                }
+            };
+            auto bfma = [&](auto NB) {
+                constexpr int nb = decltype(NB)::value;
+#pragma unroll
+                for (int uu = 0; uu < nb; ++uu)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) accn[k][t] = fmaf(wv[uu], vv[uu][k][t], accn[k][t]);
+            };
+            using U0 = std::integral_constant<int, 0>;
+            using U2 = std::integral_constant<int, 2>;
+            using U4 = std::integral_constant<int, 4>;
+            using U6 = std::integral_constant<int, 6>;
+            using N1 = std::integral_constant<int, 1>;
+            using N2 = std::integral_constant<int, 2>;
+            if (maxa > 0) bload(U0{}, N2{});
+            mid(I0{});
+            if (maxa > 0) bfma(N2{});
+            if (maxa > 2) bload(U2{}, N2{});
+            mid(I1{});
+            if (maxa > 2) bfma(N2{});
+            if (maxa > 4) bload(U4{}, N2{});
+            mid(I2{});
+            if (maxa > 4) bfma(N2{});
+            if (maxa > 6) bload(U6{}, N1{});
+            mid(I3{});
+            if (maxa > 6) bfma(N1{});
+            if (live && !far) {
+                ncn = codeof(7);
+                nwn = wld(7);
+            }
+        }
+        if (far && lrow < nloc) {
+            // CSR path: the full sum in CSR order, the current tile from
+            // LDS, every other row from x (L2); 2 entries at a time
+            const int64_t row = t0 + lrow;
+            const int eb = row_ptr[row], ee = row_ptr[row + 1];
+            for (int e = eb; e < ee; e += 2) {
+                int cj[2];
+                float wj[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const bool v = e + u < ee;
+                    cj[u] = v ? col[e + u] : -1;
+                    wj[u] = v ? ew[e + u] : 0.f;
+                }
+                f32x4 vv[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int64_t off = static_cast<int64_t>(cj[u]) - t0;
+                    if (cj[u] < 0) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) vv[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    } else if (off >= 0 && off < nloc) {
+                        const uint32_t o = static_cast<uint32_t>(off);
+                        const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB) | ((o & C::SWZ) << 4);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) vv[u][k] = *reinterpret_cast<const f32x4*>(lds + (a ^ coff[k]));
+                    } else {
+                        const float* rp = x + static_cast<int64_t>(cj[u]) * ldx;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) vv[u][k] = *reinterpret_cast<const f32x4*>(rp + (coff[k] >> 2));
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) accn[k][t] = fmaf(wj[u], vv[u][k][t], accn[k][t]);
+            }
+        }
+        wtr.stamp(2);
+        // epilogue of tile s - 1 (residual from slot (s-1) % 3, before B1),
+        // the wave's 16 rows staged in its own LDS region and read back whole
+        f32x4 vst[C::NST];
+        if (mf) {
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) {
+                const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[16 * cb + 4 * g]);
+                f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (has_res)
+                    rv = *reinterpret_cast<const f32x4*>(XP + lrow * C::ROWB + (((4 * cb + g) ^ rw) << 4));
+                const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + 16 * cb + 4 * g]);
+                const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + 16 * cb + 4 * g]);
+                f32x4 o;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    float v = ldexpf(acc[cb][t], -(pe + qw[cb])) + (rv[t] + bo[t]);
+                    if (flags & MIGNN_EPI_AFFINE) v = v * so[t] + ho[t];
+                    if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
+                    o[t] = v;
+                }
+                *reinterpret_cast<f32x4*>(STG + rw * C::ROWB + (((4 * cb + g) ^ rw) << 4)) = o;
+            }
+            const int ch = lane & 15;
+#pragma unroll
+            for (int i = 0; i < C::NST; ++i) {
+                const int sr = i * C::RPP + (lane >> 4);
+                vst[i] = *reinterpret_cast<const f32x4*>(STG + sr * C::ROWB + ((ch ^ sr) << 4));
+            }
+#pragma unroll
+            for (int i = 0; i < C::NST; ++i) {
+                const int lr = C::RPW * wave + i * C::RPP + (lane >> 4);
+                if (lr < nlocp)
+                    __builtin_nontemporal_store(vst[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
+            }
+        }
+        wtr.stamp(3);
+        // (B1) slot (s-1) % 3, the ext area and this step's records free
+        wbar<kWLgkm0>();
+        {
+            const int64_t tn2 = nx2;
+            // (the ext list of step s + 1 landed at B0; its TAB slot is not
+            // refilled this step)
+            const unsigned char* es[C::NPE];
+#pragma unroll
+            for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, nx1 >= 0);
+#pragma unroll
+            for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
+            dma_tab(tn2, tq);
+#pragma unroll
+            for (int pp = 0; pp < C::NPX; ++pp) dma_own(tn2, xp, pp);
+        }
+        wtr.stamp(5);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) accp[k] = accn[k];
+        ncode = ncn;
+        nwt = nwn;
+        xs = xs == 2 ? 0 : xs + 1;
+        prv = cur;
+        cur = nx1;
+        nx1 = nx2;
+        c2.next(S.L);
+    }
+    } else {
     // schedule: cur / nx1 = tiles of steps s / s + 1, the cursor at s + 2
     int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
     WinCursor c2{0, 0, 0};
@@ -2130,6 +2229,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         cur = nx1;
         nx1 = nx2;
         c2.next(S.L);
+    }
     }
     wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
 }

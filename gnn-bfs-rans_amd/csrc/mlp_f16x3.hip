@@ -27,6 +27,12 @@
 // at H = 128: 2 x 64 KiB + 32 KiB) and reads W4 / the biases through L1/L2.
 #include "common.hpp"
 
+// W-fragment prefetch depth of the head's MFMA loops, in (block, k-step)
+// steps of 3 MFMAs
+#ifndef MIGNN_HEAD_WPD
+#define MIGNN_HEAD_WPD 1
+#endif
+
 namespace mignn {
 namespace {
 
@@ -161,16 +167,18 @@ __device__ __forceinline__ void layer_mfma(f32x16* acc, float sc, const unsigned
         hi = *reinterpret_cast<const f16x8*>(wl + i * FRAG + loff);
         lo = *reinterpret_cast<const f16x8*>(wl + i * FRAG + 64 * 16 + loff);
     };
-    f16x8 wh[2], wo[2];
-    ld(0, wh[0], wo[0]);
+    constexpr int WPD = MIGNN_HEAD_WPD, WNF = WPD + 1;
+    f16x8 wh[WNF], wo[WNF];
+#pragma unroll
+    for (int i = 0; i < WPD; ++i) ld(i, wh[i], wo[i]);
 #pragma unroll
     for (int i = 0; i < NB * KT; ++i) {
         const int nb = i / KT, t = i % KT;
         if (t == 0) acc[nb] *= sc;   // raw bias (loaded early) -> seed: waits here only
-        if (i + 1 < NB * KT) ld(i + 1, wh[(i + 1) & 1], wo[(i + 1) & 1]);
-        acc[nb] = mfma32(wh[i & 1], ah[t], acc[nb]);
-        acc[nb] = mfma32(wh[i & 1], al[t], acc[nb]);
-        acc[nb] = mfma32(wo[i & 1], ah[t], acc[nb]);
+        if (i + WPD < NB * KT) ld(i + WPD, wh[(i + WPD) % WNF], wo[(i + WPD) % WNF]);
+        acc[nb] = mfma32(wh[i % WNF], ah[t], acc[nb]);
+        acc[nb] = mfma32(wh[i % WNF], al[t], acc[nb]);
+        acc[nb] = mfma32(wo[i % WNF], ah[t], acc[nb]);
         __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);

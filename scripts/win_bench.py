@@ -28,12 +28,13 @@ nx, ny, nz = (int(v) for v in os.environ.get("WB_GRID", "250,200,200").split(","
 pos, ei = grid_graph(nx, ny, nz, device=dev)
 n = pos.shape[0]
 old = os.environ.get("WB_OLD", "1") != "0"
-_, inv_c, info = locality_order(pos, ei, cols=True)
+perm_c, inv_c, info = locality_order(pos, ei, cols=True)
 csr_c = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv_c)
 csr_b = None
 if old:
     _, inv_b = locality_order(pos, ei)
     csr_b = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv_b)
+pos_c = pos[perm_c].contiguous()          # coordinates in the column order (layer-0 codes)
 del ei, pos
 nnz = int(csr_c.row_ptr[-1].item())
 # the product entry points from the product library (the diag build carries
@@ -99,7 +100,21 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     res.setdefault("win_plan_stats", {})[H] = wstats.tolist()
     res.setdefault("win_header", {})[H] = hdr[:32].view(torch.int32).tolist() + hdr[32:64].view(torch.int64).tolist()
     cases = {"win_plan": mk_wplan, "win": win, "win_aggregate": win_agg}
-    vout = {}
+    codes = xcoef = None
+    if H == 128:
+        # the codes form (layer 1 from layer 0's row codes: the headline's layer 1)
+        codes = torch.zeros((n, 8), dtype=torch.float32, device=dev)
+        xcoef = (torch.randn(H, 8, device=dev, generator=g) * 0.5).contiguous()
+        _lib.check(LP.mignn_gcn_layer0_codes(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(pos_c), 3, 3,
+                                             0, n, P(codes), 8, st), "codes")
+        Ywc = torch.empty_like(X)
+
+        def win_codes(VL=LP, pl=wplan, Yo=Ywc):
+            _lib.check(VL.mignn_gcn_layer_win_codes(P(pl), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
+                                                    P(codes), 8, 0, n, H, P(xcoef), P(W), P(b), P(sc),
+                                                    P(sh), 15, P(Yo), H, st), "win_codes")
+        cases["win_codes"] = win_codes
+    vout, vchecks = {}, {}
     for vname, VL in VARIANTS.items():
         # each variant builds its own plan (plan formats may differ)
         vnb = VL.mignn_gcn_win_plan_bytes(0, n, H)
@@ -109,15 +124,22 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
         Yv = torch.empty_like(X)
         vout[vname] = Yv
 
-        def fv(VL=VL, vplan=vplan, Yv=Yv):
+        def fv(VL=VL, vplan=vplan, Yv=Yw):
+            # (timed into the product's output buffer: same pages for every variant)
             _lib.check(VL.mignn_gcn_layer_win(P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
                                               H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yv), H, st), "wv")
+        vcheck = (lambda VL=VL, vplan=vplan, Yv=Yv: _lib.check(VL.mignn_gcn_layer_win(
+            P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X), H, 0, n, H, P(W), P(b), P(sc),
+            P(sh), 15, P(Yv), H, st), "wv"))
+        vchecks[vname] = vcheck
 
         def fva(VL=VL, vplan=vplan):
             _lib.check(VL.mignn_gcn_aggregate_win(P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
-                                                  P(X), H, 0, n, H, P(Yd), H, st), "wva")
+                                                  P(X), H, 0, n, H, P(Ywa), H, st), "wva")
         cases[f"win@{vname}"] = fv
         cases[f"win_aggregate@{vname}"] = fva
+        if codes is not None:
+            cases[f"win_codes@{vname}"] = (lambda VL=VL, vplan=vplan: win_codes(VL, vplan, Ywc))
     for m in [int(v) for v in os.environ.get("WB_MODES", "").split(",") if v]:
         def fw(m=m):
             _lib.check(L.mignn_diag_win(m, P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
@@ -155,7 +177,7 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     out["win_deterministic"] = bool(torch.equal(Yw, Yw2))
     del Yw2
     for vname in vout:
-        cases[f"win@{vname}"]()
+        vchecks[vname]()
         torch.cuda.synchronize()
         out[f"win_vs_{vname}_max_diff"] = (Yw - vout[vname]).abs().max().item()
         out[f"win_vs_{vname}_bitwise"] = bool(torch.equal(Yw, vout[vname]))
