@@ -71,16 +71,6 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 #define MIGNN_WIN_PDX 1
 #endif
 constexpr int kWinPD = MIGNN_WIN_PD, kWinPDX = MIGNN_WIN_PDX;   // (codes form: PDX)
-// the pipelined step's DMA pieces interleaved with phase B and the split (1)
-// or issued together after B1 (0)
-// H = 64: the pipelined step (1: phase B + split first, the MFMAs inside
-// phase A, the epilogue before B1) or the round-5 order (0)
-#ifndef MIGNN_WIN64_PIPE
-#define MIGNN_WIN64_PIPE 1
-#endif
-#ifndef MIGNN_WIN_DMAIL
-#define MIGNN_WIN_DMAIL 1
-#endif
 constexpr int kWRec = 48;                 // bytes per plan record: 8 u16 codes + 8 f32 weights
 constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the next-tile entry
 constexpr int kWHdr = 256;                // plan header bytes
@@ -1299,7 +1289,8 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             // DMA pieces of this step: ext rows of step s + 1, the records of
             // step s + 2, the own rows of tile s + 2 (codes form: the records
             // only), issued between phase B's and the split's VALU work
-            // (MIGNN_WIN_DMAIL; 0: all at once after B1)
+            // (as a burst after B1 they stall the vector memory pipe: 3.26
+            // vs 2.86 ms)
             const unsigned char* es[C::NPE];
             if constexpr (!X0) {
                 // this wave's records of step s + 1 landed (its ext list);
@@ -1327,8 +1318,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                 for (int q = q0; q < q1 && q < NPC; ++q) dpiece(q);
                 __builtin_amdgcn_sched_barrier(0);
             };
-            constexpr bool DIL = MIGNN_WIN_DMAIL != 0;
-            if (!DIL || prv < 0) dpieces(0, NPC);
+            if (prv < 0) dpieces(0, NPC);
             wtr.stamp(4);
             // ---- phase B of tile s - 1 (its +z term, from tile s), split
             if (prv >= 0) {
@@ -1339,7 +1329,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
 #pragma unroll
                     for (int j = 0; j < C::CH; ++j) pv[qd][j] = *reinterpret_cast<const f32x4*>(lds + ad + 256 * j);
                 }
-                if (DIL) dpieces(0, 3);
+                dpieces(0, 3);
 #pragma unroll
                 for (int qd = 0; qd < C::NQ; ++qd)
 #pragma unroll
@@ -1348,7 +1338,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         for (int r = 0; r < 4; ++r) accp[qd][j][r] = fmaf(nwt[qd], pv[qd][j][r], accp[qd][j][r]);
 #pragma unroll
                 for (int qd = 0; qd < C::NQ; ++qd) {
-                    if (DIL && qd == 1) dpieces(3, 5);
+                    if (qd == 1) dpieces(3, 5);
                     uint32_t m = 0;
 #pragma unroll
                     for (int j = 0; j < C::CH; ++j)
@@ -1376,7 +1366,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                     }
                     if (iq == 0) REXP[C::RPW * wave + 4 * qd + (ln >> 4)] = pe;
                 }
-                if (DIL) dpieces(5, NPC);
+                dpieces(5, NPC);
             }
             if constexpr (X0) {
                 // codes form: tile s + 2's own rows (slot (s-1) % 3) and step s +
@@ -1715,8 +1705,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
     c2.next(S.L);
     c2.next(S.L);
     int xs = 0;
-    if constexpr (MIGNN_WIN64_PIPE) {
-    // ---- pipelined step (MIGNN_WIN64_PIPE): phase B and the split of tile
+    // ---- the pipelined step: phase B and the split of tile
     // s - 1 first (its +z rows are in tile s, landed at B0), its 24 MFMAs in
     // four groups between phase A's slot batches of tile s, its epilogue,
     // staging and stores before B1, then this step's DMA pieces
@@ -1979,257 +1968,6 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         cur = nx1;
         nx1 = nx2;
         c2.next(S.L);
-    }
-    } else {
-    // schedule: cur / nx1 = tiles of steps s / s + 1, the cursor at s + 2
-    int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
-    WinCursor c2{0, 0, 0};
-    c2.next(S.L);
-    c2.next(S.L);
-    int xs = 0;
-    for (int s = 0;; ++s) {
-        if (cur < 0 && prv < 0) break;            // (uniform)
-        const int64_t nx2 = win_tile_c(S, p, c2);
-        const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1 (and of tile s + 2)
-        const int tq = static_cast<int>(s & 1);
-        const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
-        const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
-        const int64_t tp0 = rb + (prv >= 0 ? prv : 0) * C::BM;
-        const int64_t nlocp = prv >= 0 ? (re - tp0 < C::BM ? re - tp0 : C::BM) : 0;
-        const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
-        const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
-        wtr.flush(wave, s - 1);
-        wtr.stamp(0);
-        // (B0) this step's ext rows and the records of step s + 1 landed;
-        // younger: the own rows of tile s + 1, the last step's stores
-        if (s == 0) wbar<wvm(0) & kWLgkm0>();
-        else if (s == 1) wbar<wvm(C::NPX) & kWLgkm0>();
-        else wbar<wvm(C::NPX + C::NST) & kWLgkm0>();
-        wtr.stamp(1);
-        // reads with no dependence on this step's arithmetic, first: the ext
-        // list of step s + 1 (its DMA goes out after B1) and tile s - 1's +z
-        // rows (phase B, slot s % 3)
-        const unsigned char* es[C::NPE];
-#pragma unroll
-        for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, nx1 >= 0);
-        f32x4 pbv[4];
-        if (prv >= 0) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) pbv[k] = *reinterpret_cast<const f32x4*>(lds + (ncode ^ coff[k]));
-        }
-
-        // ---- phase A of tile s
-        f32x4 accn[4];
-        uint32_t ncn = C::OFF_ZERO;
-        float nwn = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) accn[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (cur >= 0) {
-            const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
-            const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-                *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
-            const int maxa = static_cast<int>(summ & 0xffu);
-            const bool far = ((summ >> 8) & 1u) != 0u;
-            if (!far) {
-                const unsigned char* rec = RW + rw * kWRec;
-                const uint4 cds = *reinterpret_cast<const uint4*>(rec);
-                const uint4 w03 = *reinterpret_cast<const uint4*>(rec + 16);
-                const uint4 w47 = *reinterpret_cast<const uint4*>(rec + 32);
-                auto codeof = [&](int u) -> uint32_t {
-                    const uint32_t d = u < 2 ? cds.x : u < 4 ? cds.y : u < 6 ? cds.z : cds.w;
-                    return (u & 1) ? (d >> 16) : (d & 0xffffu);
-                };
-                auto wof = [&](int u) -> float {
-                    const uint32_t d = u == 0 ? w03.x : u == 1 ? w03.y : u == 2 ? w03.z : u == 3 ? w03.w
-                                     : u == 4 ? w47.x : u == 5 ? w47.y : u == 6 ? w47.z : w47.w;
-                    return __uint_as_float(d);
-                };
-                auto batch = [&](auto U0, auto NB) {
-                    constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
-                    f32x4 vv[nb][4];
-#pragma unroll
-                    for (int uu = 0; uu < nb; ++uu) {
-                        const uint32_t cd = codeof(u0 + uu);
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) vv[uu][k] = *reinterpret_cast<const f32x4*>(lds + (cd ^ coff[k]));
-                    }
-#pragma unroll
-                    for (int uu = 0; uu < nb; ++uu) {
-                        const float w = wof(u0 + uu);
-#pragma unroll
-                        for (int k = 0; k < 4; ++k)
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) accn[k][t] = fmaf(w, vv[uu][k][t], accn[k][t]);
-                    }
-                };
-                // (batches of 2 slots: the 256-VGPR budget)
-                if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
-                if (maxa > 2) batch(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
-                if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
-                if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
-                ncn = codeof(7);
-                nwn = wof(7);
-            } else if (lrow < nloc) {
-                // CSR path: the full sum in CSR order, the current tile from
-                // LDS, every other row from x (L2); 2 entries at a time (registers)
-                const int64_t row = t0 + lrow;
-                const int eb = row_ptr[row], ee = row_ptr[row + 1];
-                for (int e = eb; e < ee; e += 2) {
-                    int cj[2];
-                    float wj[2];
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const bool v = e + u < ee;
-                        cj[u] = v ? col[e + u] : -1;
-                        wj[u] = v ? ew[e + u] : 0.f;
-                    }
-                    f32x4 vv[2][4];
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const int64_t off = static_cast<int64_t>(cj[u]) - t0;
-                        if (cj[u] < 0) {
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) vv[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-                        } else if (off >= 0 && off < nloc) {
-                            const uint32_t o = static_cast<uint32_t>(off);
-                            const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB) | ((o & C::SWZ) << 4);
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) vv[u][k] = *reinterpret_cast<const f32x4*>(lds + (a ^ coff[k]));
-                        } else {
-                            const float* rp = x + static_cast<int64_t>(cj[u]) * ldx;
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) vv[u][k] = *reinterpret_cast<const f32x4*>(rp + (coff[k] >> 2));
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < 2; ++u)
-#pragma unroll
-                        for (int k = 0; k < 4; ++k)
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) accn[k][t] = fmaf(wj[u], vv[u][k][t], accn[k][t]);
-                }
-            }
-        }
-        // residual + bias of tile s - 1 (row lrow, columns 16 cb + 4 g ..), read
-        // before slot (s-1) % 3 is refilled
-        f32x4 seed[4];
-        if constexpr (!AGG) {
-            if (prv >= 0) {
-#pragma unroll
-                for (int cb = 0; cb < 4; ++cb) {
-                    const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[16 * cb + 4 * g]);
-                    f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
-                    if (has_res)
-                        rv = *reinterpret_cast<const f32x4*>(XP + lrow * C::ROWB + (((4 * cb + g) ^ rw) << 4));
-                    seed[cb] = rv + bo;
-                }
-            }
-        }
-        wtr.stamp(2);
-        // (B1) slot (s-1) % 3, the ext area and this step's records free
-        wbar<kWLgkm0>();
-        wtr.stamp(3);
-        wtr.stamp(6);
-        {
-            const int64_t tn2 = nx2;
-#pragma unroll
-            for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
-            dma_tab(tn2, tq);
-#pragma unroll
-            for (int pp = 0; pp < C::NPX; ++pp) dma_own(tn2, xp, pp);
-        }
-
-        if (prv >= 0) {
-            // ---- phase B of tile s - 1 (its +z term, read after B0)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) accp[k][t] = fmaf(nwt, pbv[k][t], accp[k][t]);
-            if constexpr (AGG) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    *reinterpret_cast<f32x4*>(STG + rw * C::ROWB + (((coff[k] >> 4) ^ rw) << 4)) = accp[k];
-            } else {
-                // split: one power-of-two scale per row (its 4 lanes)
-                uint32_t m = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) m = max(m, __float_as_uint(fabsf(accp[k][t])));
-                const int pe = wsplit_exp(wrow4_max(m));
-                const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
-                f16x8w bh[2], bl[2];
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const float sv = accp[k][t] * sc;
-                        const _Float16 hh = static_cast<_Float16>(sv);
-                        bh[k >> 1][4 * (k & 1) + t] = hh;
-                        bl[k >> 1][4 * (k & 1) + t] = static_cast<_Float16>(sv - static_cast<float>(hh));
-                    }
-                f32x4 acc[4];
-#pragma unroll
-                for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if constexpr (!(MODE & 4)) {
-#pragma unroll
-                    for (int kc = 0; kc < 2; ++kc)
-#pragma unroll
-                        for (int cb = 0; cb < 4; ++cb) {
-                            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], bh[kc], acc[cb], 0, 0, 0);
-                            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cb][kc], bl[kc], acc[cb], 0, 0, 0);
-                            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cb][kc], bh[kc], acc[cb], 0, 0, 0);
-                        }
-                }
-                wtr.stamp(4);
-                // epilogue (gnn_model.py:184-191: conv + bias, + x, BN, ReLU):
-                // lane (r, g) holds row rw, columns 16 cb + 4 g + t
-#pragma unroll
-                for (int cb = 0; cb < 4; ++cb) {
-                    const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + 16 * cb + 4 * g]);
-                    const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + 16 * cb + 4 * g]);
-                    f32x4 o;
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        float v = ldexpf(acc[cb][t], -(pe + qw[cb])) + seed[cb][t];
-                        if (flags & MIGNN_EPI_AFFINE) v = v * so[t] + ho[t];
-                        if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
-                        o[t] = v;
-                    }
-                    *reinterpret_cast<f32x4*>(STG + rw * C::ROWB + (((4 * cb + g) ^ rw) << 4)) = o;
-                }
-            }
-            // the wave's 16 rows out, whole rows (its own staging region: LDS
-            // ops of one wave complete in order, no barrier)
-            {
-                const int ch = lane & 15;
-                f32x4 v[C::NST];
-#pragma unroll
-                for (int i = 0; i < C::NST; ++i) {
-                    const int sr = i * C::RPP + (lane >> 4);
-                    v[i] = *reinterpret_cast<const f32x4*>(STG + sr * C::ROWB + ((ch ^ sr) << 4));
-                }
-#pragma unroll
-                for (int i = 0; i < C::NST; ++i) {
-                    const int lr = C::RPW * wave + i * C::RPP + (lane >> 4);
-                    // (a partial tile is the last of its workgroup: fewer
-                    // stores there change no later wait)
-                    if (lr < nlocp)
-                        __builtin_nontemporal_store(v[i], reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + 4 * ch));
-                }
-            }
-            wtr.stamp(5);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) accp[k] = accn[k];
-        ncode = ncn;
-        nwt = nwn;
-        xs = xs == 2 ? 0 : xs + 1;
-        prv = cur;
-        cur = nx1;
-        nx1 = nx2;
-        c2.next(S.L);
-    }
     }
     wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
 }
