@@ -42,10 +42,12 @@
 // columns of the same y-row -- for the full columns of the order, then the
 // remaining tiles as contiguous chunks.  Any CSR is correct under any order:
 // the plan classifies every entry by where its row is resident at that step.
-// Plan records: 48 B per row -- slots 0..6 {u16 code, f32 w} in CSR order
-// (code = the LDS offset of the neighbour row, >> 1 at H = 128), slot 7 the
-// +z (next-tile) entry; waves with a row outside that form (degree > 8, ext
-// capacity exceeded) take the CSR path (row_ptr / col / ew, global x).
+// Plan records: 16 B per row -- slots 0..6 u16 codes in CSR order (code = the
+// LDS offset of the neighbour row, >> 1 at H = 128, | its degree class), slot
+// 7 the +z (next-tile) entry; the weights dinv_j dinv_i are rebuilt in LDS
+// from the classes (win_rexp).  Waves with a row outside that form (degree >
+// 8, ext capacity exceeded, a weight that is not dv[c_j] dv[c_i]) take the
+// CSR path (row_ptr / col / ew, global x).
 #include <type_traits>
 
 #include "common.hpp"
@@ -67,11 +69,13 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 #ifndef MIGNN_WIN_PD
 #define MIGNN_WIN_PD 3
 #endif
-#ifndef MIGNN_WIN_PDX
-#define MIGNN_WIN_PDX 1
-#endif
-constexpr int kWinPD = MIGNN_WIN_PD, kWinPDX = MIGNN_WIN_PDX;   // (codes form: PDX)
-constexpr int kWRec = 48;                 // bytes per plan record: 8 u16 codes + 8 f32 weights
+constexpr int kWinPD = MIGNN_WIN_PD;
+// Plan record of a row: 8 u16 codes (16 B), each with the neighbour's degree
+// class in its low 3 bits (the code's LDS offset is 16-B aligned: those bits
+// are free), plus the row's own class in a nibble of its wave's list.  The
+// weight w_ij = dinv_j dinv_i is rebuilt in LDS from the plan's class table
+// (round 6: 48 -> 16 B per row; the 8 f32 weights were 0.32 GB per launch)
+constexpr int kWRec = 16;                 // plan bytes per row (global)
 constexpr int kWA = 7;                    // slots 0..6: phase A; slot 7: the next-tile entry
 constexpr int kWHdr = 256;                // plan header bytes
 constexpr uint32_t kWMagic = 0x4E495747u;
@@ -93,13 +97,16 @@ struct WCfg {
     static constexpr int KX = 32;                      // ext rows per tile (an 8x8 plane's faces)
     static constexpr int EXT_BYTES = KX * ROWB;
     static constexpr int EPW = KX / NW;                // ext rows DMA'd per wave
-    static constexpr int XLW = (EPW + 4) / 4 * 4;      // ext-list group per wave: EPW columns, summary
-    static constexpr int RECW = RPW * kWRec + XLW * 4; // a wave's records + list in LDS
-    static constexpr int RLANES = RPW * kWRec / 16;    // lanes of the records' DMA
-    static constexpr int TLANES = RECW / 16;
-    static constexpr int TAB_BYTES = BM * kWRec + NW * XLW * 4;
+    static constexpr int XLW = (EPW + 4) / 4 * 4;      // ext-list group per wave: EPW columns, summary, row classes
+    static constexpr int RECG = RPW * kWRec + XLW * 4; // a wave's codes + list in the plan (DMA'd as is)
+    static constexpr int OFF_RL = RPW * kWRec;         // in a wave's LDS records: the list
+    static constexpr int OFF_RW = RECG;                // the weights [RPW][8] (rebuilt in LDS)
+    static constexpr int RECW = RECG + RPW * 32;       // a wave's records in LDS
+    static constexpr int TLANES = RECG / 16;
+    static constexpr int TAB_G = NW * RECG;            // plan bytes per tile
+    static constexpr int TAB_BYTES = NW * RECW;        // LDS bytes per tile
     static constexpr int A_BYTES = BM * H * 2;         // hi or lo image (16-B chunks swizzled)
-    // LDS: X[3] | EXT | ZERO (the code-addressed region) | TAB[2] | AH | AL | REXP | EPI
+    // LDS: X[3] | EXT | ZERO (the code-addressed region) | TAB[2] | AH | AL | REXP | EPI | DV
     static constexpr int OFF_X = 0;
     static constexpr int OFF_EXT = NSLOT * X_BYTES;
     static constexpr int OFF_ZERO = OFF_EXT + EXT_BYTES;
@@ -110,7 +117,8 @@ struct WCfg {
     static constexpr int OFF_AL = OFF_AH + A_BYTES;
     static constexpr int OFF_REXP = OFF_AL + A_BYTES;
     static constexpr int OFF_EPI = OFF_REXP + BM * 4;
-    static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
+    static constexpr int OFF_DV = OFF_EPI + 3 * H * 4; // the plan's dinv table [8]
+    static constexpr int LDS_BYTES = OFF_DV + 32;
     // layer 1 from layer-0 codes (MODE 64): per wave 8 own-row + 4 ext-row
     // codes (32 B each) DMA'd per step, the [H][8] expansion table
     static constexpr int CODEB = 32, CODE_W = (RPW + KX / NW) * CODEB;
@@ -128,9 +136,9 @@ struct WCfg {
     static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
     static_assert(LDS_BYTES_X0 * WGPC <= 160 * 1024, "LDS budget (codes form)");
     static_assert(RPW == 8 && KX / NW == 4 && CODE_W / 16 <= 64, "codes DMA: 16 own + 8 ext lanes");
-    static_assert(EPW == NPE * RPP && EPW + 1 <= XLW, "ext rows per wave");
+    static_assert(EPW == NPE * RPP && EPW + 1 + RPW / 8 <= XLW, "ext rows per wave, row classes");
     static_assert((CODE_END >> CSH) <= 65536, "u16 codes");
-    static_assert(RECW % 16 == 0 && TLANES <= 64 && TAB_BYTES % 16 == 0, "records DMA");
+    static_assert(RECG % 16 == 0 && TLANES <= 64 && RECW % 16 == 0, "records DMA");
 };
 
 // H = 64: the wave-independent kernel (gcn_win64_kernel).  4 waves of 16 rows
@@ -152,12 +160,14 @@ struct WCfg<64> {
     static constexpr int EXT_BYTES = KX * ROWB;
     static constexpr int EPW = KX / NW;                // 8
     static constexpr int XLW = (EPW + 4) / 4 * 4;      // 12
-    static constexpr int RECW = RPW * kWRec + XLW * 4;
-    static constexpr int RLANES = RPW * kWRec / 16;
-    static constexpr int TLANES = RECW / 16;
-    static constexpr int TAB_BYTES = BM * kWRec + NW * XLW * 4;
+    static constexpr int RECG = RPW * kWRec + XLW * 4;
+    static constexpr int OFF_RL = RPW * kWRec, OFF_RW = RECG;
+    static constexpr int RECW = RECG + RPW * 32;
+    static constexpr int TLANES = RECG / 16;
+    static constexpr int TAB_G = NW * RECG;
+    static constexpr int TAB_BYTES = NW * RECW;
     static constexpr int STG_BYTES = RPW * ROWB;       // a wave's output staging
-    // LDS: X[3] | EXT | ZERO (code-addressed) | TAB[2] | STG[NW] | EPI
+    // LDS: X[3] | EXT | ZERO (code-addressed) | TAB[2] | STG[NW] | EPI | DV
     static constexpr int OFF_X = 0;
     static constexpr int OFF_EXT = NSLOT * X_BYTES;
     static constexpr int OFF_ZERO = OFF_EXT + EXT_BYTES;
@@ -166,16 +176,17 @@ struct WCfg<64> {
     static constexpr int OFF_TAB = CODE_END;
     static constexpr int OFF_STG = OFF_TAB + 2 * TAB_BYTES;
     static constexpr int OFF_EPI = OFF_STG + NW * STG_BYTES;
-    static constexpr int LDS_BYTES = OFF_EPI + 3 * H * 4;
+    static constexpr int OFF_DV = OFF_EPI + 3 * H * 4;
+    static constexpr int LDS_BYTES = OFF_DV + 32;
     static constexpr int WGPC = 2;
     static constexpr int RPP = 1024 / ROWB, LPR = 64 / RPP;   // 4 rows of 16 lanes per DMA piece
     static constexpr int NPX = X_BYTES / 1024 / NW;    // 4
     static constexpr int NPE = EXT_BYTES / 1024 / NW;  // 2
     static constexpr int NST = RPW / RPP;              // 4 whole-row stores per wave
     static_assert(LDS_BYTES * WGPC <= 160 * 1024, "LDS budget");
-    static_assert(EPW == NPE * RPP && EPW + 1 <= XLW, "ext rows per wave");
+    static_assert(EPW == NPE * RPP && EPW + 1 + RPW / 8 <= XLW, "ext rows per wave, row classes");
     static_assert(CODE_END <= 65536, "u16 codes");
-    static_assert(RECW % 16 == 0 && TLANES <= 64 && TAB_BYTES % 16 == 0 && OFF_STG % 16 == 0, "records DMA");
+    static_assert(RECG % 16 == 0 && TLANES <= 64 && RECW % 16 == 0 && OFF_STG % 16 == 0, "records DMA");
 };
 
 // ------------------------------------------------------------------ schedule
@@ -188,6 +199,7 @@ struct WinHdr {
     int32_t R1, chunk, nsteps, Z;
     int64_t ntiles, t2, rb, re;
     int32_t zrun;   // (plan build) tiles from tile 0 that chain as z-planes of one column
+    float dv[8];    // degree class c -> dinv = (c + 1)^-1/2 (csr_finalize_kernel's expression)
 };
 static_assert(sizeof(WinHdr) <= kWHdr, "plan header");
 
@@ -298,6 +310,7 @@ __global__ void win_hdr_kernel(WinHdr* hdr, const int32_t* __restrict__ info, in
     hdr->t2 = static_cast<int64_t>(bestR1) * G * bestL;
     hdr->rb = rb;
     hdr->re = re;
+    for (int c = 0; c < 8; ++c) hdr->dv[c] = 1.0f / sqrtf(static_cast<float>(c + 1));
 }
 
 __device__ inline WinSched win_sched(const WinHdr* h) {
@@ -460,6 +473,29 @@ struct WTrace {
     }
 };
 
+// The weights of a wave's records in LDS (RW: its TAB slot region), from
+// the codes' degree classes: lane (row, slot) writes w = dv[c_j] dv[c_i]
+// (csr_finalize_kernel's dinv_j * dinv_i, bitwise -- the plan checked every
+// entry) and clears the code's class bits.  Run on records this wave DMA'd
+// itself once its vmcnt covers them; wave-local (LDS is in order within a
+// wave), so no barrier.
+template <class C>
+__device__ __forceinline__ void win_rexp(unsigned char* RW, const float* DV, int lane) {
+    // (lane opaque: its offsets hoisted out of the step loop would be live
+    // through the kernels' register peak)
+    asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int it = 0; it < C::RPW / 8; ++it) {
+        const int row = 8 * it + (lane >> 3), u = lane & 7;
+        uint16_t* const cp = reinterpret_cast<uint16_t*>(RW + row * kWRec) + u;
+        const uint32_t cd = *cp;
+        const uint32_t cw = *reinterpret_cast<const uint32_t*>(RW + C::OFF_RL + 4 * (C::EPW + 1 + it));
+        const uint32_t ci = (cw >> (4 * (row & 7))) & 7u;
+        *reinterpret_cast<float*>(RW + C::OFF_RW + row * 32 + 4 * u) = DV[cd & 7u] * DV[ci];
+        *cp = static_cast<uint16_t>(cd & ~7u);
+    }
+}
+
 // ------------------------------------------------------------------ plan
 // One 64-thread block per tile, a thread per row.  Entry classes at the
 // tile's step: the current tile (slot s % 3), the workgroup's previous tile
@@ -481,6 +517,9 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
     const int64_t rb = hdr->rb, re = hdr->re, ntiles = hdr->ntiles;
     __shared__ uint32_t xl[C::NW * C::XLW];
     const uint32_t zcode = static_cast<uint32_t>(C::OFF_ZERO >> C::CSH);
+    float dv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) dv[c] = hdr->dv[c];
     for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         int p, s;
         win_where32(S, static_cast<int>(t), p, s);
@@ -532,6 +571,30 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
                 wj[e] = 0u;
             }
         }
+        // degree classes: the row's own from its self entry (weight dv[c]^2),
+        // each entry's c_j with weight == dv[c_j] dv[c_i] bitwise (the
+        // kernel rebuilds exactly that product); a row with an entry outside
+        // that form (no self entry, a weighted graph, a degree > 8) takes
+        // the CSR path, which reads ew itself
+        int ci = -1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (cj[e] >= 0 && static_cast<int64_t>(cj[e]) == r)
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    if (__float_as_uint(dv[c] * dv[c]) == wj[e]) ci = c;
+        const float di = dv[ci >= 0 ? ci : 0];
+        bool wok = ci >= 0 || deg == 0;
+        uint32_t cls[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            int k = -1;
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                if (__float_as_uint(dv[c] * di) == wj[e]) k = c;
+            if (cj[e] >= 0 && k < 0) wok = false;
+            cls[e] = k >= 0 ? static_cast<uint32_t>(k) : 0u;
+        }
         // pass 1: ext entries of the row
         int next = 0, nA = 0;
         bool haveN = false;
@@ -557,14 +620,10 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
         }
         pre -= next;
         __syncthreads();
-        bool far = !small || nA > kWA || pre + next > C::KX;
+        bool far = !small || nA > kWA || pre + next > C::KX || !wok;
         uint32_t code[8];
-        uint32_t wb[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            code[q] = zcode;
-            wb[q] = 0u;
-        }
+        for (int q = 0; q < 8; ++q) code[q] = zcode;
         if (lr < nloc && deg > 0 && small) {
             int k = pre, a = 0;
             bool usedN = false;
@@ -572,7 +631,6 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
             for (int e = 0; e < 8; ++e) {
                 if (cj[e] < 0) continue;
                 const int64_t c = cj[e];
-                const uint32_t w = wj[e];
                 int64_t off;
                 uint32_t cd;
                 int slot;
@@ -598,10 +656,7 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
                 }
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
-                    if (q == slot) {
-                        code[q] = cd;
-                        wb[q] = w;
-                    }
+                    if (q == slot) code[q] = cd | cls[e];
             }
         }
         // summary of the row's wave (RPW rows): max phase-A count | any CSR-path row
@@ -612,15 +667,18 @@ __global__ __launch_bounds__(64) void win_plan_kernel(const int32_t* __restrict_
             af |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(af), d, C::RPW));
         }
         if ((lr % C::RPW) == 0) xl[(lr / C::RPW) * C::XLW + C::EPW] = md | (af << 8);
+        // the row's class: nibble lr % 8 of list word EPW + 1 + (lr % RPW) / 8
+        if (lr < nloc && ci > 0)
+            atomicOr(&xl[(lr / C::RPW) * C::XLW + C::EPW + 1 + (lr % C::RPW) / 8],
+                     static_cast<uint32_t>(ci) << (4 * (lr & 7)));
         __syncthreads();
-        unsigned char* const base = tabs + t * C::TAB_BYTES;
-        uint4* dst = reinterpret_cast<uint4*>(base + lr * kWRec);
-        dst[0] = make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
-                            code[4] | (code[5] << 16), code[6] | (code[7] << 16));
-        dst[1] = make_uint4(wb[0], wb[1], wb[2], wb[3]);
-        dst[2] = make_uint4(wb[4], wb[5], wb[6], wb[7]);
+        // per wave: its rows' codes, then its list (one contiguous DMA)
+        unsigned char* const base = tabs + t * C::TAB_G;
+        *reinterpret_cast<uint4*>(base + (lr / C::RPW) * C::RECG + (lr % C::RPW) * kWRec) =
+            make_uint4(code[0] | (code[1] << 16), code[2] | (code[3] << 16),
+                       code[4] | (code[5] << 16), code[6] | (code[7] << 16));
         for (int i = lr; i < C::NW * C::XLW; i += 64)
-            reinterpret_cast<uint32_t*>(base + C::BM * kWRec)[i] = xl[i];
+            *reinterpret_cast<uint32_t*>(base + (i / C::XLW) * C::RECG + C::OFF_RL + 4 * (i % C::XLW)) = xl[i];
         if (stats != nullptr) {
             if (far && lr < nloc) atomicAdd(&stats[1], 1ull);
             const int kt = __shfl(pre + next, 63, 64);
@@ -703,15 +761,18 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         const int pos = lane % C::LPR;
         xoff[pp] = static_cast<uint32_t>(lr) * ldxb + 16u * static_cast<uint32_t>(pos ^ (lr & 7));
     }
-    const uint32_t toff = lane < C::RLANES
-                              ? static_cast<uint32_t>(wave * C::RPW * kWRec + 16 * lane)
-                              : static_cast<uint32_t>(C::BM * kWRec + wave * (C::XLW * 4) + 16 * (lane - C::RLANES));
+    const uint32_t toff = static_cast<uint32_t>(wave * C::RECG + 16 * lane);
     // records of tile t (or tile 0: a dummy of the same op count) -> TAB slot q
     auto dma_tab = [&](int64_t t, int q) {
         if (lane < C::TLANES)
-            wdma_s(tabs + (t >= 0 ? t : 0) * C::TAB_BYTES, toff,
+            wdma_s(tabs + (t >= 0 ? t : 0) * C::TAB_G, toff,
                    wlds(lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW));
     };
+    // the weights of the wave's records in TAB slot q (landed: this wave's
+    // own DMA, waited by vmcnt; wave-local, LDS in order -- no barrier):
+    // lane (row, slot) writes dv[c_j] dv[c_i] and clears the code's class bits
+    float* const DV = reinterpret_cast<float*>(lds + C::OFF_DV);
+    auto rexp = [&](int q) { win_rexp<C>(lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW, DV, lane); };
     // own rows of tile t (dummy: tile 0) -> X slot q, piece pp
     auto dma_own = [&](int64_t t, int q, int pp) {
         const int64_t tt = t >= 0 ? t : 0;
@@ -734,7 +795,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     };
     // ext rows of the step whose records sit in TAB slot q (dummy: the zero row)
     auto ext_src = [&](int q, int i, bool real) -> const unsigned char* {
-        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::RPW * kWRec;
+        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::OFF_RL;
         int l = lane;
         asm volatile("" : "+v"(l));
         const int kk = i * C::RPP + l / C::LPR;
@@ -768,7 +829,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                 row = rb + tt * C::BM + C::RPW * wave + (l >> 1);
                 if (row >= re) row = re - 1;
             } else {
-                const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::RPW * kWRec;
+                const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::OFF_RL;
                 row = *reinterpret_cast<const uint32_t*>(tab + 4 * ((l - 16) >> 1));
             }
             wdma(x + row * ldx + 4 * (l & 1), wlds(lds + C::OFF_CODE + wave * C::CODE_W));
@@ -828,6 +889,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
 
     // ------------------------------------------------------------ prologue
     for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
+    if (tid < 8) DV[tid] = hdr->dv[tid];
     if constexpr (X0)
         for (int i = tid; i < H * 2; i += C::NT) {   // i = chunk * 8 + k
             const int c4 = i >> 3, k = i & 7;
@@ -883,6 +945,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         dma_tab(tile_of(1), 1);
         code_dma(tile_of(0), 0, false);
         wbar<wvm(0) & kWLgkm0>();                 // (all waves), zero row, EPI, COEF
+        rexp(0);
 #pragma unroll
         for (int rbk = 0; rbk < C::BM / 16; ++rbk) xblock_store(0, rbk, xblock_mfma(rbk));
         wbar<kWLgkm0>();                          // every wave's CODE reads before the refill
@@ -898,6 +961,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
 #pragma unroll
         for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(1), 1, pp);
         wbar<wvm(0) & kWLgkm0>();                 // (all waves), zero row, EPI
+        rexp(0);
         const unsigned char* es[C::NPE];
 #pragma unroll
         for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(0, i, true);
@@ -905,6 +969,16 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         for (int i = 0; i < C::NPE; ++i) ext_dma(i, es[i]);
     }
 
+    // layer 0's per-feature chain for 4 features from a row code (the codes
+    // form's CSR path, round-5 loop: the coefficient chunks in registers)
+    [[maybe_unused]] auto expand4r = [&](const f32x4 (&cf)[8], const float (&v)[7]) -> f32x4 {
+        f32x4 t = cf[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t[q] = fmaf(cf[k][q], v[k], t[q]);
+        return f32x4{relu_nan(t[0]), relu_nan(t[1]), relu_nan(t[2]), relu_nan(t[3])};
+    };
     // ---- phase A of a tile (its records in TAB slot tq, its rows in X): the
     // in-window / ext entries from LDS in CSR order, the +z entry held back
     // for phase B (ncn, nwn), or the CSR path for a wave with a row outside
@@ -926,7 +1000,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         // of the MFMA groups in the branches cost ~100 spilled VGPRs)
         const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
         const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-            *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
+            *reinterpret_cast<const int*>(RW + C::OFF_RL + 4 * C::EPW)));
         const bool far = live && ((summ >> 8) & 1u) != 0u;
         const int maxa = (live && !far) ? static_cast<int>(summ & 0xffu) : 0;
         {
@@ -943,7 +1017,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                     return (u & 1) ? (d >> 16) : (d & 0xffffu);
                 };
                 auto wld = [&](int qd, int u) -> float {
-                    return *reinterpret_cast<const float*>(RW + (4 * qd + gq) * kWRec + 16 + 4 * u);
+                    return *reinterpret_cast<const float*>(RW + C::OFF_RW + (4 * qd + gq) * 32 + 4 * u);
                 };
                 float wv[C::NQ][2];
                 // slots in batches of 2: loads of a batch, mid(G), then its FMAs
@@ -1009,7 +1083,8 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     // phase_a returned true): every entry of the wave's rows in CSR order,
     // the current tile from LDS, everything else from x (L2); the full sum
     // (no phase B).  Run by the caller where the fewest registers are live
-    // (the pipelined step: after tile s - 2's stores)
+    // (the pipelined step: after tile s - 2's stores).  The codes form keeps
+    // its own CSR path in its loop.
     auto phase_a_far = [&](int64_t t0, int64_t nloc, const unsigned char* X, f32x4 (&accn)[C::NQ][C::CH]) {
         // CSR path: every entry of the wave's rows in CSR order, the
         // current tile from LDS, everything else from x (L2); the full
@@ -1028,52 +1103,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         const bool v = e + k < ee;
                         cj[k] = v ? col[e + k] : -1;
                         wj[k] = v ? ew[e + k] : 0.f;
-                    }
-                    if constexpr (X0) {
-                        // codes form: one entry at a time (registers), rows
-                        // outside the tile expanded from their codes
-#pragma unroll 1
-                        for (int k = 0; k < 4; ++k) {
-                            if (cj[k] < 0) continue;
-                            f32x4 vk[C::CH];
-                            const int64_t off = static_cast<int64_t>(cj[k]) - t0;
-                            if (off >= 0 && off < nloc) {
-                                const uint32_t o = static_cast<uint32_t>(off);
-                                const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
-#pragma unroll
-                                for (int j = 0; j < C::CH; ++j)
-                                    vk[j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
-                            } else {
-                                const float* cp = x + static_cast<int64_t>(cj[k]) * ldx;
-                                const float4 v0 = ld4(cp), v1 = ld4(cp + 4);
-                                const float v[7] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z};
-#pragma unroll 1
-                                for (int j = 0; j < C::CH; ++j) {
-                                    // layer 0's chain (expand4's order), one
-                                    // coefficient chunk live at a time: the
-                                    // table offset opaque and the steps pinned
-                                    // (hoisted, the 8 chunks are 32 VGPRs the
-                                    // pipelined step does not have)
-                                    uint32_t co = static_cast<uint32_t>(C::OFF_COEF + (c0 + 16 * j) * 8 * 16);
-                                    asm volatile("" : "+v"(co));
-                                    f32x4 t = *reinterpret_cast<const f32x4*>(lds + co + 7 * 16);
-#pragma unroll
-                                    for (int k = 0; k < 7; ++k) {
-                                        __builtin_amdgcn_sched_barrier(0);
-                                        const f32x4 cfk = *reinterpret_cast<const f32x4*>(lds + co + k * 16);
-#pragma unroll
-                                        for (int q = 0; q < 4; ++q) t[q] = fmaf(cfk[q], v[k], t[q]);
-                                    }
-                                    __builtin_amdgcn_sched_barrier(0);
-                                    vk[j] = f32x4{relu_nan(t[0]), relu_nan(t[1]), relu_nan(t[2]), relu_nan(t[3])};
-                                }
-                            }
-#pragma unroll
-                            for (int j = 0; j < C::CH; ++j)
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vk[j][r], accn[qd][j][r]);
-                        }
-                        continue;
                     }
                     f32x4 vv[4][C::CH];
 #pragma unroll
@@ -1107,8 +1136,377 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     };
         auto no_mid = [](auto) {};
 
-    if constexpr (!AGG) {
-        // ---- the pipelined step (every full-layer mode).  Step s runs phase
+    if constexpr (X0) {
+    // ---- the codes form keeps the round-5 step: the row expansion (12 f32
+    // MFMAs and 6 row-block stores per wave) interleaved with the transform's
+    // MFMAs after B2 -- in the pipelined step it lands on the post-B1 tail
+    // (2.98 vs 2.78 ms per launch in the bench)
+    // phase-B carry: tile s-1's partial sums and +z entries
+    f32x4 accp[C::NQ][C::CH];
+    uint32_t ncode[C::NQ];
+    float nwt[C::NQ];
+#pragma unroll
+    for (int qd = 0; qd < C::NQ; ++qd) {
+        ncode[qd] = C::OFF_ZERO >> C::CSH;
+        nwt[qd] = 0.f;
+#pragma unroll
+        for (int j = 0; j < C::CH; ++j) accp[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    // schedule: cur / nx1 = tiles of steps s / s + 1, the cursor at s + 2
+    int64_t prv = -1, cur = tile_of(0), nx1 = tile_of(1);
+    WinCursor c2{0, 0, 0};
+    c2.next(S.L);
+    c2.next(S.L);
+    int xs = 0;                                   // X slot of step s (s % 3)
+    for (int s = 0;; ++s) {
+        if (cur < 0 && prv < 0) break;            // (uniform)
+        const int64_t nx2 = win_tile_c(S, p, c2);
+        const int rr = rr0, gg = gg0;
+        const int iql = iq;
+        // (the REXP row recomputed from an opaque lane: hoisted out of the
+        // step loop it is a register too many at H = 64)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int xp = xs == 0 ? 2 : xs - 1;      // slot of tile s - 1
+        const int xn2 = xp;                       // slot of tile s + 2 (= (s-1) % 3)
+        const int tq = static_cast<int>(s & 1);   // TAB slot of step s
+        const int64_t t0 = rb + (cur >= 0 ? cur : 0) * C::BM;
+        const int64_t nloc = cur >= 0 ? (re - t0 < C::BM ? re - t0 : C::BM) : 0;
+        const int64_t tp0 = rb + (prv >= 0 ? prv : 0) * C::BM;
+        const int64_t nlocp = prv >= 0 ? (re - tp0 < C::BM ? re - tp0 : C::BM) : 0;
+        const unsigned char* const X = lds + C::OFF_X + xs * C::X_BYTES;
+        const unsigned char* const XP = lds + C::OFF_X + xp * C::X_BYTES;
+        // (B0) every row of the step was expanded by a ds_write of the last
+        //      step; the records of step s + 1 landed (the ext list of the
+        //      codes DMA'd below); younger only the last step's stores
+        wtr.flush(wave, s - 1);
+        wtr.stamp(0);
+        if (s < 2) wbar<wvm(0) & kWLgkm0>();
+        else wbar<wvm(C::NST) & kWLgkm0>();
+        // this step's codes: own rows of tile s + 2, ext rows of step s + 1
+        // (landing under phase A; expanded between the transform's MFMAs)
+        code_dma(nx2, tq ^ 1, true);
+
+        wtr.stamp(1);
+        // ---- (P1) phase A of tile s
+        f32x4 accn[C::NQ][C::CH];
+        uint32_t ncn[C::NQ];
+        float nwn[C::NQ];
+#pragma unroll
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            ncn[qd] = C::OFF_ZERO >> C::CSH;
+            nwn[qd] = 0.f;
+#pragma unroll
+            for (int j = 0; j < C::CH; ++j) accn[qd][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (cur >= 0) {
+            const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
+            const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+                *reinterpret_cast<const int*>(RW + C::OFF_RL + 4 * C::EPW)));
+            const int maxa = static_cast<int>(summ & 0xffu);
+            const bool far = ((summ >> 8) & 1u) != 0u;
+            if (!far) {
+                uint4 cds[C::NQ], w03[C::NQ], w47[C::NQ];
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    const unsigned char* wr = RW + C::OFF_RW + (4 * qd + gq) * 32;
+                    cds[qd] = *reinterpret_cast<const uint4*>(RW + (4 * qd + gq) * kWRec);
+                    w03[qd] = *reinterpret_cast<const uint4*>(wr);
+                    w47[qd] = *reinterpret_cast<const uint4*>(wr + 16);
+                }
+                auto codeof = [&](int qd, int u) -> uint32_t {
+                    const uint32_t d = u < 2 ? cds[qd].x : u < 4 ? cds[qd].y : u < 6 ? cds[qd].z : cds[qd].w;
+                    return (u & 1) ? (d >> 16) : (d & 0xffffu);
+                };
+                auto wof = [&](int qd, int u) -> float {
+                    const uint32_t d = u == 0 ? w03[qd].x : u == 1 ? w03[qd].y : u == 2 ? w03[qd].z
+                                     : u == 3 ? w03[qd].w : u == 4 ? w47[qd].x : u == 5 ? w47[qd].y
+                                     : u == 6 ? w47[qd].z : w47[qd].w;
+                    return __uint_as_float(d);
+                };
+                // slots in batches of 2: loads of a batch first
+                auto batch = [&](auto U0, auto NB) {
+                    constexpr int u0 = decltype(U0)::value, nb = decltype(NB)::value;
+                    f32x4 vv[C::NQ][nb][C::CH];
+#pragma unroll
+                    for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                        for (int uu = 0; uu < nb; ++uu) {
+                            const uint32_t a = decode(codeof(qd, u0 + uu));
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+                                vv[qd][uu][j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+                        }
+#pragma unroll
+                    for (int qd = 0; qd < C::NQ; ++qd)
+#pragma unroll
+                        for (int uu = 0; uu < nb; ++uu) {
+                            const float w = wof(qd, u0 + uu);
+#pragma unroll
+                            for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(w, vv[qd][uu][j][r], accn[qd][j][r]);
+                        }
+                };
+                // (batches of 2: the 128-VGPR budget of 4 waves per SIMD)
+                if (maxa > 0) batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+                if (maxa > 2) batch(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
+                if (maxa > 4) batch(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
+                if (maxa > 6) batch(std::integral_constant<int, 6>{}, std::integral_constant<int, 1>{});
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    ncn[qd] = codeof(qd, 7);
+                    nwn[qd] = wof(qd, 7);
+                }
+            } else {
+                // CSR path: every entry of the wave's rows in CSR order, the
+                // current tile from LDS, everything else from x (L2); the full
+                // sum (no phase B)
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    const int lrow = C::RPW * wave + 4 * qd + gq;
+                    if (lrow < nloc) {
+                        const int64_t row = t0 + lrow;
+                        const int eb = row_ptr[row], ee = row_ptr[row + 1];
+                        for (int e = eb; e < ee; e += 4) {
+                            int cj[4];
+                            float wj[4];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const bool v = e + k < ee;
+                                cj[k] = v ? col[e + k] : -1;
+                                wj[k] = v ? ew[e + k] : 0.f;
+                            }
+                            {
+                                // codes form: one entry at a time (registers), rows
+                                // outside the tile expanded from their codes
+#pragma unroll 1
+                                for (int k = 0; k < 4; ++k) {
+                                    if (cj[k] < 0) continue;
+                                    f32x4 vk[C::CH];
+                                    const int64_t off = static_cast<int64_t>(cj[k]) - t0;
+                                    if (off >= 0 && off < nloc) {
+                                        const uint32_t o = static_cast<uint32_t>(off);
+                                        const uint32_t a = (static_cast<uint32_t>(X - lds) + o * C::ROWB + ((o & 7u) << 4)) ^ coff0;
+#pragma unroll
+                                        for (int j = 0; j < C::CH; ++j)
+                                            vk[j] = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+                                    } else {
+                                        const float* cp = x + static_cast<int64_t>(cj[k]) * ldx;
+                                        const float4 v0 = ld4(cp), v1 = ld4(cp + 4);
+                                        const float v[7] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z};
+#pragma unroll 1
+                                        for (int j = 0; j < C::CH; ++j) {
+                                            f32x4 cf[8];
+#pragma unroll
+                                            for (int q = 0; q < 8; ++q)
+                                                cf[q] = *reinterpret_cast<const f32x4*>(
+                                                    lds + C::OFF_COEF + ((c0 + 16 * j) * 8 + q) * 16);
+                                            vk[j] = expand4r(cf, v);
+                                        }
+                                    }
+#pragma unroll
+                                    for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                                        for (int r = 0; r < 4; ++r) accn[qd][j][r] = fmaf(wj[k], vk[j][r], accn[qd][j][r]);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+
+        wtr.stamp(2);
+        // ---- (P1) phase B of tile s - 1, its split and residual seeds
+        f32x4 seed[IBW][CPW];
+        if (prv >= 0) {
+#pragma unroll
+            for (int qd = 0; qd < C::NQ; ++qd) {
+                const uint32_t a = decode(ncode[qd]);
+#pragma unroll
+                for (int j = 0; j < C::CH; ++j) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(lds + a + 256 * j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) accp[qd][j][r] = fmaf(nwt[qd], v[r], accp[qd][j][r]);
+                }
+            }
+            {
+#pragma unroll
+                for (int qd = 0; qd < C::NQ; ++qd) {
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) m = max(m, __float_as_uint(fabsf(accp[qd][j][r])));
+                    m = wrow_max(m);
+                    const int pe = wsplit_exp(m);
+                    const float sc = __uint_as_float(static_cast<uint32_t>(pe + 127) << 23);
+                    const int lrow = C::RPW * wave + 4 * qd + gq;
+                    const int sw = asw<H>(lrow);
+#pragma unroll
+                    for (int j = 0; j < C::CH; ++j) {
+                        f16x4w hv, lv;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float sv = accp[qd][j][r] * sc;
+                            const _Float16 hh = static_cast<_Float16>(sv);
+                            hv[r] = hh;
+                            lv[r] = static_cast<_Float16>(sv - static_cast<float>(hh));
+                        }
+                        const int cc = c0 + 16 * j;             // the lane's 16-B fp32 chunk
+                        const int ao = lrow * H + 8 * ((cc >> 1) ^ sw) + 4 * (cc & 1);
+                        *reinterpret_cast<f16x4w*>(&AH[ao]) = hv;
+                        *reinterpret_cast<f16x4w*>(&AL[ao]) = lv;
+                    }
+                    if (iql == 0) {
+                        // (the row index recomputed from an opaque lane: hoisted
+                        // out of the step loop it is a register too many at H = 64)
+                        REXP[C::RPW * wave + 4 * qd + (ln >> 4)] = pe;
+                    }
+                }
+                // residual + bias of my output blocks (tile s-1's rows of my
+                // row group, my columns), before slot (s-1) % 3 is refilled
+#pragma unroll
+                for (int cp = 0; cp < CPW; ++cp) {
+                    const f32x4 bo = *reinterpret_cast<const f32x4*>(&EPI[n0 + 16 * cp + 4 * gg]);
+#pragma unroll
+                    for (int ib = 0; ib < IBW; ++ib) {
+                        const int lr = (wm * IBW + ib) * 16 + rr;
+                        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (has_res) {
+                            const int ch = ((n0 + 16 * cp) >> 2) + gg;
+                            rv = *reinterpret_cast<const float4*>(XP + lr * C::ROWB + ((ch ^ (lr & 7)) << 4));
+                        }
+                        seed[ib][cp] = f32x4{rv.x + bo[0], rv.y + bo[1], rv.z + bo[2], rv.w + bo[3]};
+                    }
+                }
+            }
+        }
+        // (B2) A image complete; every read of slot (s-1) % 3, the ext area
+        // and this step's records done
+        wtr.stamp(3);
+        wbar<wvm(0) & kWLgkm0>();                 // (+ every wave's codes)
+        wtr.stamp(4);
+        // the DMA of this step: the records of step s + 2 (into this step's
+        // TAB slot; the rows' codes went at B0)
+        const int64_t tn2 = nx2;
+        auto dma_piece = [&](int) { dma_tab(tn2, tq); };
+        constexpr int NPC = 1;
+
+        if (prv >= 0) {
+            {
+                // (3) transform: my output column blocks x my row blocks
+                int pr[IBW];
+                f32x4 accm[IBW][CPW];
+#pragma unroll
+                for (int ib = 0; ib < IBW; ++ib) {
+                    pr[ib] = REXP[(wm * IBW + ib) * 16 + rr];
+#pragma unroll
+                    for (int cp = 0; cp < CPW; ++cp)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) accm[ib][cp][r] = ldexpf(seed[ib][cp][r], pr[ib] + qw[cp]);
+                }
+                {
+                    const int sw = asw<H>(rr);
+                    auto frag = [&](int t, f16x8w& bh, f16x8w& bl) {
+                        const int kc = t / IBW, ib = t % IBW;
+                        const int R = (wm * IBW + ib) * 16 + rr;
+                        const int ao = R * H + 8 * ((4 * kc + gg) ^ sw);
+                        bh = *reinterpret_cast<const f16x8w*>(&AH[ao]);
+                        bl = *reinterpret_cast<const f16x8w*>(&AL[ao]);
+                    };
+                    __builtin_amdgcn_sched_barrier(0);
+                    constexpr int PD = 5, NF = PD + 1, NTT = C::KC * IBW;
+                    f16x8w fh[NF], fl[NF];
+#pragma unroll
+                    for (int t = 0; t < PD && t < NTT; ++t) frag(t, fh[t], fl[t]);
+                    // codes form: the expansion rows between the MFMAs, one
+                    // every XS t-steps from t = XT (the codes DMA'd at B0)
+                    constexpr int XT = 2, XS = 2;
+                    f32x4 xd[2];
+#pragma unroll
+                    for (int t = 0; t < NTT; ++t) {
+                        const int kc = t / IBW, ib = t % IBW;
+                        if (t < NPC) dma_piece(t);
+                        {
+                            // block i's MFMAs, block i - 1's store (its result landed)
+                            static_assert(XT + XS * (NXB - 1) < NTT, "expansion inside the transform");
+                            const int i = (t - XT) / XS;
+                            if (t >= XT && (t - XT) % XS == 0 && i < NXB) {
+                                xd[i & 1] = xblock_mfma(i);
+                                if (i > 0) xblock_store(xn2, i - 1, xd[(i - 1) & 1]);
+                            }
+                        }
+                        if (MODE & 4) continue;
+                        if (t + PD < NTT) frag(t + PD, fh[(t + PD) % NF], fl[(t + PD) % NF]);
+#pragma unroll
+                        for (int cp = 0; cp < CPW; ++cp) {
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[cp][kc], fl[t % NF], accm[ib][cp], 0, 0, 0);
+                            accm[ib][cp] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[cp][kc], fh[t % NF], accm[ib][cp], 0, 0, 0);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int t = NTT; t < NPC; ++t) dma_piece(t);
+                    xblock_store(xn2, NXB - 1, xd[(NXB - 1) & 1]);
+                }
+                wtr.stamp(5);
+                {
+                    // epilogue stored straight from the accumulators: lane (rr, gg) of
+                    // block (ib, cp) holds row 16 ib + rr, columns n0 + 16 cp + 4 gg .. +3
+                    static_assert(IBW * CPW == C::NST, "one store per block keeps the per-step store count");
+#pragma unroll
+                    for (int cp = 0; cp < CPW; ++cp) {
+                        const int nc = n0 + 16 * cp + 4 * gg;
+                        const f32x4 so = *reinterpret_cast<const f32x4*>(&EPI[H + nc]);
+                        const f32x4 ho = *reinterpret_cast<const f32x4*>(&EPI[2 * H + nc]);
+#pragma unroll
+                        for (int ib = 0; ib < IBW; ++ib) {
+                            f32x4 o;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                float v = ldexpf(accm[ib][cp][r], -(pr[ib] + qw[cp]));
+                                if (flags & MIGNN_EPI_AFFINE) v = v * so[r] + ho[r];
+                                if (flags & MIGNN_EPI_RELU) v = relu_nan(v);
+                                o[r] = v;
+                            }
+                            const int lr = (wm * IBW + ib) * 16 + rr;
+                            if (lr < nlocp)
+                                __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + nc));
+                        }
+                    }
+                }
+                wtr.stamp(7);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NPC; ++q) dma_piece(q);
+            if constexpr (X0) {
+#pragma unroll
+                for (int rbk = 0; rbk < NXB; ++rbk) xblock_store(xn2, rbk, xblock_mfma(rbk));
+            }
+        }
+        rexp(tq ^ 1);                             // tile s + 1's weights (records landed at B0)
+        // carry tile s into phase B
+#pragma unroll
+        for (int qd = 0; qd < C::NQ; ++qd) {
+            ncode[qd] = ncn[qd];
+            nwt[qd] = nwn[qd];
+#pragma unroll
+            for (int j = 0; j < C::CH; ++j) accp[qd][j] = accn[qd][j];
+        }
+        xs = xs == 2 ? 0 : xs + 1;
+        prv = cur;
+        cur = nx1;
+        nx1 = nx2;
+        c2.next(S.L);
+    }
+        wwait<wvm(0)>();   // no LDS-DMA may outlive the workgroup
+    } else if constexpr (!AGG) {
+        // ---- the pipelined step (every full-layer mode but the codes form).  Step s runs phase
         // A of tile s with the transform of tile s - 2 (its 48 MFMAs in four
         // groups between phase A's slot batches: the matrix pipe works under
         // the aggregation's LDS reads and FMAs instead of in a phase of its
@@ -1123,7 +1521,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         //       -> DMA ext rows of step s + 1, records of step s + 2, own rows
         //       of tile s + 2 into slot (s-1) % 3
         //   phase B(s - 1) (its +z term from tile s), split -> A image, REXP
-        //   (codes form: tile s + 2's and step s + 1's rows expanded here)
         f32x4 accp[C::NQ][C::CH];
         uint32_t ncode[C::NQ];
         float nwt[C::NQ];
@@ -1148,7 +1545,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
         c2.next(S.L);
         int xs = 0;                               // X slot of step s (s % 3)
         const int rr = rr0, gg = gg0;
-        constexpr int PD = X0 ? kWinPDX : kWinPD, NF = PD + 1, NTT = C::KC * IBW, TG = NTT / 4;
+        constexpr int PD = kWinPD, NF = PD + 1, NTT = C::KC * IBW, TG = NTT / 4;
         static_assert(NTT % 4 == 0 && PD < NTT, "four MFMA groups");
         for (int s = 0;; ++s) {
             if (cur < 0 && prv < 0 && prv2 < 0) break;   // (uniform)
@@ -1167,12 +1564,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             wtr.flush(wave, s - 1);
             wtr.stamp(0);
             // (B0)
-            if constexpr (X0) {
-                // (codes form: the records of step s + 1 landed -- the ext list of
-                // the codes DMA'd below; nothing younger)
-                wbar<wvm(0) & kWLgkm0>();
-                code_dma(nx2, tq ^ 1, true);
-            } else if (s == 0) wbar<wvm(0) & kWLgkm0>();
+            if (s == 0) wbar<wvm(0) & kWLgkm0>();
             else wbar<wvm(1 + C::NPX) & kWLgkm0>();
             wtr.stamp(1);
 
@@ -1283,33 +1675,29 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
             }
             // (B1)
             wtr.stamp(3);
-            if constexpr (X0) wbar<wvm(0) & kWLgkm0>();   // (+ every wave's codes)
-            else wbar<kWLgkm0>();
+            wbar<kWLgkm0>();
             const int64_t tn1 = nx1, tn2 = nx2;
             // DMA pieces of this step: ext rows of step s + 1, the records of
-            // step s + 2, the own rows of tile s + 2 (codes form: the records
-            // only), issued between phase B's and the split's VALU work
+            // step s + 2, the own rows of tile s + 2, issued between phase B's
+            // and the split's VALU work
             // (as a burst after B1 they stall the vector memory pipe: 3.26
             // vs 2.86 ms)
+            // this wave's records of step s + 1 landed (its ext list);
+            // younger: the own rows of tile s + 1, the stores of tile s - 2
+            if (s == 0) wwait<wvm(0)>();
+            else if (s == 1) wwait<wvm(C::NPX)>();
+            else wwait<wvm(C::NPX + C::NST)>();
+            rexp(tq ^ 1);                         // tile s + 1's weights (same-box A/B:
+                                                  // here, at B0 on tile s, or at the step's
+                                                  // end within 0.3 %)
             const unsigned char* es[C::NPE];
-            if constexpr (!X0) {
-                // this wave's records of step s + 1 landed (its ext list);
-                // younger: the own rows of tile s + 1, the stores of tile s - 2
-                if (s == 0) wwait<wvm(0)>();
-                else if (s == 1) wwait<wvm(C::NPX)>();
-                else wwait<wvm(C::NPX + C::NST)>();
 #pragma unroll
-                for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
-            }
-            constexpr int NPC = X0 ? 1 : C::NPE + 1 + C::NPX;
+            for (int i = 0; i < C::NPE; ++i) es[i] = ext_src(tq ^ 1, i, tn1 >= 0);
+            constexpr int NPC = C::NPE + 1 + C::NPX;
             auto dpiece = [&](int q) {
-                if constexpr (X0) {
-                    dma_tab(tn2, tq);
-                } else {
-                    if (q < C::NPE) ext_dma(q, es[q]);
-                    else if (q == C::NPE) dma_tab(tn2, tq);
-                    else dma_own(tn2, xp, q - C::NPE - 1);
-                }
+                if (q < C::NPE) ext_dma(q, es[q]);
+                else if (q == C::NPE) dma_tab(tn2, tq);
+                else dma_own(tn2, xp, q - C::NPE - 1);
             };
             // pieces [q0, q1)
             auto dpieces = [&](int q0, int q1) {
@@ -1367,17 +1755,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                     if (iq == 0) REXP[C::RPW * wave + 4 * qd + (ln >> 4)] = pe;
                 }
                 dpieces(5, NPC);
-            }
-            if constexpr (X0) {
-                // codes form: tile s + 2's own rows (slot (s-1) % 3) and step s +
-                // 1's ext rows, block i's MFMAs before block i - 1's store
-                f32x4 xd[2];
-#pragma unroll
-                for (int i = 0; i < NXB; ++i) {
-                    xd[i & 1] = xblock_mfma(i);
-                    if (i > 0) xblock_store(xp, i - 1, xd[(i - 1) & 1]);
-                }
-                xblock_store(xp, NXB - 1, xd[(NXB - 1) & 1]);
             }
             wtr.stamp(5);
             // carry
@@ -1486,6 +1863,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                             __builtin_nontemporal_store(accp[qd][j], reinterpret_cast<f32x4*>(out + (tp0 + lrow) * ldo + 4 * (c0 + 16 * j)));
                     }
             }
+            rexp(tq ^ 1);                         // tile s + 1's weights (records waited after B2)
             // carry tile s into phase B
 #pragma unroll
             for (int qd = 0; qd < C::NQ; ++qd) {
@@ -1594,14 +1972,14 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         const int pos = lane % C::LPR;
         xoff[pp] = static_cast<uint32_t>(lr) * ldxb + 16u * static_cast<uint32_t>(pos ^ (lr & C::SWZ));
     }
-    const uint32_t toff = lane < C::RLANES
-                              ? static_cast<uint32_t>(wave * C::RPW * kWRec + 16 * lane)
-                              : static_cast<uint32_t>(C::BM * kWRec + wave * (C::XLW * 4) + 16 * (lane - C::RLANES));
+    const uint32_t toff = static_cast<uint32_t>(wave * C::RECG + 16 * lane);
     auto dma_tab = [&](int64_t t, int q) {
         if (lane < C::TLANES)
-            wdma_s(tabs + (t >= 0 ? t : 0) * C::TAB_BYTES, toff,
+            wdma_s(tabs + (t >= 0 ? t : 0) * C::TAB_G, toff,
                    wlds(lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW));
     };
+    float* const DV = reinterpret_cast<float*>(lds + C::OFF_DV);
+    auto rexp = [&](int q) { win_rexp<C>(lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW, DV, lane); };
     auto dma_own = [&](int64_t t, int q, int pp) {
         const int64_t tt = t >= 0 ? t : 0;
         const int64_t t0 = rb + tt * C::BM;
@@ -1622,7 +2000,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         }
     };
     auto ext_src = [&](int q, int i, bool real) -> const unsigned char* {
-        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::RPW * kWRec;
+        const unsigned char* const tab = lds + C::OFF_TAB + q * C::TAB_BYTES + wave * C::RECW + C::OFF_RL;
         int l = lane;
         asm volatile("" : "+v"(l));
         const int kk = i * C::RPP + l / C::LPR;
@@ -1639,6 +2017,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
 
     // ------------------------------------------------------------ prologue
     for (int i = tid; i < C::ROWB / 4; i += C::NT) reinterpret_cast<float*>(lds + C::OFF_ZERO)[i] = 0.f;
+    if (tid < 8) DV[tid] = hdr->dv[tid];
     // W split in registers: A fragment (cb, kc) of lane l = W[16 cb + (l & 15)]
     // [32 kc + 8 (l >> 4) .. +7], one exponent per 16-column block
     f16x8w wh[4][2], wl[4][2];
@@ -1685,6 +2064,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
 #pragma unroll
     for (int pp = 0; pp < C::NPX; ++pp) dma_own(tile_of(1), 1, pp);
     wbar<wvm(0) & kWLgkm0>();
+    rexp(0);
     {
         const unsigned char* es[C::NPE];
 #pragma unroll
@@ -1810,18 +2190,18 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
         for (int k = 0; k < 4; ++k) accn[k] = f32x4{0.f, 0.f, 0.f, 0.f};
         const unsigned char* const RW = lds + C::OFF_TAB + tq * C::TAB_BYTES + wave * C::RECW;
         const uint32_t summ = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-            *reinterpret_cast<const int*>(RW + C::RPW * kWRec + 4 * C::EPW)));
+            *reinterpret_cast<const int*>(RW + C::OFF_RL + 4 * C::EPW)));
         const bool live = cur >= 0;
         const bool far = live && ((summ >> 8) & 1u) != 0u;
         const int maxa = (live && !far) ? static_cast<int>(summ & 0xffu) : 0;
         {
-            const unsigned char* rec = RW + rw * kWRec;
-            const uint4 cds = *reinterpret_cast<const uint4*>(rec);
+            const uint4 cds = *reinterpret_cast<const uint4*>(RW + rw * kWRec);
             auto codeof = [&](int u) -> uint32_t {
                 const uint32_t d = u < 2 ? cds.x : u < 4 ? cds.y : u < 6 ? cds.z : cds.w;
                 return (u & 1) ? (d >> 16) : (d & 0xffffu);
             };
-            auto wld = [&](int u) -> float { return *reinterpret_cast<const float*>(rec + 16 + 4 * u); };
+            const unsigned char* const wr = RW + C::OFF_RW + rw * 32;
+            auto wld = [&](int u) -> float { return *reinterpret_cast<const float*>(wr + 4 * u); };
             f32x4 vv[2][4];
             float wv[2];
             auto bload = [&](auto U0, auto NB) {
@@ -1959,6 +2339,7 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
             for (int pp = 0; pp < C::NPX; ++pp) dma_own(tn2, xp, pp);
         }
         wtr.stamp(5);
+        rexp(tq ^ 1);                             // tile s + 1's weights (its records landed at B0)
 #pragma unroll
         for (int k = 0; k < 4; ++k) accp[k] = accn[k];
         ncode = ncn;
@@ -2047,7 +2428,7 @@ using namespace mignn;
 extern "C" size_t mignn_gcn_win_plan_bytes(int64_t row_begin, int64_t row_end, int h) {
     if (row_end <= row_begin || (h != 64 && h != 128)) return 0;
     const int64_t ntiles = (row_end - row_begin + 63) / 64;
-    return kWHdr + static_cast<size_t>(ntiles) * (h == 128 ? WCfg<128>::TAB_BYTES : WCfg<64>::TAB_BYTES);
+    return kWHdr + static_cast<size_t>(ntiles) * (h == 128 ? WCfg<128>::TAB_G : WCfg<64>::TAB_G);
 }
 
 extern "C" int mignn_gcn_win_plan(const int32_t* row_ptr, const int32_t* col, const float* ew,

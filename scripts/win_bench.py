@@ -110,27 +110,40 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
         Ywc = torch.empty_like(X)
 
         def win_codes(VL=LP, pl=wplan, Yo=Ywc):
+            # layers 0 + 1 as the model runs them: the codes written just
+            # before the codes form reads them (MALL-resident, as in the
+            # forward -- codes left in HBM by other kernels time differently)
+            _lib.check(VL.mignn_gcn_layer0_codes(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(pos_c),
+                                                 3, 3, 0, n, P(codes), 8, st), "codes")
             _lib.check(VL.mignn_gcn_layer_win_codes(P(pl), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
                                                     P(codes), 8, 0, n, H, P(xcoef), P(W), P(b), P(sc),
                                                     P(sh), 15, P(Yo), H, st), "win_codes")
-        cases["win_codes"] = win_codes
+        cases["win_layers01_codes"] = win_codes
     vout, vchecks = {}, {}
     for vname, VL in VARIANTS.items():
         # each variant builds its own plan (plan formats may differ)
         vnb = VL.mignn_gcn_win_plan_bytes(0, n, H)
         vplan = torch.empty(vnb, dtype=torch.uint8, device=dev)
+        vst = torch.zeros(4, dtype=torch.int64, device=dev)
         _lib.check(VL.mignn_gcn_win_plan(P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), 0, n, H, P(info),
-                                         P(vplan), vnb, None, st), "vplan")
-        Yv = torch.empty_like(X)
-        vout[vname] = Yv
+                                         P(vplan), vnb, P(vst), st), "vplan")
+        torch.cuda.synchronize()
+        res.setdefault("variant_plan", {}).setdefault(H, {})[vname] = {"bytes": vnb, "stats": vst.tolist()}
+        Yv, Yva = torch.empty_like(X), torch.empty_like(X)
+        Yvc = torch.empty_like(X) if codes is not None else None
+        vout[vname] = (Yv, Yva, Yvc)
 
         def fv(VL=VL, vplan=vplan, Yv=Yw):
             # (timed into the product's output buffer: same pages for every variant)
             _lib.check(VL.mignn_gcn_layer_win(P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
                                               H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yv), H, st), "wv")
-        vcheck = (lambda VL=VL, vplan=vplan, Yv=Yv: _lib.check(VL.mignn_gcn_layer_win(
-            P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X), H, 0, n, H, P(W), P(b), P(sc),
-            P(sh), 15, P(Yv), H, st), "wv"))
+        def vcheck(VL=VL, vplan=vplan, Yv=Yv, Yva=Yva, Yvc=Yvc):
+            _lib.check(VL.mignn_gcn_layer_win(P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
+                                              H, 0, n, H, P(W), P(b), P(sc), P(sh), 15, P(Yv), H, st), "wv")
+            _lib.check(VL.mignn_gcn_aggregate_win(P(vplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew),
+                                                  P(X), H, 0, n, H, P(Yva), H, st), "wva")
+            if Yvc is not None:
+                win_codes(VL, vplan, Yvc)
         vchecks[vname] = vcheck
 
         def fva(VL=VL, vplan=vplan):
@@ -139,7 +152,7 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
         cases[f"win@{vname}"] = fv
         cases[f"win_aggregate@{vname}"] = fva
         if codes is not None:
-            cases[f"win_codes@{vname}"] = (lambda VL=VL, vplan=vplan: win_codes(VL, vplan, Ywc))
+            cases[f"win_layers01_codes@{vname}"] = (lambda VL=VL, vplan=vplan: win_codes(VL, vplan, Ywc))
     for m in [int(v) for v in os.environ.get("WB_MODES", "").split(",") if v]:
         def fw(m=m):
             _lib.check(L.mignn_diag_win(m, P(wplan), P(csr_c.row_ptr), P(csr_c.col), P(csr_c.ew), P(X),
@@ -169,6 +182,8 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     # the block-order CSR by the pc kernel (rows matched through the orders)
     win()
     win_agg()
+    if codes is not None:
+        win_codes()
     torch.cuda.synchronize()
     out = {"win_deterministic": None}
     Yw2 = Yw.clone()
@@ -179,8 +194,12 @@ for H in [int(v) for v in os.environ.get("WB_H", "128,64").split(",")]:
     for vname in vout:
         vchecks[vname]()
         torch.cuda.synchronize()
-        out[f"win_vs_{vname}_max_diff"] = (Yw - vout[vname]).abs().max().item()
-        out[f"win_vs_{vname}_bitwise"] = bool(torch.equal(Yw, vout[vname]))
+        Yv, Yva, Yvc = vout[vname]
+        out[f"win_vs_{vname}_max_diff"] = (Yw - Yv).abs().max().item()
+        out[f"win_vs_{vname}_bitwise"] = bool(torch.equal(Yw, Yv))
+        out[f"agg_vs_{vname}_bitwise"] = bool(torch.equal(Ywa, Yva))
+        if Yvc is not None:
+            out[f"codes_vs_{vname}_bitwise"] = bool(torch.equal(Ywc, Yvc))
     if old:
         pc()
         torch.cuda.synchronize()

@@ -366,3 +366,56 @@ def test_model_gcn_codes_bitwise():
         csr = next(iter(m._csr.entries.values()))
         assert m._use_gcn_codes(csr) == codes
     assert torch.equal(ys[True], ys[False])
+
+
+@pytest.mark.parametrize("H", [64, 128])
+def test_win_plan_weight_classes(H):
+    """The 16-B plan record carries degree classes, not weights: the kernel
+    rebuilds w_ij = dv[c_j] dv[c_i] and the plan admits a row only if that
+    equals its ew bitwise.  A one-ulp change of one entry's weight moves
+    exactly that row to the CSR path (stats[1] + 1) and the layer still
+    follows ew; a graph with arbitrary weights runs every row through the CSR
+    path, correct against fp64."""
+    csr, n, info = _graph("cols", (64, 48, 40))
+    g, W, b, sc, sh = _weights(H, 31)
+    X = torch.randn(n, H, generator=g).to(DEV)
+    _, st0 = _plan(csr, 0, n, H, info)
+    base_far = st0.tolist()[1]
+    # a row of a wave that takes the planned path (its summary word's CSR-path
+    # bit clear; plan layout per tile: per wave its 16-B codes, then its list
+    # -- EPW ext columns, the summary, the row classes): bump its first weight
+    plan0, _ = _plan(csr, 0, n, H, info)
+    rpw, epw, recg = (16, 8, 304) if H == 64 else (8, 4, 160)
+    nw = 64 // rpw
+    tabs = plan0[256:].cpu().numpy()
+    ntiles = (n + 63) // 64
+    summ = np.frombuffer(tabs.tobytes(), dtype=np.uint32).reshape(ntiles, nw, recg // 4)[:, :, rpw * 4 + epw]
+    ok = np.argwhere((summ >> 8) & 1 == 0)
+    t, w = map(int, ok[len(ok) // 2])
+    row = 64 * t + rpw * w + 3
+    rp = csr.row_ptr.long()
+    e = int(rp[row])
+    ew2 = csr.ew.clone()
+    ew2[e] = torch.nextafter(ew2[e], torch.tensor(2.0, device=DEV))
+    csr2 = copy_with_ew(csr, ew2)
+    plan2, st2 = _plan(csr2, 0, n, H, info)
+    assert st2.tolist()[1] == base_far + 1, (base_far, st2.tolist())
+    out = torch.full((n, H), float("nan"), device=DEV)
+    _layer(csr2, plan2, X, H, 0, n, H, W, b, sc, sh, out)
+    _, ref = _ref(csr2, X, W, b, sc, sh)
+    assert (out.cpu().double() - ref).abs().max().item() < 1e-5
+    # arbitrary weights: every row with entries takes the CSR path
+    csr3 = copy_with_ew(csr, (torch.rand(csr.ew.shape[0], generator=g) + 0.1).to(DEV))
+    plan3, st3 = _plan(csr3, 0, n, H, info)
+    assert st3.tolist()[1] == n, st3.tolist()
+    out.fill_(float("nan"))
+    _layer(csr3, plan3, X, H, 0, n, H, W, b, sc, sh, out)
+    _, ref3 = _ref(csr3, X, W, b, sc, sh)
+    assert (out.cpu().double() - ref3).abs().max().item() < 1e-5 * max(1.0, ref3.abs().max().item())
+
+
+def copy_with_ew(csr, ew):
+    import copy
+    c = copy.copy(csr)
+    c.ew = ew
+    return c
