@@ -1314,12 +1314,17 @@ struct GatCfg {
     static constexpr int XC = H / 32;                  // x chunks
     static constexpr int NPB = 16;                     // column blocks per image chunk (padded)
     static constexpr int WCH = NCB * 2 * AFRAG;        // real bytes of one W chunk
-    static constexpr int STEPW = 4 * WCH;              // the 4 heads' chunks of one x chunk
     static constexpr int REST = AW * 16 * 4 * 8 * 4 + AW * 16 * 4 * 8 + 4 * H * 4 + H * 16;
-    // W buffers: 2 (next step's chunks in flight) unless that leaves no room
-    // for a second block on the CU (H = 128 with 4 waves: 1, refilled after
-    // the step's MFMAs; the other block covers the wait)
-    static constexpr int WB = (AW == 4 && 2 * STEPW + REST > 80 * 1024) ? 1 : 2;
+    // W steps: the 4 heads' chunks of one x chunk, double-buffered (the next
+    // step's chunks DMA'd under this step's MFMAs) -- or, where two such
+    // buffers leave no room for a second block on the CU (H = 128, 4 waves),
+    // 2 heads per step, two steps per x chunk (round 5 kept ONE 4-head buffer
+    // there, refilled after the chunk's MFMAs: every refill's latency exposed)
+    static constexpr int HPS = (AW == 4 && 2 * 4 * WCH + REST > 80 * 1024) ? 2 : 4;
+    static constexpr int NG = 4 / HPS;                  // W steps per x chunk
+    static constexpr int NSTEP = XC * NG;
+    static constexpr int STEPW = HPS * WCH;             // bytes of one W step
+    static constexpr int WB = 2;
     static constexpr int OFF_AL = WB * STEPW;          // alphas [AW][16][4][8]
     static constexpr int OFF_ST = OFF_AL + AW * 16 * 4 * 8 * 4;   // (max, sum) [AW][16][4]
     static constexpr int OFF_EPI = OFF_ST + AW * 16 * 4 * 8;       // QF | BF | SC | SH [H]
@@ -1369,14 +1374,16 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
     const bool rv = row < re;
     const int64_t rowc = rv ? row : re - 1;
 
-    // W chunks of x chunk t (heads 0..3: image chunks k XC + t) -> buffer t & 1
-    auto w_dma = [&](int t) {
-        if (t >= C::XC || (flags & MIGNN_SCHED_INTERLEAVED)) return;
-        unsigned char* dst = lds + (C::WB == 2 ? (t & 1) : 0) * C::STEPW;
+    // W step j (x chunk j / NG, heads (j % NG) HPS .. + HPS - 1: image chunks
+    // k XC + t) -> buffer j & 1
+    auto w_dma = [&](int j) {
+        if (j >= C::NSTEP || (flags & MIGNN_SCHED_INTERLEAVED)) return;
+        const int t = j / C::NG, k0 = (j % C::NG) * C::HPS;
+        unsigned char* dst = lds + (j & 1) * C::STEPW;
 #pragma unroll
         for (int pc = 0; pc < C::STEPW / 1024 / C::AW; ++pc) {
             const int piece = wave + pc * C::AW;              // 1-KB piece of the step
-            const int hd = piece / (C::WCH / 1024), q = piece % (C::WCH / 1024);
+            const int hd = k0 + piece / (C::WCH / 1024), q = piece % (C::WCH / 1024);
             const unsigned char* src = img + static_cast<size_t>(hd * C::XC + t) * C::NPB * 2 * AFRAG;
             glds16_ag(src + q * 1024 + lane * 16, lds_addr_ag(dst + piece * 1024));
         }
@@ -1546,8 +1553,8 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
 
 #pragma unroll 1
     for (int t = 0; t < C::XC; ++t) {
-        chunk_barrier();                           // W chunks of t and this chunk's rows landed
-        if constexpr (C::WB == 2) w_dma(t + 1);
+        chunk_barrier();                           // W step t NG and this chunk's rows landed
+        w_dma(t * C::NG + 1);
         // the 4 heads' weighted sums of this x chunk (CSR order)
         f32x4 a[HEADS][2];
 #pragma unroll
@@ -1601,9 +1608,17 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
         // buffers live at once spilled registers)
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < C::XC && !(flags & MIGNN_DIAG_NO_PRODUCE)) gather(t + 1);
-        const unsigned char* wb = wl0 + (C::WB == 2 ? (t & 1) : 0) * C::STEPW;
 #pragma unroll
         for (int k = 0; k < HEADS; ++k) {
+            const int j = t * C::NG + k / C::HPS;          // this head's W step
+            if (C::NG > 1 && k > 0 && k % C::HPS == 0) {
+                // W step j landed (younger: the next chunk's 2 AS row loads),
+                // every wave's reads of buffer (j + 1) & 1 done -> its refill
+                if (L0 || t + 1 >= C::XC || (flags & MIGNN_DIAG_NO_PRODUCE)) vm_barrier64<0>();
+                else vm_barrier64<2 * AS>();
+                w_dma(j + 1);
+            }
+            const unsigned char* wb = wl0 + (j & 1) * C::STEPW + (k % C::HPS) * C::WCH;
             uint32_t m = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -1634,7 +1649,7 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
 #pragma unroll
             for (int cb = 0; cb < C::NCB; ++cb) {
                 if (flags & MIGNN_DIAG_NO_MFMA) break;
-                const unsigned char* wf = wb + k * C::WCH + (2 * cb) * AFRAG;
+                const unsigned char* wf = wb + (2 * cb) * AFRAG;
                 const f16x8 wh = *reinterpret_cast<const f16x8*>(wf);
                 const f16x8 wl = *reinterpret_cast<const f16x8*>(wf + AFRAG);
                 acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, bh, acc[cb], 0, 0, 0);
@@ -1644,12 +1659,6 @@ gat_fused_kernel(const int32_t* __restrict__ row_ptr, const int32_t* __restrict_
             // (one head's fragments at a time: hoisting the next heads' LDS
             // reads above these MFMAs spilled registers)
             __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (C::WB == 1) {
-            if (t + 1 < C::XC) {
-                vm_barrier64<63>();                // every wave's W reads done (gathers may fly)
-                w_dma(t + 1);
-            }
         }
     }
     // epilogue (staged, whole-row stores): the W / alpha buffers are free once

@@ -69,6 +69,10 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 #ifndef MIGNN_WIN_PD
 #define MIGNN_WIN_PD 3
 #endif
+// (experiment) s_setprio(1) over the pipelined step's MFMA groups
+#ifndef MIGNN_WIN_PRIO
+#define MIGNN_WIN_PRIO 0
+#endif
 constexpr int kWinPD = MIGNN_WIN_PD;
 // Plan record of a row: 8 u16 codes (16 B), each with the neighbour's degree
 // class in its low 3 bits (the code's LDS offset is 16-B aligned: those bits
@@ -380,6 +384,13 @@ __device__ __forceinline__ void wbar() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
+
+// The H = 128 epilogue stores 64-B row pieces (each of 8 waves its 16
+// columns of 16 rows, at different times of a step): plain stores, so L2
+// merges a row's pieces into whole lines -- as nontemporal stores 1/3 of the
+// lines went to HBM in pieces (WRITE_SIZE 6.83 vs 5.12 GB per 10M-row launch,
+// 2.2 % of the layer's time; `profiles/r06_kpmc_st_*.json`)
+__device__ __forceinline__ void wstore(const f32x4& v, f32x4* p) { *p = v; }
 
 __device__ __forceinline__ uint32_t wlds(const unsigned char* p) {
     return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_w)(p)));
@@ -1475,7 +1486,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                             }
                             const int lr = (wm * IBW + ib) * 16 + rr;
                             if (lr < nlocp)
-                                __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + nc));
+                                wstore(o, reinterpret_cast<f32x4*>(out + (tp0 + lr) * ldo + nc));
                         }
                     }
                 }
@@ -1597,6 +1608,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                 constexpr int g = decltype(G)::value;
                 if (!mf) return;
                 __builtin_amdgcn_sched_barrier(0);
+                if constexpr (MIGNN_WIN_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int t = g * TG; t < (g + 1) * TG; ++t) {
                     const int kc = t / IBW, ib = t % IBW;
@@ -1610,6 +1622,7 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         }
                     }
                 }
+                if constexpr (MIGNN_WIN_PRIO == 1) __builtin_amdgcn_s_setprio(0);
                 __builtin_amdgcn_sched_barrier(0);
             };
 
@@ -1643,14 +1656,18 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                 // there change no wait that matters: the later steps' records
                 // and rows are dummies)
                 static_assert(IBW * CPW == C::NST, "one store per block keeps the per-step store count");
+                // (the lane's store offsets from an opaque lane: hoisted, its
+                // 64-bit row pointer is spilled and reloaded under a vmcnt(0))
+                int ls = lane;
+                asm volatile("" : "+v"(ls));
 #pragma unroll
                 for (int cp = 0; cp < CPW; ++cp) {
-                    const int nc = n0 + 16 * cp + 4 * gg;
+                    const int nc = n0 + 16 * cp + 4 * (ls >> 4);
 #pragma unroll
                     for (int ib = 0; ib < IBW; ++ib) {
-                        const int lr = (wm * IBW + ib) * 16 + rr;
+                        const int lr = (wm * IBW + ib) * 16 + (ls & 15);
                         if (lr < nloc2)
-                            __builtin_nontemporal_store(accm[ib][cp], reinterpret_cast<f32x4*>(out + (t20 + lr) * ldo + nc));
+                            wstore(accm[ib][cp], reinterpret_cast<f32x4*>(out + (t20 + lr) * ldo + nc));
                     }
                 }
             }

@@ -326,7 +326,11 @@ int mignn_gcn_aggregate_ring(const void* plan, const int32_t* row_ptr, const int
  * out-of-tile rows.  The plan (mignn_gcn_win_plan, size
  * mignn_gcn_win_plan_bytes; device memory, 16-B aligned) carries a header
  * with the launch grid and schedule, checked by the layer kernel
- * (MIGNN_DEVERR_PLAN on a mismatch), and a 48-B record per row.
+ * (MIGNN_DEVERR_PLAN on a mismatch), and a 16-B record per row: the
+ * neighbours' LDS codes with their degree classes -- the weights are rebuilt
+ * as dinv_j dinv_i (dinv = (deg + 1)^-1/2), so a row whose ew is not that
+ * gcn_norm product bitwise (a weighted graph, a neighbour of degree > 8) is
+ * planned onto the CSR path, which reads ew itself: any CSR stays correct.
  * order_info (nullable: the int32[4] info of mignn_locality_order_cols,
  * rows from row_begin = 0 in that order -- the whole graph, or a shard's
  * interior range with its boundary planes moved out) selects the column

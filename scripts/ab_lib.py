@@ -41,9 +41,15 @@ if mode == "gat":
     imgc = f16x3_image(WCAT)
     GSCR = torch.empty(max(_lib.lib().mignn_gat_layer_scratch_bytes(n, n, H, 4), 1),
                        dtype=torch.uint8, device=dev)
-libs = {"cur": _lib.lib(),
-        "prev": _lib._load(os.path.join(HERE, "gnn-bfs-rans_amd", "mignn", "libmignn_prev.so"),
-                           _lib.SIGNATURES)}
+# AB_LIBS (name=path,...): variant builds (scripts/build_variant.sh) timed
+# beside the in-tree library; default: libmignn_prev.so
+libs = {"cur": _lib.lib()}
+for item in [v for v in os.environ.get("AB_LIBS", "").split(",") if v]:
+    name, path = item.split("=")
+    libs[name] = _lib._load(path, _lib.SIGNATURES)
+if len(libs) == 1:
+    libs["prev"] = _lib._load(os.path.join(HERE, "gnn-bfs-rans_amd", "mignn", "libmignn_prev.so"),
+                              _lib.SIGNATURES)
 P = _lib.ptr
 st = _lib.stream()
 
@@ -106,9 +112,11 @@ else:
 for k, L in libs.items():
     run(L, Ys[k])
 torch.cuda.synchronize()
-res = {"mode": mode, "n": n, "max_diff": (Ys["cur"] - Ys["prev"]).abs().nan_to_num(0.0).max().item(),
+res = {"mode": mode, "n": n, "h": H,
+       "max_diff": {k: (Ys["cur"] - v).abs().nan_to_num(0.0).max().item() for k, v in Ys.items()},
        "nan_rows": {k: int(torch.isnan(v).any(1).sum().item()) for k, v in Ys.items()},
-       "bitwise_equal": bool(torch.equal(Ys["cur"].view(torch.int32), Ys["prev"].view(torch.int32)))}
+       "bitwise_equal": {k: bool(torch.equal(Ys["cur"].view(torch.int32), v.view(torch.int32)))
+                         for k, v in Ys.items()}}
 times = {k: [] for k in libs}
 for rnd in range(int(os.environ.get("AB_REPS", "5")) + 1):
     for k, L in libs.items():

@@ -1,4 +1,4 @@
-"""Same-box A/B of the fused output head (mignn_mlp_head, H = 128, out 7) on
+"""Same-box A/B of the fused output head (mignn_mlp_head, H = HA_H (128), out 7) on
 HA_N rows (default the headline's 10M): the product library against variant
 builds of mlp_f16x3.hip (HA_LIBS name=path,...; scripts/build_variant.sh),
 one prepared image, one output buffer for the timing, outputs compared
@@ -17,7 +17,7 @@ from mignn import _lib  # noqa: E402
 
 dev = torch.device("cuda", 0)
 n = int(os.environ.get("HA_N", "10000000"))
-H, OUT = 128, 7
+H, OUT = int(os.environ.get("HA_H", "128")), 7
 g = torch.Generator(device=dev).manual_seed(0)
 x = torch.relu(torch.randn(n, H, device=dev, generator=g))
 w = [torch.randn(H, H, device=dev, generator=g) * 0.08, torch.randn(H, H, device=dev, generator=g) * 0.08,
