@@ -69,10 +69,6 @@ using f16x4w = __attribute__((ext_vector_type(4))) _Float16;
 #ifndef MIGNN_WIN_PD
 #define MIGNN_WIN_PD 3
 #endif
-// (experiment) s_setprio(1) over the pipelined step's MFMA groups
-#ifndef MIGNN_WIN_PRIO
-#define MIGNN_WIN_PRIO 0
-#endif
 constexpr int kWinPD = MIGNN_WIN_PD;
 // Plan record of a row: 8 u16 codes (16 B), each with the neighbour's degree
 // class in its low 3 bits (the code's LDS offset is 16-B aligned: those bits
@@ -731,6 +727,12 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
     int lane = tid & 63;
     asm volatile("" : "+v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the two waves of a SIMD (w, w + NW / 2) at different priorities: both
+    // meet at the same barriers and would reach their MFMA groups and their
+    // LDS / VALU phases together; the first now runs ahead and the second
+    // fills its gaps (same-box A/B, DESIGN 3.17: H = 128 -0.75 %, H = 64
+    // -2.3 %, codes form -0.75 %)
+    if (wave < C::NW / 2) __builtin_amdgcn_s_setprio(1);
 
     const WinHdr* const hdr = reinterpret_cast<const WinHdr*>(plan);
     {
@@ -1608,7 +1610,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                 constexpr int g = decltype(G)::value;
                 if (!mf) return;
                 __builtin_amdgcn_sched_barrier(0);
-                if constexpr (MIGNN_WIN_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int t = g * TG; t < (g + 1) * TG; ++t) {
                     const int kc = t / IBW, ib = t % IBW;
@@ -1622,7 +1623,6 @@ __global__ __launch_bounds__(WCfg<H>::NT, WCfg<H>::NW / 4 * WCfg<H>::WGPC) void 
                         }
                     }
                 }
-                if constexpr (MIGNN_WIN_PRIO == 1) __builtin_amdgcn_s_setprio(0);
                 __builtin_amdgcn_sched_barrier(0);
             };
 
@@ -1939,6 +1939,12 @@ __global__ __launch_bounds__(WCfg<64>::NT, 2) void gcn_win64_kernel(
     int lane = tid & 63;
     asm volatile("" : "+v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the two waves of a SIMD (w, w + NW / 2) at different priorities: both
+    // meet at the same barriers and would reach their MFMA groups and their
+    // LDS / VALU phases together; the first now runs ahead and the second
+    // fills its gaps (same-box A/B, DESIGN 3.17: H = 128 -0.75 %, H = 64
+    // -2.3 %, codes form -0.75 %)
+    if (wave < C::NW / 2) __builtin_amdgcn_s_setprio(1);
 
     const WinHdr* const hdr = reinterpret_cast<const WinHdr*>(plan);
     {
