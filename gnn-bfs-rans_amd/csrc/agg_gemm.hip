@@ -1107,6 +1107,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void h
     asm volatile("" : "+v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 15, g = lane >> 4;
+    // the two waves of a SIMD at different priorities (the barrier per W
+    // chunk puts them in the same phase): 13.06 -> 12.55 ms at 12.6M rows
+    // (no gain in agg_gemm_kernel / the H = 128 head)
+    if (wave < AW / 2) __builtin_amdgcn_s_setprio(1);
     const int64_t ntiles = (n + BM - 1) / BM;
     const int64_t per_xcd = gridDim.x >> 3;
     const int64_t tile = static_cast<int64_t>(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
