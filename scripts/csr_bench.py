@@ -47,6 +47,9 @@ a = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv)
 b = build_csr(ei, n, _lib.CSR_ONE_SELF_LOOP, relabel=inv)
 res["csr_deterministic"] = bool(torch.equal(a.col, b.col) and torch.equal(a.ew, b.ew)
                                 and torch.equal(a.row_ptr, b.row_ptr))
+import hashlib  # noqa: E402
+res["csr_sha1"] = hashlib.sha1(a.row_ptr.cpu().numpy().tobytes() + a.col.cpu().numpy().tobytes()
+                               + a.ew.cpu().numpy().tobytes()).hexdigest()
 a.order_info = info
 L = _lib.lib()
 for H in (128, 64):
