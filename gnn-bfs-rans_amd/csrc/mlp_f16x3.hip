@@ -90,14 +90,32 @@ __device__ __forceinline__ uint32_t pair_max(uint32_t m) {
     return max(static_cast<uint32_t>(sw[0]), static_cast<uint32_t>(sw[1]));
 }
 
-// 8 floats (already scaled) -> hi / lo fp16 fragments
-__device__ __forceinline__ void split8(const float* s, f16x8& hi, f16x8& lo) {
+// 8 floats times the power of two f -> hi / lo fp16 fragments: hi = f16(a f),
+// lo = f16(a f - hi) (a f and a f - hi exact in fp32, so one rounding each,
+// as converting the scaled value and its remainder).  Both come straight from
+// the mixed-precision FMA, one instruction per half written into its half of
+// the fragment register (v_fma_mixlo / mixhi_f16, src2 an f16 half for lo):
+// 4 VALU per pair.  Left to itself the compiler SLP-packs the same
+// arithmetic into v_pk_mul_f32, v_cvt_pk_f16_f32, two v_cvt_f32_f16 and
+// v_pk_fma_f32 per pair -- more instructions, and packed fp32 ones, beside
+// the partner wave's MFMAs.
+__device__ __forceinline__ void split8(const float* a, float f, f16x8& hi, f16x8& lo) {
+    using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+    u32x4 h, l;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const _Float16 hh = static_cast<_Float16>(s[j]);
-        hi[j] = hh;
-        lo[j] = static_cast<_Float16>(s[j] - static_cast<float>(hh));
+    for (int q = 0; q < 4; ++q) {
+        uint32_t hq, lq;
+        asm("v_fma_mixlo_f16 %0, %1, %3, 0\n\t"
+            "v_fma_mixhi_f16 %0, %2, %3, 0"
+            : "=&v"(hq) : "v"(a[2 * q]), "v"(a[2 * q + 1]), "v"(f));
+        asm("v_fma_mixlo_f16 %0, %1, %3, -%4 op_sel_hi:[0,0,1]\n\t"
+            "v_fma_mixhi_f16 %0, %2, %3, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "=&v"(lq) : "v"(a[2 * q]), "v"(a[2 * q + 1]), "v"(f), "v"(hq));
+        h[q] = hq;
+        l[q] = lq;
     }
+    hi = __builtin_bit_cast(f16x8, h);
+    lo = __builtin_bit_cast(f16x8, l);
 }
 
 // raw bias of one accumulator block, in register order (16 floats at bl)
@@ -142,12 +160,20 @@ __device__ __forceinline__ int chain(f32x16* a, int pq, f16x8* oh, f16x8* ol,
         for (int s = 0; s < 2; ++s) {
             float v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = a[nb][8 * s + j] * f;
-            split8(v, oh[2 * nb + s], ol[2 * nb + s]);
+            for (int j = 0; j < 8; ++j) v[j] = a[nb][8 * s + j];
+            split8(v, f, oh[2 * nb + s], ol[2 * nb + s]);
             // a[nb] consumed: start the next layer's raw bias load into it
             if (s == 1 && nb < NBNEXT) a[nb] = ldbias(bnext + nb * 32);
         }
     return pn;
+}
+
+// a layer's LDS base + lane offset, opaque: its fragment reads then carry
+// their distance from it in the 16-bit ds_read offset field (past 64 KiB the
+// compiler otherwise adds the constant to the lane offset once per read)
+__device__ __forceinline__ uint32_t lds_base(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
 }
 
 // One layer: acc[nb] = acc[nb] sc + W[nb] . act (acc[nb] holds the raw
@@ -295,21 +321,17 @@ __global__ __launch_bounds__(NWV * 64) void mlp_head_kernel(
         f32x16 acc[C::NB1];
 #pragma unroll
         for (int nb = 0; nb < C::NB1; ++nb) acc[nb] = ldbias(bimg + (C::BOFF1 >> 2) + nb * 32);
-        uint32_t m = 0;
+        float fm = 0.f;
 #pragma unroll
         for (int t = 0; t < C::KT1; ++t)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(xv[t][j])));
-        int p = head_scale_exp(pair_max(m));
+            for (int j = 0; j < 8; ++j) fm = __builtin_fmaxf(fm, fabsf(xv[t][j]));
+        int p = head_scale_exp(pair_max(__float_as_uint(fm)));
         f16x8 ah[C::KT1], al[C::KT1];
         {
             const float sc = exp2_int(p);
 #pragma unroll
-            for (int t = 0; t < C::KT1; ++t) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) xv[t][j] *= sc;
-                split8(xv[t], ah[t], al[t]);
-            }
+            for (int t = 0; t < C::KT1; ++t) split8(xv[t], sc, ah[t], al[t]);
         }
         // ---- L1 (H -> H) + ReLU
         if constexpr ((DIAG & 2) == 0)
@@ -317,7 +339,8 @@ __global__ __launch_bounds__(NWV * 64) void mlp_head_kernel(
         p = chain<C::NB1, C::NB2>(acc, p + q1, ah, al, bimg + (C::BOFF2 >> 2));
         // ---- L2 (H -> H) + ReLU
         if constexpr ((DIAG & 2) == 0)
-            layer_mfma<C::NB2, C::KT2, (DIAG & 4) != 0>(acc, exp2_int(p + q2), lds + C::W1_BYTES, loff, ah, al);
+            layer_mfma<C::NB2, C::KT2, (DIAG & 4) != 0>(acc, exp2_int(p + q2), lds,
+                                                         lds_base(C::W1_BYTES + loff), ah, al);
         p = chain<C::NB2, C::NB3>(acc, p + q2, ah, al, bimg + (C::BOFF3 >> 2));
         // ---- L3 (H -> H/2) + ReLU.  Issued ahead of its MFMAs: W4 fragments,
         // L4's bias and the NEXT block's x rows (registers free from here on)
@@ -332,8 +355,8 @@ __global__ __launch_bounds__(NWV * 64) void mlp_head_kernel(
         const int64_t row = blk * 32 + r32;
         if constexpr (PF) load_x(blk + stride);
         if constexpr ((DIAG & 2) == 0)
-            layer_mfma<C::NB3, C::KT3, (DIAG & 4) != 0>(acc, exp2_int(p + q3),
-                                                         lds + C::W1_BYTES + C::W2_BYTES, loff, ah, al);
+            layer_mfma<C::NB3, C::KT3, (DIAG & 4) != 0>(acc, exp2_int(p + q3), lds,
+                                                         lds_base(C::W1_BYTES + C::W2_BYTES + loff), ah, al);
         p = chain<C::NB3, 0>(acc, p + q3, ah, al, nullptr);
         // ---- L4 (H/2 -> out), no activation
         o *= exp2_int(p + q4);
