@@ -141,6 +141,25 @@ __device__ __forceinline__ float4 fma4(float s, float4 x, float4 acc) {
     return acc;
 }
 
+// Split-fp16 pair: (a0, a1) times the power of two f -> hi = f16(a f),
+// lo = f16(a f - hi) packed two halves a dword (element 0 in the low half).
+// a f and a f - hi are exact in fp32, so each half is one rounding of the
+// same value as converting the scaled product and its remainder.  The
+// mixed-precision FMA writes each half straight from the fp32 operands
+// (v_fma_mixlo / mixhi_f16, hi's half as an f16 source for lo): 4 VALU per
+// pair, where the compiler's own form of the same arithmetic is SLP-packed
+// v_pk_mul_f32 + v_cvt_pk_f16_f32 + 2 v_cvt_f32_f16 + v_pk_fma_f32 + a
+// second v_cvt_pk_f16_f32.
+__device__ __forceinline__ void split_pair(float a0, float a1, float f, uint32_t& hi,
+                                           uint32_t& lo) {
+    asm("v_fma_mixlo_f16 %0, %1, %3, 0\n\t"
+        "v_fma_mixhi_f16 %0, %2, %3, 0"
+        : "=&v"(hi) : "v"(a0), "v"(a1), "v"(f));
+    asm("v_fma_mixlo_f16 %0, %1, %3, -%4 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %2, %3, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(lo) : "v"(a0), "v"(a1), "v"(f), "v"(hi));
+}
+
 // Reference epilogue order (gnn_model.py:184-191 with the conv bias first):
 //   v = acc + bias; v = residual + v; v = v*scale + shift; relu.
 // ReLU in one v_maximum3_f32: NaN-propagating, like torch.relu (-0 -> +0)

@@ -90,27 +90,15 @@ __device__ __forceinline__ uint32_t pair_max(uint32_t m) {
     return max(static_cast<uint32_t>(sw[0]), static_cast<uint32_t>(sw[1]));
 }
 
-// 8 floats times the power of two f -> hi / lo fp16 fragments: hi = f16(a f),
-// lo = f16(a f - hi) (a f and a f - hi exact in fp32, so one rounding each,
-// as converting the scaled value and its remainder).  Both come straight from
-// the mixed-precision FMA, one instruction per half written into its half of
-// the fragment register (v_fma_mixlo / mixhi_f16, src2 an f16 half for lo):
-// 4 VALU per pair.  Left to itself the compiler SLP-packs the same
-// arithmetic into v_pk_mul_f32, v_cvt_pk_f16_f32, two v_cvt_f32_f16 and
-// v_pk_fma_f32 per pair -- more instructions, and packed fp32 ones, beside
-// the partner wave's MFMAs.
+// 8 floats times the power of two f -> hi / lo fp16 fragments (split_pair:
+// mixed-precision FMAs, no packed fp32)
 __device__ __forceinline__ void split8(const float* a, float f, f16x8& hi, f16x8& lo) {
     using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
     u32x4 h, l;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         uint32_t hq, lq;
-        asm("v_fma_mixlo_f16 %0, %1, %3, 0\n\t"
-            "v_fma_mixhi_f16 %0, %2, %3, 0"
-            : "=&v"(hq) : "v"(a[2 * q]), "v"(a[2 * q + 1]), "v"(f));
-        asm("v_fma_mixlo_f16 %0, %1, %3, -%4 op_sel_hi:[0,0,1]\n\t"
-            "v_fma_mixhi_f16 %0, %2, %3, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-            : "=&v"(lq) : "v"(a[2 * q]), "v"(a[2 * q + 1]), "v"(f), "v"(hq));
+        split_pair(a[2 * q], a[2 * q + 1], f, hq, lq);
         h[q] = hq;
         l[q] = lq;
     }
