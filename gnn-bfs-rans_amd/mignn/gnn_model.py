@@ -173,8 +173,10 @@ class Csr:
         schedule -- the column schedule when the CSR is in the column order
         and the plan's rows start at row 0 (a shard's interior range: the
         plane count per column taken from the CSR, mignn_gcn_win_plan) --
-        and a 48-B record per row), built on first use and kept with the CSR
-        (it copies the ew weights)."""
+        and a 16-B record per row: neighbour codes and degree classes, the
+        weights rebuilt in LDS from the header's class table -- a row whose
+        ew are not exactly those products takes the CSR path), built on first
+        use and kept with the CSR (it reads ew once, at build time)."""
         key = ("win", h, row_begin, row_end, torch.cuda.current_device())
         plan = self.plans.get(key)
         if plan is None:
