@@ -76,8 +76,19 @@ __device__ __forceinline__ bool wave_run(uint32_t key, bool active, int lane, in
     return head;
 }
 
+// Range mode (RangeIds.inv != nullptr, mignn_csr_build_range): edge ids are
+// GLOBAL ids of a node-range shard [lo, hi) of `ng` nodes, mapped on the fly
+// to the shard's local ids as mignn_range_relabel does (owned -> inv[id - lo],
+// a ghost -> n_own - 1 + ghost_rank[id]); valid = destination owned, source
+// in [0, ng).  N is then the local node count (n_own + ghosts).
+struct RangeIds {
+    const int64_t* inv;
+    const int64_t* ghost_rank;
+    int64_t lo, hi, ng;
+};
+
 __global__ void csr_count_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t N, int mode,
-                                 int transpose, const int32_t* __restrict__ relabel,
+                                 int transpose, const int32_t* __restrict__ relabel, RangeIds rg,
                                  uint32_t* __restrict__ keys, int32_t* __restrict__ vals,
                                  int32_t* __restrict__ deg,
                                  unsigned long long* __restrict__ counters) {
@@ -110,9 +121,19 @@ __global__ void csr_count_kernel(const int64_t* __restrict__ ei, int64_t E, int6
         int64_t sn[kU], dn[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            valid[u] = in[u] & (s[u] >= 0) & (s[u] < N) & (d[u] >= 0) & (d[u] < N);
             sn[u] = s[u];
             dn[u] = d[u];
+            if (rg.inv != nullptr) {                // a shard: global ids -> local ids
+                valid[u] = in[u] & (s[u] >= 0) & (s[u] < rg.ng) & (d[u] >= rg.lo) & (d[u] < rg.hi);
+                if (valid[u]) {
+                    const int64_t n_own = rg.hi - rg.lo;
+                    sn[u] = (s[u] >= rg.lo && s[u] < rg.hi) ? rg.inv[s[u] - rg.lo]
+                                                            : n_own - 1 + rg.ghost_rank[s[u]];
+                    dn[u] = rg.inv[d[u] - rg.lo];
+                }
+                continue;
+            }
+            valid[u] = in[u] & (s[u] >= 0) & (s[u] < N) & (d[u] >= 0) & (d[u] < N);
             if (relabel != nullptr && valid[u]) {   // node ids in the internal (relabelled) order
                 sn[u] = relabel[s[u]];
                 dn[u] = relabel[d[u]];
@@ -519,10 +540,39 @@ extern "C" int mignn_csr_build_relabeled(const int64_t* edge_index, int64_t E, i
                                scratch, scratch_bytes, stream_);
 }
 
+static int csr_build_impl(const int64_t* edge_index, int64_t E, int64_t N, int mode,
+                          const int32_t* relabel, RangeIds rg, int32_t* row_ptr, int32_t* col,
+                          float* dinv, float* ew, int64_t* info, void* scratch,
+                          size_t scratch_bytes, void* stream_);
+
 extern "C" int mignn_csr_build_gcn(const int64_t* edge_index, int64_t E, int64_t N, int mode,
                                    const int32_t* relabel, int32_t* row_ptr, int32_t* col,
                                    float* dinv, float* ew, int64_t* info, void* scratch,
                                    size_t scratch_bytes, void* stream_) {
+    return csr_build_impl(edge_index, E, N, mode, relabel, RangeIds{nullptr, nullptr, 0, 0, 0},
+                          row_ptr, col, dinv, ew, info, scratch, scratch_bytes, stream_);
+}
+
+extern "C" int mignn_csr_build_range(const int64_t* edge_index, int64_t E, int64_t num_nodes,
+                                     int64_t lo, int64_t hi, const int64_t* inv,
+                                     const int64_t* ghost_rank, int64_t n_local, int mode,
+                                     int32_t* row_ptr, int32_t* col, float* dinv, float* ew,
+                                     int64_t* info, void* scratch, size_t scratch_bytes,
+                                     void* stream_) {
+    MIGNN_REQUIRE(lo >= 0 && hi >= lo && num_nodes >= hi && n_local >= hi - lo,
+                  "csr_build_range: bad range [%lld, %lld) of %lld, n_local %lld", (long long)lo,
+                  (long long)hi, (long long)num_nodes, (long long)n_local);
+    MIGNN_REQUIRE(E == 0 || (inv && ghost_rank), "csr_build_range: null pointer");
+    MIGNN_REQUIRE(!(mode & MIGNN_CSR_TRANSPOSE), "csr_build_range: no transposed mode");
+    return csr_build_impl(edge_index, E, n_local, mode, nullptr,
+                          RangeIds{E ? inv : nullptr, ghost_rank, lo, hi, num_nodes}, row_ptr, col,
+                          dinv, ew, info, scratch, scratch_bytes, stream_);
+}
+
+static int csr_build_impl(const int64_t* edge_index, int64_t E, int64_t N, int mode,
+                          const int32_t* relabel, RangeIds rg, int32_t* row_ptr, int32_t* col,
+                          float* dinv, float* ew, int64_t* info, void* scratch,
+                          size_t scratch_bytes, void* stream_) {
     MIGNN_REQUIRE(N >= 0 && E >= 0, "csr_build: negative sizes (E=%lld N=%lld)", (long long)E,
                   (long long)N);
     MIGNN_REQUIRE(E + N < (int64_t(1) << 31) - 1, "csr_build: E+N exceeds int32 CSR range");
@@ -554,7 +604,8 @@ extern "C" int mignn_csr_build_gcn(const int64_t* edge_index, int64_t E, int64_t
     MIGNN_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), st));
     if (E > 0) {
         hipLaunchKernelGGL(csr_count_kernel, dim3(grid_for(E, kBlock, 8192)), dim3(kBlock), 0, st,
-                           edge_index, E, N, mode, transpose, relabel, keys, vals, deg, counters);
+                           edge_index, E, N, mode, transpose, relabel, rg, keys, vals, deg,
+                           counters);
         if ((rc = launch_status("csr_count_kernel"))) return rc;
     }
     size_t temp = L.temp_bytes;

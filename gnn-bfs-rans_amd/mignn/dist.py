@@ -171,20 +171,22 @@ class RangeLayout:
         self.inv = torch.empty_like(perm)
         self.inv[perm] = torch.arange(self.n_own, device=dev)
         # local edge list: owned -> local position, ghost -> n_own + ghost
-        # index (the ghost's rank among the marked ids: the prefix sum above)
+        # index (the ghost's rank among the marked ids: the prefix sum above).
+        # On the device it is not written here: build_csr maps the global ids
+        # inside the CSR build (mignn_csr_build_range); `edge_index`
+        # materialises it on first use (mignn_range_relabel)
+        self._ei_global = self._ghost_rank = None
+        self._edge_index: Optional[torch.Tensor] = None
         if dev.type == "cuda" and E > 0:
-            from . import _lib
-            ei64 = edge_index if (edge_index.dtype == torch.int64 and edge_index.is_contiguous()) \
+            self._ei_global = edge_index if (edge_index.dtype == torch.int64
+                                             and edge_index.is_contiguous()) \
                 else torch.stack([src, dst])
-            self.edge_index = torch.empty((2, E), dtype=torch.int64, device=dev)
-            _lib.check(_lib.lib().mignn_range_relabel(
-                _lib.ptr(ei64), E, lo, hi, _lib.ptr(self.inv), _lib.ptr(csum), self.n_own,
-                _lib.ptr(self.edge_index), _lib.stream(dev)), "mignn_range_relabel")
+            self._ghost_rank = csum
         else:
             own_src = (src >= lo) & (src < hi)
             lsrc = torch.where(own_src, self.inv[(src - lo).clamp(0, max(self.n_own - 1, 0))],
                                self.n_own - 1 + csum[src.clamp(0, N)])
-            self.edge_index = torch.stack([lsrc, self.inv[dst - lo]])
+            self._edge_index = torch.stack([lsrc, self.inv[dst - lo]])
         # send lists: every peer's ghost requests, answered with my local rows
         req = {q: ghost[self.ghost_ptr[q]:self.ghost_ptr[q + 1]]
                for q in range(self.world) if q != rank and counts[q] > 0}
@@ -192,6 +194,32 @@ class RangeLayout:
         self.send_idx: Dict[int, torch.Tensor] = {
             q: self.inv[ids.to(dev).long() - lo].to(torch.int32) for q, ids in got.items()
             if ids.numel() > 0}
+
+    @property
+    def edge_index(self) -> torch.Tensor:
+        """The rank-local edge list [2, E_r] (int64): a source in [lo, hi) ->
+        its local position, a ghost -> n_own + its ghost index; a destination
+        -> its local position."""
+        if self._edge_index is None:
+            from . import _lib
+            ei = self._ei_global
+            E = int(ei.shape[1])
+            out = torch.empty((2, E), dtype=torch.int64, device=ei.device)
+            _lib.check(_lib.lib().mignn_range_relabel(
+                _lib.ptr(ei), E, self.lo, self.hi, _lib.ptr(self.inv), _lib.ptr(self._ghost_rank),
+                self.n_own, _lib.ptr(out), _lib.stream(ei.device)), "mignn_range_relabel")
+            self._edge_index = out
+        return self._edge_index
+
+    def build_csr(self, mode: int):
+        """This rank's local CSR (mignn.gnn_model.build_csr of `edge_index`,
+        n_total nodes); on the device straight from the global-id in-edges
+        (mignn_csr_build_range: the local list is never written)."""
+        from .gnn_model import build_csr, build_csr_range
+        if self._edge_index is None and self._ei_global is not None:
+            return build_csr_range(self._ei_global, self.bounds[-1], self.lo, self.hi, self.inv,
+                                   self._ghost_rank, self.n_total, mode)
+        return build_csr(self.edge_index, self.n_total, mode)
 
     def ghost_slice(self, q: int) -> slice:
         return slice(self.n_own + self.ghost_ptr[q], self.n_own + self.ghost_ptr[q + 1])
@@ -490,11 +518,10 @@ class FlowGNNShard(Shard):
         from edge_index when its CSR cache is off (the bench's per-step graph
         setup)."""
         from ._lib import CSR_ONE_SELF_LOOP, CSR_VERBATIM
-        from .gnn_model import build_csr
         m = self.model
         mode = CSR_ONE_SELF_LOOP if m.layer_type in ("GCN", "GAT") else CSR_VERBATIM
         for sh in shards:
-            sh.csr = build_csr(sh.layout.edge_index, sh.layout.n_total, mode)
+            sh.csr = sh.layout.build_csr(mode)
             # (the column order: the window kernel's route; its plans cover
             # row ranges -- interior, boundary -- so they take the contiguous
             # chunk schedule, the info only marks the order)

@@ -264,6 +264,37 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int, mode: int,
     return Csr(row_ptr, col, dinv, info, N, E, ei, ew=ew)
 
 
+def build_csr_range(edge_index: torch.Tensor, num_nodes: int, lo: int, hi: int,
+                    inv: torch.Tensor, ghost_rank: torch.Tensor, n_local: int, mode: int) -> Csr:
+    """A node-range shard's CSR straight from its global-id in-edges
+    (mignn_csr_build_range): ids mapped to the shard's local ids inside the
+    build as mignn_range_relabel maps them (`inv` int64 [hi - lo],
+    `ghost_rank` int64 [num_nodes + 1], mignn.dist.RangeLayout's) -- the same
+    CSR as build_csr(<the relabelled list>, n_local, mode), bit for bit."""
+    dev = edge_index.device
+    ei = edge_index
+    if ei.dtype != torch.int64 or not ei.is_contiguous():
+        ei = ei.to(torch.int64).contiguous()
+    E = int(ei.shape[1])
+    N = int(n_local)
+    row_ptr = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(max(E + N, 1), dtype=torch.int32, device=dev)
+    dinv = torch.empty(max(N, 1), dtype=torch.float32, device=dev) if mode == CSR_ONE_SELF_LOOP else None
+    info = torch.zeros(4, dtype=torch.int64, device=dev)
+    L = _lib.lib()
+    nbytes = L.mignn_csr_scratch_bytes(E, N)
+    if nbytes == 0:
+        raise _lib.MignnError("csr scratch query failed: " + _lib.last_error())
+    scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    ew = torch.empty_like(col, dtype=torch.float32) if mode == CSR_ONE_SELF_LOOP else None
+    _lib.check(L.mignn_csr_build_range(_lib.ptr(ei), E, int(num_nodes), int(lo), int(hi),
+                                       _lib.ptr(inv), _lib.ptr(ghost_rank), N, mode,
+                                       _lib.ptr(row_ptr), _lib.ptr(col), _lib.ptr(dinv),
+                                       _lib.ptr(ew), _lib.ptr(info), _lib.ptr(scratch), nbytes,
+                                       _lib.stream(dev)), "mignn_csr_build_range")
+    return Csr(row_ptr, col, dinv, info, N, E, None, ew=ew)
+
+
 class _CsrCache:
     """Keyed by (edge_index storage, version, shape, N, mode, device) -- plus
     the positions' storage / version when a locality order is requested;

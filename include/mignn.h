@@ -89,6 +89,19 @@ int mignn_csr_build_gcn(const int64_t* edge_index, int64_t num_edges, int64_t nu
                         const int32_t* relabel, int32_t* row_ptr, int32_t* col, float* dinv,
                         float* ew, int64_t* info, void* scratch, size_t scratch_bytes,
                         void* stream);
+/* As mignn_csr_build_gcn for one node-range shard (mignn.dist.RangeLayout):
+ * edge_index holds GLOBAL ids (destinations in [lo, hi) of num_nodes), mapped
+ * in the build's first pass to the shard's local ids exactly as
+ * mignn_range_relabel maps them (inv, ghost_rank as there) -- the CSR of the
+ * relabelled list without writing that list.  n_local = n_own + ghosts (the
+ * CSR's node count); scratch as mignn_csr_scratch_bytes(num_edges, n_local).
+ * No transposed mode.  (Replaces mignn_range_relabel + mignn_csr_build_gcn on
+ * the shard route; the reference has no sharded path) */
+int mignn_csr_build_range(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                          int64_t lo, int64_t hi, const int64_t* inv, const int64_t* ghost_rank,
+                          int64_t n_local, int mode, int32_t* row_ptr, int32_t* col, float* dinv,
+                          float* ew, int64_t* info, void* scratch, size_t scratch_bytes,
+                          void* stream);
 
 /* Locality order of the nodes for the internal activation layout (no
  * reference counterpart: the forward's results are the same up to fp32

@@ -193,6 +193,36 @@ def test_range_layout_device_matches_host(P):
             assert torch.equal(lh.send_idx[q], ld.send_idx[q].cpu())
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("P", [2, 3])
+def test_range_csr_matches_relabelled_list(P, mode):
+    """A shard's CSR built straight from its global-id in-edges
+    (RangeLayout.build_csr -> mignn_csr_build_range, the ids mapped inside the
+    build) equals build_csr of the materialised local list
+    (mignn_range_relabel) bit for bit -- row_ptr, col, dinv, gcn_norm ew, the
+    kept / invalid counts -- with duplicate edges and self-loops, in both CSR
+    modes (VERBATIM, ONE_SELF_LOOP)."""
+    from mignn.gnn_model import build_csr
+    g = torch.Generator().manual_seed(10 + P)
+    n = 3000
+    ei = torch.randint(0, n, (2, 40000), generator=g)
+    ei = torch.cat([ei, torch.stack([torch.arange(n), torch.arange(n)]), ei[:, :500]], 1)
+    b = range_bounds(n, P)
+    edges = [ei[:, (ei[1] >= b[r]) & (ei[1] < b[r + 1])].to(DEV) for r in range(P)]
+    for lay in build_local_layouts(edges, b):
+        assert lay._edge_index is None            # the device layout writes no local list
+        c1 = lay.build_csr(mode)
+        c2 = build_csr(lay.edge_index, lay.n_total, mode)
+        torch.cuda.synchronize()
+        assert torch.equal(c1.row_ptr, c2.row_ptr)
+        nnz = int(c2.row_ptr[-1])
+        assert torch.equal(c1.col[:nnz], c2.col[:nnz])
+        assert torch.equal(c1.info, c2.info)
+        if mode == 1:
+            assert torch.equal(c1.dinv, c2.dinv)
+            assert torch.equal(c1.ew[:nnz], c2.ew[:nnz])
+
+
 @pytest.mark.parametrize("shuffle", [None, 2])
 @pytest.mark.parametrize("P", [2, 4])
 @pytest.mark.parametrize("H", [64, 128])
