@@ -469,6 +469,26 @@ __global__ void range_mark_kernel(const int64_t* __restrict__ ei, int64_t E, int
     }
 }
 
+// a node-range shard's local order (mignn.dist.RangeLayout): interior rows
+// first, boundary rows last, each in the base order -- a stable partition of
+// base by the boundary flag, from ci = the inclusive prefix count of interior
+// rows along base: position p (row b = base[p]) goes to ci[p] - 1 when
+// interior, n_int + (p + 1 - ci[p]) - 1 when boundary; perm[dest] = b,
+// inv[b] = dest.
+__global__ void range_partition_kernel(const int64_t* __restrict__ base,
+                                       const uint8_t* __restrict__ boundary,
+                                       const int32_t* __restrict__ ci, int64_t n_own, int64_t n_int,
+                                       int64_t* __restrict__ perm, int64_t* __restrict__ inv) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n_own;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = base[p];
+        const int64_t c = ci[p];
+        const int64_t dest = boundary[b] ? n_int + (p + 1 - c) - 1 : c - 1;
+        perm[dest] = b;
+        inv[b] = dest;
+    }
+}
+
 // a node-range shard's local edge list (mignn.dist.RangeLayout): source ids
 // in [lo, hi) -> the owned row's local position inv[id - lo], others (ghosts)
 // -> n_own + the ghost's rank among the ghost ids (ghost_rank[id] - 1: the
@@ -643,6 +663,17 @@ extern "C" int mignn_range_mark(const int64_t* edge_index, int64_t E, int64_t lo
     hipLaunchKernelGGL(range_mark_kernel, dim3(grid_for(E, kBlock, 8192)), dim3(kBlock), 0,
                        as_stream(stream), edge_index, E, lo, hi, N, ghost_mark, boundary_mark, bad);
     return launch_status("range_mark_kernel");
+}
+
+extern "C" int mignn_range_partition(const int64_t* base, const uint8_t* boundary,
+                                     const int32_t* ci, int64_t n_own, int64_t n_int,
+                                     int64_t* perm, int64_t* inv, void* stream) {
+    MIGNN_REQUIRE(n_own >= 0 && n_int >= 0 && n_int <= n_own, "range_partition: bad sizes");
+    if (n_own == 0) return MIGNN_OK;
+    MIGNN_REQUIRE(base && boundary && ci && perm && inv, "range_partition: null pointer");
+    hipLaunchKernelGGL(range_partition_kernel, dim3(grid_for(n_own, kBlock, 65536)), dim3(kBlock), 0,
+                       as_stream(stream), base, boundary, ci, n_own, n_int, perm, inv);
+    return launch_status("range_partition_kernel");
 }
 
 extern "C" int mignn_range_relabel(const int64_t* edge_index, int64_t E, int64_t lo, int64_t hi,

@@ -100,6 +100,7 @@ SIGNATURES = {
                                         c_int, _P, c_int64, _P]),
     "mignn_range_mark": (c_int, [_P, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P]),
     "mignn_range_relabel": (c_int, [_P, c_int64, c_int64, c_int64, _P, _P, c_int64, _P, _P]),
+    "mignn_range_partition": (c_int, [_P, _P, _P, c_int64, c_int64, _P, _P, _P]),
     "mignn_csr_build_range": (c_int, [_P, c_int64, c_int64, c_int64, c_int64, _P, _P, c_int64, c_int,
                                       _P, _P, _P, _P, _P, _P, c_size_t, _P]),
     "mignn_gcn_layer0_codes": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_int64, c_int64, _P,

@@ -162,14 +162,22 @@ class RangeLayout:
         # interior first, boundary last, each in the base order: a stable
         # partition by prefix sums (a stable sort of the 0/1 keys cost 0.7 ms)
         bnd = boundary[base]
-        ci = torch.cumsum((~bnd).to(torch.int32), 0)
-        cb = torch.cumsum(bnd.to(torch.int32), 0)
-        dest = torch.where(bnd, self.n_int + cb - 1, ci - 1).long()
+        ci = torch.cumsum(~bnd, 0, dtype=torch.int32)
         perm = torch.empty_like(base)
-        perm[dest] = base                                          # local position -> owned offset
+        self.inv = torch.empty_like(base)
+        if dev.type == "cuda" and self.n_own > 0:
+            # (one pass: destination, perm and inv scatters -- mignn_range_partition)
+            from . import _lib
+            base = base.contiguous()
+            _lib.check(_lib.lib().mignn_range_partition(
+                _lib.ptr(base), _lib.ptr(boundary.contiguous()), _lib.ptr(ci), self.n_own, self.n_int,
+                _lib.ptr(perm), _lib.ptr(self.inv), _lib.stream(dev)), "mignn_range_partition")
+        else:
+            cb = torch.arange(1, self.n_own + 1, device=dev, dtype=torch.int32) - ci
+            dest = torch.where(bnd, self.n_int + cb - 1, ci - 1).long()
+            perm[dest] = base                                      # local position -> owned offset
+            self.inv[perm] = torch.arange(self.n_own, device=dev)
         self.perm = perm
-        self.inv = torch.empty_like(perm)
-        self.inv[perm] = torch.arange(self.n_own, device=dev)
         # local edge list: owned -> local position, ghost -> n_own + ghost
         # index (the ghost's rank among the marked ids: the prefix sum above).
         # On the device it is not written here: build_csr maps the global ids

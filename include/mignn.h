@@ -690,6 +690,14 @@ int mignn_range_mark(const int64_t* edge_index, int64_t E, int64_t lo, int64_t h
 int mignn_range_relabel(const int64_t* edge_index, int64_t E, int64_t lo, int64_t hi,
                         const int64_t* inv, const int64_t* ghost_rank, int64_t n_own,
                         int64_t* out, void* stream);
+/* The shard's local order: a stable partition of base [n_own] (a permutation
+ * of the owned offsets) by boundary[offset] (0/1 bytes) -- interior rows
+ * first, then boundary rows, each in base order.  ci [n_own] = the inclusive
+ * prefix count of interior rows along base, n_int = their total.
+ * perm[local position] = owned offset, inv = its inverse. */
+int mignn_range_partition(const int64_t* base, const uint8_t* boundary, const int32_t* ci,
+                          int64_t n_own, int64_t n_int, int64_t* perm, int64_t* inv,
+                          void* stream);
 /* Periodic nx*ny*nz hex grid, k-slab [z_begin, z_begin+z_count): writes
  * edge_index [2, 6*n] (src = neighbour, dst = node; global ids) and
  * x [n, 3] = cell centres in [0,1]^3.  n = nx*ny*z_count. */
