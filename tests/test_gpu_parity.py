@@ -110,6 +110,32 @@ def _check_gcn_weights(csr, name):
     np.testing.assert_allclose(ew.cpu().numpy(), want, rtol=1e-6, err_msg=name)
 
 
+@pytest.mark.parametrize("rb,re", [(0, 5000), (37, 4100), (1000, 1001), (64, 128)])
+def test_gcn_norm_row_ranges(rb, re):
+    """mignn_gcn_norm over rows [rb, re) of a CSR with empty rows, long rows
+    and ragged chunk ends: every entry of those rows = dinv[col] * dinv[row]
+    (fp32 product, bitwise), every other entry untouched."""
+    g = np.random.default_rng(rb + 7 * re)
+    n = 5000
+    deg = g.integers(0, 12, n)
+    deg[g.random(n) < 0.2] = 0
+    deg[g.integers(0, n, 5)] = 200
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    col = g.integers(0, n, rp[-1]).astype(np.int32)
+    dinv = g.random(n).astype(np.float32) + np.float32(0.5)
+    d = torch.device("cuda", 0)
+    t_rp, t_col, t_dinv = (torch.from_numpy(a).to(d) for a in (rp, col, dinv))
+    ew = torch.full((max(int(rp[-1]), 1),), float("nan"), device=d)
+    _lib.check(_lib.lib().mignn_gcn_norm(_lib.ptr(t_rp), _lib.ptr(t_col), _lib.ptr(t_dinv), rb, re,
+                                         _lib.ptr(ew), _lib.stream(d)), "mignn_gcn_norm")
+    got = ew.cpu().numpy()[: rp[-1]]
+    rows = np.repeat(np.arange(n), deg)
+    inside = (rows >= rb) & (rows < re)
+    want = dinv[col] * dinv[rows]
+    assert np.array_equal(got[inside].view(np.uint32), want[inside].view(np.uint32))
+    assert np.isnan(got[~inside]).all()
+
+
 @pytest.mark.parametrize("mode", [_lib.CSR_VERBATIM, _lib.CSR_ONE_SELF_LOOP])
 def test_csr_build_relabeled_and_transposed(mode):
     """relabel (a permutation of the node ids) and the transposed build equal
