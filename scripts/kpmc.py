@@ -2,7 +2,7 @@
 (250x200x200, locality order, H = KP_H), each launched KP_REPS times, nothing
 else -- run under `rocprofv3 --pmc ...` (scripts/gpu_kpmc.sh).  KP_KINDS:
 pc, ring, win, winagg, wincodes (the codes form, MODE 64), windiag, gin, tf,
-gat."""
+gat, head (the fused output head at H = KP_H, out 7)."""
 import os
 import sys
 
@@ -77,7 +77,18 @@ if "gat" in kinds:
     GIMG = f16x3_image(WCAT)
     GSCR = torch.empty(max(L.mignn_gat_layer_scratch_bytes(n, n, H, 4), 1), dtype=torch.uint8,
                        device=dev)
+if "head" in kinds:
+    HW = [torch.randn(H, H, device=dev, generator=g) * 0.08, torch.randn(H, H, device=dev, generator=g) * 0.08,
+          torch.randn(H // 2, H, device=dev, generator=g) * 0.08, torch.randn(7, H // 2, device=dev, generator=g) * 0.1]
+    HB = [torch.randn(w.shape[0], device=dev, generator=g) * 0.05 for w in HW]
+    HIMG = torch.empty(L.mignn_mlp_head_prep_bytes(H), dtype=torch.uint8, device=dev)
+    _lib.check(L.mignn_mlp_head_prep(P(HW[0]), P(HB[0]), P(HW[1]), P(HB[1]), P(HW[2]), P(HB[2]), P(HW[3]),
+                                     P(HB[3]), H, 7, P(HIMG), HIMG.numel(), st), "head prep")
+    XR = torch.relu(X)
+    HOUT = torch.empty(n, 7, device=dev)
 for _ in range(reps):
+    if "head" in kinds:
+        _lib.check(L.mignn_mlp_head(P(XR), H, n, H, P(HIMG), 7, P(HOUT), 7, None, st), "head")
     if "gin" in kinds:
         _lib.check(L.mignn_gin_layer_fused(P(csr.row_ptr), P(csr.col), P(X), H, 0, n, H, 0.0,
                                            P(GI1), P(b), P(GI2), P(b), P(sc), P(sh), 15, P(Y), H,

@@ -14,7 +14,7 @@ for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), re
         k = row.get("Kernel_Name", "")
         import re
         m = re.search(r"(gcn_\w+_kernel|agg_gemm_kernel|tf_fused_kernel|gat_fused_kernel|"
-                      r"gemm_f16x3_kernel|gin0_fused_kernel)(<[^>]*>)?", k)
+                      r"gemm_f16x3_kernel|gin0_fused_kernel|mlp_head_kernel)(<[^>]*>)?", k)
         if not m:
             continue
         short = m.group(1) + (m.group(2) or "")
